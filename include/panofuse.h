@@ -1,0 +1,140 @@
+/*
+ * panofuse.h -- C-ABI of the MI355X (gfx950) panorama-depth fusion library (libpanofuse.so).
+ *
+ * Drop-in for the reference's DepthNamespace hot path (Depth.h:286-307 and the OpenGL E->P
+ * render of Main.cpp:242-326).  Plain pointers and sizes only; every data pointer is a DEVICE
+ * pointer (hipMalloc'd memory or a torch tensor's data_ptr()) owned by the caller, and every
+ * call is stream-ordered on the context's stream.  Calls return PF_OK (0) or a negative PF_E*
+ * code; pf_last_error() gives the message.  A context is bound to one device and one stream and
+ * is not thread-safe: use one context per host thread per device.
+ *
+ * Batched layout in HBM (row-major, row 0 = zenith 0):
+ *   emap  [batch][eh][ew][ec]           fp32 baseline equirectangular depth in [0,1]
+ *   tiles [batch][sum_i th_i*tw_i*tc]   fp32 perspective tiles, tile i at offset sum_{j<i}
+ *   out   [batch][out_h][out_w]         u16 fused panorama
+ *   coeffs[batch][ntiles][4]            fp32 {a,b,c,d} of y = a x^3 + b x^2 + c x + d
+ */
+#ifndef PANOFUSE_H
+#define PANOFUSE_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define PF_OK 0
+#define PF_EINVAL (-1)     /* bad argument, shape or layout */
+#define PF_ENOMEM (-2)     /* device allocation failed */
+#define PF_EHIP (-3)       /* HIP runtime error */
+#define PF_ESTATE (-4)     /* call order (e.g. no tiles set) */
+#define PF_EDEGENERATE (-5) /* a tile box with x0 == x1 (the reference loops forever there) */
+
+typedef struct pf_ctx pf_ctx;
+
+/* {azimuth_left, azimuth_right, zenith_top, zenith_down} in radians.  As a viewing window
+ * this is PerspectiveMap::SetWindow's argument list (Depth.cpp:120); as a valid range it is
+ * PerspectiveMap::ranges (Depth.h:82). */
+typedef struct pf_window {
+    float az_left, az_right, zen_top, zen_down;
+} pf_window;
+
+/* Synthetic stand-in for the external depth net (not part of the reference): per tile,
+ * d' = clamp01(alpha*d + (kappa*d)*d + beta + sigma*u), u uniform in [-1,1) hashed from
+ * (seed, tile, pixel).  Used only to manufacture benchmark tiles from a ground-truth pano. */
+typedef struct pf_response {
+    float alpha, kappa, beta, sigma;
+    uint32_t seed, pad;
+} pf_response;
+
+int pf_create(int device, pf_ctx** out);
+void pf_destroy(pf_ctx* ctx);
+const char* pf_last_error(const pf_ctx* ctx);
+/* hipStream_t to order all work on (NULL = the null stream). */
+int pf_set_stream(pf_ctx* ctx, void* hip_stream);
+int pf_synchronize(pf_ctx* ctx);
+const char* pf_version(void);
+
+/* Tile layout.  Replaces PerspectiveMap::SetWindow + ranges (Depth.cpp:780-786).
+ * cap_ranges != 0 applies MergeDepthMaps' MIN2(range, D2R(359.9)) to ranges[0..1]
+ * (Depth.cpp:783-784).  tile_c = channels per tile pixel (channel 0 is used, as Value() does). */
+int pf_set_tiles(pf_ctx* ctx, const pf_window* fovs, const pf_window* ranges, int ntiles,
+                 const int* tile_w, const int* tile_h, int tile_c, int cap_ranges);
+
+/* SolveDepthToDepth (Depth.cpp:1261-1414) for every tile with only that tile active
+ * (MergeDepthMaps' loop, Depth.cpp:794-805), closed-form fp64 least squares of degree
+ * `degree` (3 = the reference's FunctorDepth2Depth3; 1 = scale/shift); coeffs may be NULL.
+ * coeffs64 (optional, [batch][ntiles][4] doubles) receives the unrounded solution.
+ * apply != 0 then runs Depth2DepthTransform (Depth.cpp:245-274) on the tiles in place. */
+int pf_register(pf_ctx* ctx, const float* emap, int ew, int eh, int ec, float* tiles,
+                int batch, float zr0, float zr1, int degree, int apply, float* coeffs,
+                double* coeffs64);
+
+/* SolveDepthAll (Depth.cpp:1416-1771): multi-level Laplacian-target scatter + damped Jacobi,
+ * u16 output.  coeffs (optional, from pf_register with apply = 0) fuses Depth2DepthTransform
+ * into the tile gather instead of rewriting the tiles. */
+int pf_fuse(pf_ctx* ctx, const float* emap, int ew, int eh, int ec, const float* tiles,
+            const float* coeffs, int batch, int out_w, int out_h, float zr0, float zr1,
+            uint16_t* out);
+
+/* MergeDepthMaps core (Depth.cpp:789-913) without file I/O: pf_register (degree 3) then
+ * pf_fuse with the transform fused.  Tiles are left untouched; coeffs (optional) receives the
+ * per-tile abcd. */
+int pf_merge(pf_ctx* ctx, const float* emap, int ew, int eh, int ec, const float* tiles,
+             int batch, int out_w, float zr0, float zr1, float* coeffs, uint16_t* out);
+
+/* E->P depth warp: tile pixel (X,Y) -> ToSphericalCoord(X/(W-1), Y/(H-1)) (Depth.cpp:157-166)
+ * -> bilinear sample of pano [batch][ph][pw] at (az/2pi*(pw-1), zen/pi*(ph-1)).  resp
+ * ([batch][ntiles], optional) applies the synthetic depth-net response. */
+int pf_warp_depth(pf_ctx* ctx, const float* pano, int pw, int ph, int batch,
+                  const pf_response* resp, float* tiles);
+
+/* E->P RGB warp (Main.cpp:242-326 SaveCubeMap + SphereMesh.cpp:154-210 texture mapping):
+ * u8 RGB pano [batch][ph][pw][3] -> tiles [batch][sum_i th_i*tw_i*3], GL camera conventions,
+ * GL_LINEAR + GL_REPEAT, rows top-first. */
+int pf_warp_rgb(pf_ctx* ctx, const uint8_t* pano, int pw, int ph, int batch, uint8_t* tiles);
+
+/* ---- multi-GPU fusion of one panorama (tiles sharded over ranks) ----
+ * pf_fuse_partial scatters the Laplacian targets of tiles [t0, t1) for level `level` into
+ * lsum/cnt ([out levels h][w] fp32 and fp32 counts); the caller sums them over ranks
+ * (RCCL reduce), then pf_fuse_finish_level runs normalisation + Jacobi on the summed grids. */
+int pf_level_info(int out_w, int out_h, float zr0, float zr1, int level, int* w, int* h,
+                  int* h0, int* h1, int* iters, int* nlevels);
+int pf_fuse_partial(pf_ctx* ctx, const float* tiles, const float* coeffs, int t0, int t1,
+                    int out_w, int out_h, float zr0, float zr1, int level, float* lsum,
+                    float* cnt);
+/* buf: the level's buffer (in: seed/upsampled values, out: after the sweeps).  When
+ * level == nlevels-1, out (if not NULL) receives the u16 quantisation. */
+int pf_fuse_seed(pf_ctx* ctx, const float* emap, int ew, int eh, int ec, const float* prev,
+                 int out_w, int out_h, float zr0, float zr1, int level, float* buf);
+int pf_fuse_finish_level(pf_ctx* ctx, const float* lsum, const float* cnt, int out_w,
+                         int out_h, float zr0, float zr1, int level, float* buf,
+                         uint16_t* out);
+
+/* ---- stage timing (hipEvents on the context stream; replaces the reference's timeGetTime
+ * brackets around registration and fusion, Depth.cpp:792-808, 907-916) ----
+ * While enabled, every entry point records an event pair around each stage it launches.
+ * pf_profile_read synchronises, then writes PF_NSTAGES entries of: elapsed ms, algorithmic
+ * bytes (SURVEY.md section 8d accounting) and kernel launches; it resets the accumulators. */
+#define PF_STAGE_WARP 0
+#define PF_STAGE_REGISTER 1
+#define PF_STAGE_SEED 2
+#define PF_STAGE_TARGETS 3
+#define PF_STAGE_JACOBI 4
+#define PF_STAGE_QUANTIZE 5
+#define PF_NSTAGES 6
+int pf_profile_enable(pf_ctx* ctx, int on);
+int pf_profile_read(pf_ctx* ctx, double* ms, double* bytes, long long* launches);
+
+/* ---- parity probes (bit-exact index maps) ----
+ * For level `level` of out_w: per covered pixel and tap k (5 taps in std::map order), the
+ * linear tile index (Y*W+X)*C of the tap for the first covering tile, -1 elsewhere.
+ * tap_index: [out_h_level][w][5] int32 device buffer.  lsum/cnt as pf_fuse_partial. */
+int pf_probe_taps(pf_ctx* ctx, int out_w, int out_h, float zr0, float zr1, int level,
+                  int32_t* tap_index);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,248 @@
+"""GPU parity: the HIP path (through the C-ABI) against the CPU oracle on identical inputs.
+
+Bars: bit-exact for tile index maps, level seeds, Laplacian targets,
+Jacobi buffers, registration coefficients and the u16 output; the E->P warps, whose atan2 is
+evaluated on the device in fp64 where the oracle calls glibc atan2f, within 2e-6 absolute (depth)
+and 1 LSB (RGB u8).  Oracle parity against the reference itself is unpinned (pf_oracle.h).
+"""
+import numpy as np
+import pytest
+
+torch = pytest.importorskip("torch")
+
+pytestmark = pytest.mark.gpu
+
+import panofuse  # noqa: E402
+import pf_layouts as PL  # noqa: E402
+import pf_synth  # noqa: E402
+import pyoracle as O  # noqa: E402
+
+ZR = PL.ZENITH_RANGE
+DEV = "cuda:0"
+WARP_TOL = 2e-6
+
+CFGS = {"C1": (512, 128), "C2": (2048, 512)}
+
+
+@pytest.fixture(scope="module")
+def fuser():
+    if not torch.cuda.is_available():
+        pytest.fail("GPU test collected on a host without a GPU")
+    return panofuse.Fuser(0)
+
+
+def _inputs(cfg, seed=0):
+    out_w, ew = CFGS[cfg]
+    lay = PL.config_layout(cfg)
+    seeds = pf_synth.seeds_for(1, 20261015 + 101 * seed)
+    emap = pf_synth.baseline_emap(seeds, ew, ew // 2)[0].numpy()
+    gt = pf_synth.scene_depth(seeds, out_w, out_w // 2)[0].numpy()
+    tiles, total = O.make_tiles(lay)
+    resp = pf_synth.responses(seeds, lay.ntiles)
+    data = O.warp_depth(gt, tiles, total, O.responses(resp))
+    return lay, emap, gt, tiles, total, data, resp
+
+
+def _dev(a):
+    return torch.from_numpy(np.ascontiguousarray(a)).to(DEV)
+
+
+@pytest.mark.parametrize("cfg", ["C1", "C2", "LERES"])
+def test_tap_index_maps_bit_exact(fuser, cfg):
+    lay = PL.config_layout(cfg)
+    out_w = 2048 if cfg != "C1" else 512
+    fuser.set_tiles(lay)
+    tiles, _ = O.make_tiles(lay)
+    for level in range(O.num_levels(out_w)):
+        got = fuser.probe_taps(out_w, ZR, level).cpu().numpy()
+        ref = O.probe_taps(tiles, O.level_dims(out_w, out_w // 2, ZR, level))
+        assert got.shape == ref.shape
+        bad = int((got != ref).sum())
+        assert bad == 0, f"{cfg} level {level}: {bad} tap indices differ"
+
+
+@pytest.mark.parametrize("cfg", ["C1", "C2"])
+def test_level_internals_bit_exact(fuser, cfg):
+    lay, emap, gt, tiles, total, data, _ = _inputs(cfg)
+    out_w = CFGS[cfg][0]
+    fuser.set_tiles(lay)
+    t_tiles = _dev(data)
+    t_emap = _dev(emap)[None]
+    prev_gpu = None
+    prev_ref = None
+    for level in range(O.num_levels(out_w)):
+        lv = O.level_dims(out_w, out_w // 2, ZR, level)
+        buf = torch.zeros(lv.h * lv.w, dtype=torch.float32, device=DEV)
+        fuser.fuse_seed(t_emap if level == 0 else None, prev_gpu, out_w, ZR, level, buf)
+        ref_seed = O.seed_level0(emap, lv) if level == 0 else O.upsample(prev_ref, lv)
+        assert np.array_equal(buf.cpu().numpy().reshape(lv.h, lv.w), ref_seed), f"seed L{level}"
+        lsum = torch.zeros(lv.h * lv.w, dtype=torch.float32, device=DEV)
+        cnt = torch.zeros_like(lsum)
+        fuser.fuse_partial(t_tiles, None, 0, lay.ntiles, out_w, ZR, level, lsum, cnt)
+        rL, rn, oops, _ = O.targets(tiles, data, lv)
+        assert oops == 0
+        band = slice(lv.h0, lv.h1 + 1)
+        g_l = lsum.cpu().numpy().reshape(lv.h, lv.w)[band]
+        g_n = cnt.cpu().numpy().reshape(lv.h, lv.w)[band]
+        assert np.array_equal(g_n, rn[band].astype(np.float32)), f"coverage L{level}"
+        assert np.array_equal(g_l.view(np.uint32), rL[band].view(np.uint32)), f"targets L{level}"
+        fuser.fuse_finish_level(lsum, cnt, out_w, ZR, level, buf)
+        ref_buf = O.jacobi(ref_seed, O.normalize(rL, rn, lv), lv, lv.iters)
+        got = buf.cpu().numpy().reshape(lv.h, lv.w)
+        bad = int((got.view(np.uint32) != ref_buf.view(np.uint32)).sum())
+        assert bad == 0, f"{cfg} level {level}: {bad} Jacobi values differ"
+        prev_gpu, prev_ref = buf, ref_buf
+
+
+@pytest.mark.parametrize("cfg", ["C1", "C2"])
+def test_register_bit_exact(fuser, cfg):
+    lay, emap, gt, tiles, total, data, _ = _inputs(cfg)
+    fuser.set_tiles(lay)
+    t_tiles = _dev(data)[None].contiguous()
+    coeffs = torch.zeros((1, lay.ntiles, 4), dtype=torch.float32, device=DEV)
+    c64 = torch.zeros((1, lay.ntiles, 4), dtype=torch.float64, device=DEV)
+    fuser.register(_dev(emap)[None], t_tiles, ZR, degree=3, apply=True, coeffs=coeffs,
+                   coeffs64=c64)
+    ref = data.copy()
+    for p in range(lay.ntiles):
+        r64, rabcd, deg = O.register_tile(tiles[p], data, emap, ZR)
+        assert deg == 3
+        assert np.array_equal(c64.cpu().numpy()[0, p], r64), f"tile {p} fp64 solution"
+        assert np.array_equal(coeffs.cpu().numpy()[0, p], rabcd), f"tile {p} abcd"
+        O.depth_to_depth(tiles[p], ref, rabcd)
+    assert np.array_equal(t_tiles.cpu().numpy()[0].view(np.uint32), ref.view(np.uint32))
+
+
+def test_register_degree1_and_lstsq(fuser):
+    """Scale/shift mode (north_star's 2x2 system) and agreement with an fp64 lstsq."""
+    lay, emap, gt, tiles, total, data, _ = _inputs("C1")
+    fuser.set_tiles(lay)
+    for degree in (1, 2, 3):
+        coeffs = torch.zeros((1, lay.ntiles, 4), dtype=torch.float32, device=DEV)
+        c64 = torch.zeros((1, lay.ntiles, 4), dtype=torch.float64, device=DEV)
+        fuser.register(_dev(emap)[None], _dev(data)[None].contiguous(), ZR, degree=degree,
+                       apply=False, coeffs=coeffs, coeffs64=c64)
+        for p in range(lay.ntiles):
+            xs, ys, _, _ = O.reg_samples(tiles[p], data, emap, ZR)
+            A = np.stack([xs ** k for k in range(degree, -1, -1)], 1)
+            sol, *_ = np.linalg.lstsq(A, ys, rcond=None)
+            got = c64.cpu().numpy()[0, p][3 - degree:]
+            assert np.max(np.abs(A @ got - A @ sol)) < 1e-6
+
+
+@pytest.mark.parametrize("cfg", ["C1", "C2"])
+def test_fuse_bit_exact(fuser, cfg):
+    lay, emap, gt, tiles, total, data, _ = _inputs(cfg, seed=3)
+    out_w = CFGS[cfg][0]
+    fuser.set_tiles(lay)
+    out = torch.zeros((1, out_w // 2, out_w), dtype=torch.int16, device=DEV)
+    fuser.fuse(_dev(emap)[None], _dev(data)[None].contiguous(), out, ZR)
+    ref, _ = O.solve_depth_all(emap, tiles, data, out_w, ZR)
+    got = out.cpu().numpy().view(np.uint16)[0]
+    assert int((got != ref).sum()) == 0
+
+
+@pytest.mark.parametrize("cfg", ["C1", "C2"])
+def test_merge_bit_exact_batched(fuser, cfg):
+    """MergeDepthMaps core for a batch of 3 panoramas == the oracle per panorama."""
+    out_w, ew = CFGS[cfg]
+    lay = PL.config_layout(cfg)
+    fuser.set_tiles(lay)
+    tiles, total = O.make_tiles(lay)
+    seeds = pf_synth.seeds_for(3, 777)
+    emaps = pf_synth.baseline_emap(seeds, ew, ew // 2).numpy()
+    gts = pf_synth.scene_depth(seeds, out_w, out_w // 2).numpy()
+    resp = pf_synth.responses(seeds, lay.ntiles)
+    datas = np.stack([O.warp_depth(gts[b], tiles, total,
+                                   O.responses(resp[b * lay.ntiles:(b + 1) * lay.ntiles]))
+                      for b in range(3)])
+    out = torch.zeros((3, out_w // 2, out_w), dtype=torch.int16, device=DEV)
+    coeffs = torch.zeros((3, lay.ntiles, 4), dtype=torch.float32, device=DEV)
+    t_tiles = _dev(datas)
+    fuser.merge(_dev(emaps), t_tiles, out, ZR, coeffs=coeffs)
+    got = out.cpu().numpy().view(np.uint16)
+    assert np.array_equal(t_tiles.cpu().numpy(), datas), "merge must not modify the tiles"
+    for b in range(3):
+        ref, abcd = O.merge(emaps[b], tiles, datas[b].copy(), out_w, ZR)
+        assert np.array_equal(coeffs.cpu().numpy()[b], abcd)
+        assert int((got[b] != ref).sum()) == 0, f"pano {b}"
+
+
+@pytest.mark.parametrize("cfg", ["C1", "C2"])
+def test_warp_depth_tolerance(fuser, cfg):
+    lay, emap, gt, tiles, total, data, resp = _inputs(cfg)
+    fuser.set_tiles(lay)
+    out = torch.zeros((2, total), dtype=torch.float32, device=DEV)
+    r = panofuse.make_responses(np.concatenate([resp, resp]), DEV)
+    fuser.warp_depth(_dev(np.stack([gt, gt])), out, r)
+    got = out.cpu().numpy()
+    assert np.max(np.abs(got[0] - data)) <= WARP_TOL
+    assert np.array_equal(got[0], got[1])
+    # without the response: plain bilinear E->P gather
+    out2 = torch.zeros((1, total), dtype=torch.float32, device=DEV)
+    fuser.warp_depth(_dev(gt)[None], out2)
+    ref2 = O.warp_depth(gt, tiles, total, None)
+    diff = np.abs(out2.cpu().numpy()[0] - ref2)
+    assert diff.max() <= WARP_TOL
+    assert (diff > 0).mean() < 0.05  # the fp64 atan2 differs from glibc atan2f by <= 1 ulp
+
+
+def test_warp_rgb_tolerance(fuser):
+    lay = PL.config_layout("C1")
+    fuser.set_tiles(lay)
+    tiles, _ = O.make_tiles(lay)
+    rs = np.random.RandomState(5)
+    h, w = 256, 512
+    yy, xx = np.mgrid[0:h, 0:w]
+    pano = np.stack([(xx * 255 // (w - 1)), (yy * 255 // (h - 1)),
+                     rs.randint(0, 256, size=(h, w))], -1).astype(np.uint8)
+    ref = O.warp_rgb(pano, tiles)
+    out = torch.zeros((1, ref.size), dtype=torch.uint8, device=DEV)
+    fuser.warp_rgb(_dev(pano)[None], out)
+    got = out.cpu().numpy()[0].astype(np.int32)
+    d = np.abs(got - ref.astype(np.int32))
+    assert d.max() <= 1 and (d > 0).mean() < 1e-3
+
+
+def test_sharded_partial_sum_equals_full(fuser):
+    """C5-style tile sharding: per-shard (sum L, n) grids summed == all tiles at once."""
+    lay, emap, gt, tiles, total, data, _ = _inputs("C2")
+    fuser.set_tiles(lay)
+    t_tiles = _dev(data)
+    lv = O.level_dims(2048, 1024, ZR, 2)
+    full_l = torch.zeros(lv.h * lv.w, dtype=torch.float32, device=DEV)
+    full_n = torch.zeros_like(full_l)
+    fuser.fuse_partial(t_tiles, None, 0, lay.ntiles, 2048, ZR, 2, full_l, full_n)
+    acc_l = torch.zeros_like(full_l)
+    acc_n = torch.zeros_like(full_l)
+    for t0 in range(0, lay.ntiles, 5):
+        l = torch.zeros_like(full_l)
+        n = torch.zeros_like(full_l)
+        fuser.fuse_partial(t_tiles, None, t0, t0 + 5, 2048, ZR, 2, l, n)
+        acc_l += l
+        acc_n += n
+    assert torch.equal(acc_n, full_n)
+    assert torch.equal(acc_l.view(torch.int32), full_l.view(torch.int32))
+
+
+def test_error_paths(fuser):
+    lay = PL.config_layout("C1")
+    fuser.set_tiles(lay)
+    emap = torch.zeros((1, 64, 128), dtype=torch.float32, device=DEV)
+    tiles = torch.zeros((1, fuser.tile_elems), dtype=torch.float32, device=DEV)
+    out = torch.zeros((1, 256, 500), dtype=torch.int16, device=DEV)
+    with pytest.raises(panofuse.PanofuseError) as e:
+        fuser.fuse(emap, tiles, out, ZR)  # 500 is not divisible by 4
+    assert e.value.code == panofuse.PF_EINVAL
+    with pytest.raises(panofuse.PanofuseError) as e:
+        fuser.register(emap, tiles, ZR, degree=7)
+    assert e.value.code == panofuse.PF_EINVAL
+    # a tile whose range collapses to one column at level 0 is rejected, not looped on
+    bad = PL.Layout("bad", lay.fovs[:1].copy(), lay.ranges[:1].copy(), lay.tile_w[:1],
+                    lay.tile_h[:1])
+    bad.ranges[0, 1] = bad.ranges[0, 0] - np.float32(1e-4)
+    fuser.set_tiles(bad)
+    out = torch.zeros((1, 256, 512), dtype=torch.int16, device=DEV)
+    with pytest.raises(panofuse.PanofuseError) as e:
+        fuser.fuse(emap, tiles[:, : 256 * 256].contiguous(), out, ZR)
+    assert e.value.code == panofuse.PF_EDEGENERATE

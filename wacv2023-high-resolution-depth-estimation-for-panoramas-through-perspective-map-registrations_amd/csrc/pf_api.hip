@@ -1,0 +1,815 @@
+// pf_api.hip -- C-ABI of libpanofuse (include/panofuse.h): context, layout preparation and the
+// stream-ordered launch sequences of the drop-in entry points.
+//
+// Host-side preparation done once per layout / fusion level (all tiny): the tile windows
+// (PerspectiveMap::SetWindow, Depth.cpp:120-155), the per-level tile boxes (Depth.cpp:1497-1562)
+// and the separable trig tables of the fusion and registration grids, computed with glibc's
+// sincosf/tanf exactly as the reference calls them.  Everything per panorama runs on the GPU.
+#include "../../include/panofuse.h"
+#include "pf_internal.hpp"
+
+#include <cfloat>
+#include <cmath>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+using namespace pf;
+
+namespace {
+
+struct DevBuf {
+    void* p = nullptr;
+    size_t bytes = 0;
+};
+
+struct LevelCache {
+    int out_w = 0, out_h = 0;
+    uint32_t zr0 = 0, zr1 = 0;
+    int nlevels = 0;
+    LevelDims dims[4];
+    DevBuf box[4], cols[4], rows[4];
+    std::vector<TileBox> box_h[4];
+};
+
+}  // namespace
+
+struct pf_ctx {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    std::string err;
+    // layout
+    int ntiles = 0, tile_c = 1;
+    std::vector<pf_window> fov, rng;
+    std::vector<TileGeom> geom_h;
+    std::vector<RegGrid> reg_h;
+    long long tile_elems = 0, npix_max = 0, rgb_elems = 0;
+    DevBuf geom, reg, rcols, rrows, cams, rgb_off;
+    LevelCache lc;
+    bool reg_valid = false;
+    uint32_t reg_zr0 = 0, reg_zr1 = 0;
+    // workspace
+    DevBuf buf[3], lnorm, coeffs, lsum_ws;
+    // stage profiling
+    struct Span {
+        int stage;
+        hipEvent_t a, b;
+        double bytes;
+        long long launches;
+    };
+    bool prof_on = false;
+    std::vector<Span> spans;
+    std::vector<hipEvent_t> event_pool;
+};
+
+namespace {
+hipEvent_t take_event(pf_ctx* c)
+{
+    if (!c->event_pool.empty()) {
+        hipEvent_t e = c->event_pool.back();
+        c->event_pool.pop_back();
+        return e;
+    }
+    hipEvent_t e = nullptr;
+    (void)hipEventCreate(&e);
+    return e;
+}
+
+// Records an event pair around a stage when profiling is on (RAII: end on scope exit).
+struct StageTimer {
+    pf_ctx* c;
+    long idx = -1;
+    StageTimer(pf_ctx* c_, int stage, double bytes, long long launches) : c(c_)
+    {
+        if (!c->prof_on) return;
+        pf_ctx::Span s{stage, take_event(c), take_event(c), bytes, launches};
+        (void)hipEventRecord(s.a, c->stream);
+        c->spans.push_back(s);
+        idx = (long)c->spans.size() - 1;
+    }
+    ~StageTimer()
+    {
+        if (idx >= 0) (void)hipEventRecord(c->spans[idx].b, c->stream);
+    }
+};
+}  // namespace
+
+// ---------------------------------------------------------------------------------------------
+static int fail(pf_ctx* c, int code, const char* fmt, ...)
+{
+    char msg[512];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(msg, sizeof(msg), fmt, ap);
+    va_end(ap);
+    if (c) c->err = msg;
+    return code;
+}
+
+#define HIPCHK(ctx, expr)                                                                    \
+    do {                                                                                     \
+        hipError_t e_ = (expr);                                                              \
+        if (e_ != hipSuccess)                                                                \
+            return fail(ctx, PF_EHIP, "%s: %s", #expr, hipGetErrorString(e_));               \
+    } while (0)
+
+static int ensure(pf_ctx* c, DevBuf& b, size_t bytes)
+{
+    if (b.bytes >= bytes) return PF_OK;
+    if (b.p) {
+        (void)hipStreamSynchronize(c->stream);
+        (void)hipFree(b.p);
+        b.p = nullptr;
+        b.bytes = 0;
+    }
+    if (bytes == 0) return PF_OK;
+    if (hipMalloc(&b.p, bytes) != hipSuccess)
+        return fail(c, PF_ENOMEM, "hipMalloc(%zu) failed", bytes);
+    b.bytes = bytes;
+    return PF_OK;
+}
+
+static void release(DevBuf& b)
+{
+    if (b.p) (void)hipFree(b.p);
+    b.p = nullptr;
+    b.bytes = 0;
+}
+
+template <class T>
+static int upload(pf_ctx* c, DevBuf& b, const std::vector<T>& v)
+{
+    int rc = ensure(c, b, v.size() * sizeof(T) + 16);
+    if (rc) return rc;
+    if (!v.empty())
+        HIPCHK(c, hipMemcpyAsync(b.p, v.data(), v.size() * sizeof(T), hipMemcpyHostToDevice,
+                                 c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));  // host vector may die after return
+    return PF_OK;
+}
+
+// ---------------------------------------------------------------------------------------------
+// Host geometry: Imath Vec3<float> semantics (ImathVec.h:1467-1700).
+namespace {
+struct V3 {
+    float x, y, z;
+};
+inline V3 add(V3 a, V3 b) { return {a.x + b.x, a.y + b.y, a.z + b.z}; }
+inline V3 sub(V3 a, V3 b) { return {a.x - b.x, a.y - b.y, a.z - b.z}; }
+inline V3 mul(V3 a, float s) { return {a.x * s, a.y * s, a.z * s}; }
+inline float dot(V3 a, V3 b) { return a.x * b.x + a.y * b.y + a.z * b.z; }
+inline V3 cross(V3 a, V3 b)
+{
+    return {a.y * b.z - a.z * b.y, a.z * b.x - a.x * b.z, a.x * b.y - a.y * b.x};
+}
+float length(V3 a)
+{
+    float l2 = dot(a, a);
+    if (l2 < 2.0f * FLT_MIN) {
+        float ax = a.x >= 0.0f ? a.x : -a.x, ay = a.y >= 0.0f ? a.y : -a.y,
+              az = a.z >= 0.0f ? a.z : -a.z;
+        float mx = ax;
+        if (mx < ay) mx = ay;
+        if (mx < az) mx = az;
+        if (mx == 0.0f) return 0.0f;
+        ax /= mx; ay /= mx; az /= mx;
+        return mx * sqrtf(ax * ax + ay * ay + az * az);
+    }
+    return sqrtf(l2);
+}
+V3 normalized(V3 a)
+{
+    float l = length(a);
+    if (l != 0.0f) { a.x /= l; a.y /= l; a.z /= l; }
+    return a;
+}
+V3 sph_to_world(float az, float zen)
+{  // Depth.cpp:2955-2958 (g++ emits sincosf for each sin/cos pair)
+    float sz, cz, sa, ca;
+    sincosf(zen, &sz, &cz);
+    sincosf(az, &sa, &ca);
+    return {sz * ca, sz * sa, cz};
+}
+
+TileGeom set_window(const pf_window& f, int w, int h, int ch)
+{  // PerspectiveMap::SetWindow, Depth.cpp:120-155
+    V3 middle = sph_to_world((f.az_left + f.az_right) / 2, (f.zen_top + f.zen_down) / 2);
+    V3 left = normalized(cross(V3{0, 0, 1}, middle));
+    V3 up = normalized(cross(left, middle));
+    float ta = tanf(fabsf(f.az_right - f.az_left) / 2);
+    float tz = tanf(fabsf(f.zen_top - f.zen_down) / 2);
+    V3 left_middle = add(middle, mul(left, ta));
+    V3 right_middle = sub(middle, mul(left, ta));
+    V3 up_middle = sub(middle, mul(up, tz));
+    V3 down_middle = add(middle, mul(up, tz));
+    V3 corner0 = add(add(middle, sub(left_middle, middle)), sub(up_middle, middle));
+    V3 hedge = sub(right_middle, left_middle);
+    V3 vedge = sub(down_middle, up_middle);
+    TileGeom g{};
+    g.middle[0] = middle.x; g.middle[1] = middle.y; g.middle[2] = middle.z;
+    g.hedge[0] = hedge.x; g.hedge[1] = hedge.y; g.hedge[2] = hedge.z;
+    g.vedge[0] = vedge.x; g.vedge[1] = vedge.y; g.vedge[2] = vedge.z;
+    g.corner0[0] = corner0.x; g.corner0[1] = corner0.y; g.corner0[2] = corner0.z;
+    V3 p0mp = {middle.x - 0.0f, middle.y - 0.0f, middle.z - 0.0f};  // (p0 - p), p = Vec3f(0)
+    g.mm = dot(p0mp, middle);
+    g.hl = length(hedge);
+    g.vl = length(vedge);
+    g.w = w;
+    g.h = h;
+    g.c = ch;
+    return g;
+}
+
+LevelDims level_dims(int out_w, int out_h, float zr0, float zr1, int level)
+{  // Depth.cpp:1420-1437, 1650-1675
+    LevelDims L{};
+    int max_level = out_w >= 4096 ? 4 : 3;
+    L.nlevels = max_level;
+    L.w = (int)(out_w / pow(2, max_level - 1 - level));
+    L.h = (int)(out_h / pow(2, max_level - 1 - level));
+    L.h0 = (int)floor((double)((float)L.h * zr0) / PF_MYPI);
+    L.h1 = (int)ceil((double)((float)L.h * zr1) / PF_MYPI);
+    static const int it3[3] = {200, 100, 50};
+    static const int it4[4] = {200, 150, 100, 50};
+    L.iters = max_level == 3 ? it3[level] : it4[level];
+    return L;
+}
+
+TileBox tile_box(const pf_window& r, const LevelDims& L)
+{  // Depth.cpp:1497-1562 (enlargement disabled at :1522/:1543; the clamps stay)
+    int w = L.w, h = L.h;
+    int x0 = (int)round((double)r.az_left / (2 * PF_MYPI) * (double)(w - 1));
+    int x1 = (int)round((double)r.az_right / (2 * PF_MYPI) * (double)(w - 1));
+    int y0 = (int)round((double)r.zen_top / PF_MYPI * (double)(h - 1));
+    int y1 = (int)round((double)r.zen_down / PF_MYPI * (double)(h - 1));
+    int xs = x1 >= x0 ? 1 : -1;
+    x0 = x0 < 0 ? 0 : (x0 >= w ? w - 1 : x0);
+    x1 = x1 < 0 ? 0 : (x1 >= w ? w - 1 : x1);
+    y0 = y0 < 0 ? 0 : (y0 >= h ? h - 1 : y0);
+    y1 = y1 < 0 ? 0 : (y1 >= h ? h - 1 : y1);
+    if (y0 <= L.h0) y0 = L.h0 + 1;
+    if (y1 >= L.h1) y1 = L.h1 - 1;
+    TileBox b{};
+    b.x0 = x0; b.x1 = x1; b.y0 = y0; b.y1 = y1; b.xs = xs;
+    return b;
+}
+
+// Fusion grid coordinates (Depth.cpp:1456,1591): az = (float)xx/(float)(w-1)*2*MYPI and
+// zen = (float)yy/(float)(h-1)*MYPI, rounded to float by the Vec2f; xx in [-1, w], yy in [-1, h].
+void grid_tables(const LevelDims& L, std::vector<GridCol>& cols, std::vector<GridRow>& rows)
+{
+    cols.resize(L.w + 2);
+    rows.resize(L.h + 2);
+    for (int xx = -1; xx <= L.w; xx++) {
+        float az = (float)((double)((float)xx / (float)(L.w - 1) * 2.0f) * PF_MYPI);
+        GridCol c{};
+        c.az = az;
+        sincosf(az, &c.sa, &c.ca);
+        cols[xx + 1] = c;
+    }
+    for (int yy = -1; yy <= L.h; yy++) {
+        float zen = (float)((double)((float)yy / (float)(L.h - 1)) * PF_MYPI);
+        GridRow r{};
+        r.zen = zen;
+        sincosf(zen, &r.sz, &r.cz);
+        rows[yy + 1] = r;
+    }
+}
+}  // namespace
+
+// ---------------------------------------------------------------------------------------------
+extern "C" {
+
+const char* pf_version(void) { return "panofuse 0.1 (gfx950)"; }
+
+int pf_create(int device, pf_ctx** out)
+{
+    if (!out) return PF_EINVAL;
+    *out = nullptr;
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess || device < 0 || device >= n) return PF_EHIP;
+    if (hipSetDevice(device) != hipSuccess) return PF_EHIP;
+    pf_ctx* c = new pf_ctx();
+    c->device = device;
+    *out = c;
+    return PF_OK;
+}
+
+void pf_destroy(pf_ctx* c)
+{
+    if (!c) return;
+    (void)hipSetDevice(c->device);
+    (void)hipStreamSynchronize(c->stream);
+    DevBuf* all[] = {&c->geom, &c->reg, &c->rcols, &c->rrows, &c->cams, &c->rgb_off,
+                     &c->buf[0], &c->buf[1], &c->buf[2], &c->lnorm, &c->coeffs, &c->lsum_ws};
+    for (DevBuf* b : all) release(*b);
+    for (int l = 0; l < 4; l++) {
+        release(c->lc.box[l]);
+        release(c->lc.cols[l]);
+        release(c->lc.rows[l]);
+    }
+    for (auto& s : c->spans) {
+        (void)hipEventDestroy(s.a);
+        (void)hipEventDestroy(s.b);
+    }
+    for (hipEvent_t e : c->event_pool) (void)hipEventDestroy(e);
+    delete c;
+}
+
+const char* pf_last_error(const pf_ctx* c) { return c ? c->err.c_str() : "null context"; }
+
+int pf_set_stream(pf_ctx* c, void* s)
+{
+    if (!c) return PF_EINVAL;
+    c->stream = (hipStream_t)s;
+    return PF_OK;
+}
+
+int pf_profile_enable(pf_ctx* c, int on)
+{
+    if (!c) return PF_EINVAL;
+    double ms[PF_NSTAGES], by[PF_NSTAGES];
+    long long ln[PF_NSTAGES];
+    int rc = pf_profile_read(c, ms, by, ln);  // drains and recycles pending spans
+    c->prof_on = on != 0;
+    return rc;
+}
+
+int pf_profile_read(pf_ctx* c, double* ms, double* bytes, long long* launches)
+{
+    if (!c) return PF_EINVAL;
+    for (int s = 0; s < PF_NSTAGES; s++) {
+        if (ms) ms[s] = 0;
+        if (bytes) bytes[s] = 0;
+        if (launches) launches[s] = 0;
+    }
+    HIPCHK(c, hipSetDevice(c->device));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    for (auto& s : c->spans) {
+        float t = 0.0f;
+        HIPCHK(c, hipEventElapsedTime(&t, s.a, s.b));
+        if (ms) ms[s.stage] += t;
+        if (bytes) bytes[s.stage] += s.bytes;
+        if (launches) launches[s.stage] += s.launches;
+        c->event_pool.push_back(s.a);
+        c->event_pool.push_back(s.b);
+    }
+    c->spans.clear();
+    return PF_OK;
+}
+
+int pf_synchronize(pf_ctx* c)
+{
+    if (!c) return PF_EINVAL;
+    HIPCHK(c, hipSetDevice(c->device));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    return PF_OK;
+}
+
+int pf_level_info(int out_w, int out_h, float zr0, float zr1, int level, int* w, int* h,
+                  int* h0, int* h1, int* iters, int* nlevels)
+{
+    if (out_w < 8 || out_h < 4) return PF_EINVAL;
+    int nl = out_w >= 4096 ? 4 : 3;
+    if (level < 0 || level >= nl) return PF_EINVAL;
+    LevelDims L = level_dims(out_w, out_h, zr0, zr1, level);
+    if (w) *w = L.w;
+    if (h) *h = L.h;
+    if (h0) *h0 = L.h0;
+    if (h1) *h1 = L.h1;
+    if (iters) *iters = L.iters;
+    if (nlevels) *nlevels = L.nlevels;
+    return PF_OK;
+}
+
+int pf_set_tiles(pf_ctx* c, const pf_window* fovs, const pf_window* ranges, int ntiles,
+                 const int* tile_w, const int* tile_h, int tile_c, int cap_ranges)
+{
+    if (!c) return PF_EINVAL;
+    if (!fovs || !ranges || !tile_w || !tile_h || ntiles <= 0 || ntiles > 4096 || tile_c <= 0)
+        return fail(c, PF_EINVAL, "pf_set_tiles: bad arguments (ntiles=%d, tile_c=%d)", ntiles,
+                    tile_c);
+    HIPCHK(c, hipSetDevice(c->device));
+    c->ntiles = ntiles;
+    c->tile_c = tile_c;
+    c->fov.assign(fovs, fovs + ntiles);
+    c->rng.assign(ranges, ranges + ntiles);
+    const double cap = 359.9 / 180.0 * PF_MYPI;  // D2R(359.9), MergeDepthMaps :783-784
+    c->geom_h.resize(ntiles);
+    c->reg_h.resize(ntiles);
+    std::vector<RgbCam> cams(ntiles);
+    std::vector<long long> rgb_off(ntiles);
+    long long off = 0, roff = 0, npmax = 0;
+    for (int i = 0; i < ntiles; i++) {
+        if (tile_w[i] < 2 || tile_h[i] < 2)
+            return fail(c, PF_EINVAL, "tile %d: size %dx%d (need >= 2x2)", i, tile_w[i], tile_h[i]);
+        pf_window& r = c->rng[i];
+        if (cap_ranges) {
+            r.az_left = (float)((double)r.az_left < cap ? (double)r.az_left : cap);
+            r.az_right = (float)((double)r.az_right < cap ? (double)r.az_right : cap);
+        }
+        TileGeom g = set_window(fovs[i], tile_w[i], tile_h[i], tile_c);
+        if (!(g.hl > 0.0f) || !(g.vl > 0.0f))
+            return fail(c, PF_EINVAL, "tile %d: degenerate window (pole or zero FOV)", i);
+        g.off = off;
+        off += (long long)tile_w[i] * tile_h[i] * tile_c;
+        rgb_off[i] = roff;
+        roff += (long long)tile_w[i] * tile_h[i] * 3;
+        long long np = (long long)tile_w[i] * tile_h[i];
+        if (np > npmax) npmax = np;
+        c->geom_h[i] = g;
+        // RGB camera (SaveCubeMap, Main.cpp:246-269), in double.
+        const pf_window& f = fovs[i];
+        float azc = (f.az_right + f.az_left) / 2, zenc = (f.zen_down + f.zen_top) / 2;
+        float fovx = (float)((f.az_right - f.az_left) / PF_MYPI * 180.0);
+        float fovy = (float)((f.zen_down - f.zen_top) / PF_MYPI * 180.0);
+        float aspect = (float)(tan(fovx / 180.0 * PF_MYPI / 2) / tan(fovy / 180.0 * PF_MYPI / 2));
+        RgbCam cam{};
+        double fv[3] = {cos((double)azc) * sin((double)zenc), sin((double)azc) * sin((double)zenc),
+                        cos((double)zenc)};
+        double fl = sqrt(fv[0] * fv[0] + fv[1] * fv[1] + fv[2] * fv[2]);
+        for (int k = 0; k < 3; k++) cam.f[k] = fv[k] / fl;
+        double sv[3] = {cam.f[1], -cam.f[0], 0.0};
+        double sl = sqrt(sv[0] * sv[0] + sv[1] * sv[1]);
+        cam.s[0] = sv[0] / sl; cam.s[1] = sv[1] / sl; cam.s[2] = 0.0;
+        cam.u[0] = cam.s[1] * cam.f[2] - cam.s[2] * cam.f[1];
+        cam.u[1] = cam.s[2] * cam.f[0] - cam.s[0] * cam.f[2];
+        cam.u[2] = cam.s[0] * cam.f[1] - cam.s[1] * cam.f[0];
+        cam.ty = tan((double)fovy / 180.0 * PF_MYPI / 2);
+        cam.tx = cam.ty * (double)aspect;
+        cams[i] = cam;
+    }
+    c->tile_elems = off;
+    c->rgb_elems = roff;
+    c->npix_max = npmax;
+    c->lc.out_w = 0;  // boxes and registration grids depend on the ranges: rebuild lazily
+    c->reg_valid = false;
+    int rc;
+    if ((rc = upload(c, c->geom, c->geom_h))) return rc;
+    if ((rc = upload(c, c->cams, cams))) return rc;
+    if ((rc = upload(c, c->rgb_off, rgb_off))) return rc;
+    return PF_OK;
+}
+
+}  // extern "C"
+
+// Registration tables depend on the zenith range; built per call (tiny, cached by value).
+static int prepare_registration(pf_ctx* c, float zr0, float zr1)
+{
+    uint32_t b0, b1;
+    memcpy(&b0, &zr0, 4);
+    memcpy(&b1, &zr1, 4);
+    if (c->reg_valid && b0 == c->reg_zr0 && b1 == c->reg_zr1) return PF_OK;
+    const float subd = (float)(1 / 180.0 * PF_MYPI);
+    std::vector<GridCol> rcols;
+    std::vector<GridRow> rrows;
+    for (int i = 0; i < c->ntiles; i++) {
+        const pf_window& r = c->rng[i];
+        RegGrid rg{};
+        rg.cols = (int)roundf(fabsf(r.az_right - r.az_left) / subd);
+        float top = zr0 > r.zen_top ? zr0 : r.zen_top;      // MAX2 (:1301)
+        float down = zr1 < r.zen_down ? zr1 : r.zen_down;   // MIN2 (:1302)
+        rg.rows = (int)roundf(fabsf(down - top) / subd);
+        if (rg.cols <= 0 || rg.rows <= 0)
+            return fail(c, PF_EINVAL,
+                        "tile %d: registration grid %dx%d is empty (the reference divides by 0)",
+                        i, rg.cols, rg.rows);
+        rg.col_off = (int)rcols.size();
+        rg.row_off = (int)rrows.size();
+        for (int k = 0; k <= rg.cols; k++) {  // :1334
+            GridCol e{};
+            e.az = r.az_left + (r.az_right - r.az_left) * (float)k / (float)rg.cols;
+            sincosf(e.az, &e.sa, &e.ca);
+            rcols.push_back(e);
+        }
+        for (int k = 0; k <= rg.rows; k++) {  // :1335
+            GridRow e{};
+            e.zen = top + (down - top) * (float)k / (float)rg.rows;
+            sincosf(e.zen, &e.sz, &e.cz);
+            rrows.push_back(e);
+        }
+        c->reg_h[i] = rg;
+    }
+    int rc;
+    if ((rc = upload(c, c->reg, c->reg_h))) return rc;
+    if ((rc = upload(c, c->rcols, rcols))) return rc;
+    if ((rc = upload(c, c->rrows, rrows))) return rc;
+    c->reg_valid = true;
+    c->reg_zr0 = b0;
+    c->reg_zr1 = b1;
+    return PF_OK;
+}
+
+static int prepare_levels(pf_ctx* c, int out_w, int out_h, float zr0, float zr1)
+{
+    uint32_t b0, b1;
+    memcpy(&b0, &zr0, 4);
+    memcpy(&b1, &zr1, 4);
+    LevelCache& lc = c->lc;
+    if (lc.out_w == out_w && lc.out_h == out_h && lc.zr0 == b0 && lc.zr1 == b1) return PF_OK;
+    if (out_w < 8 || out_h < 8)
+        return fail(c, PF_EINVAL, "output %dx%d too small", out_w, out_h);
+    int nl = out_w >= 4096 ? 4 : 3;
+    for (int l = 0; l < nl; l++) {
+        LevelDims L = level_dims(out_w, out_h, zr0, zr1, l);
+        if (L.w < 4 || L.h < 4 || L.h0 < 1 || L.h1 > L.h - 2 || L.h0 >= L.h1)
+            return fail(c, PF_EINVAL,
+                        "level %d: %dx%d with band [%d,%d] (zenith range must stay inside "
+                        "(0, pi) by a row)",
+                        l, L.w, L.h, L.h0, L.h1);
+        if (l > 0 && (L.w != 2 * lc.dims[l - 1].w || L.h != 2 * lc.dims[l - 1].h))
+            return fail(c, PF_EINVAL, "output %dx%d is not divisible by 2^%d", out_w, out_h,
+                        nl - 1);
+        lc.dims[l] = L;
+        std::vector<TileBox> boxes(c->ntiles);
+        std::vector<int> cover((size_t)L.w * L.h, 0);
+        for (int p = 0; p < c->ntiles; p++) {
+            boxes[p] = tile_box(c->rng[p], L);
+            const TileBox& b = boxes[p];
+            if (b.x0 == b.x1)
+                return fail(c, PF_EDEGENERATE,
+                            "tile %d at level %d: box x0 == x1 == %d (the reference never "
+                            "terminates here)",
+                            p, l, b.x0);
+            for (int X = b.x0; X != b.x1; X += b.xs)
+                for (int Y = b.y0; Y <= b.y1; Y++)
+                    if (++cover[(size_t)Y * L.w + X] > PF_MAX_COVER)
+                        return fail(c, PF_EINVAL, "pixel (%d,%d) covered by more than %d tiles",
+                                    X, Y, PF_MAX_COVER);
+        }
+        lc.box_h[l] = boxes;
+        std::vector<GridCol> cols;
+        std::vector<GridRow> rows;
+        grid_tables(L, cols, rows);
+        int rc;
+        if ((rc = upload(c, lc.box[l], boxes))) return rc;
+        if ((rc = upload(c, lc.cols[l], cols))) return rc;
+        if ((rc = upload(c, lc.rows[l], rows))) return rc;
+    }
+    lc.nlevels = nl;
+    lc.out_w = out_w;
+    lc.out_h = out_h;
+    lc.zr0 = b0;
+    lc.zr1 = b1;
+    return PF_OK;
+}
+
+static int check_common(pf_ctx* c, int batch)
+{
+    if (!c) return PF_EINVAL;
+    if (c->ntiles <= 0) return fail(c, PF_ESTATE, "no tile layout: call pf_set_tiles first");
+    if (batch <= 0 || batch > 65535) return fail(c, PF_EINVAL, "batch %d out of range", batch);
+    if (hipSetDevice(c->device) != hipSuccess) return fail(c, PF_EHIP, "hipSetDevice failed");
+    return PF_OK;
+}
+
+static int check_emap(pf_ctx* c, const float* emap, int ew, int eh, int ec)
+{
+    if (!emap || ew < 2 || eh < 2 || ec < 1)
+        return fail(c, PF_EINVAL, "bad emap %p %dx%dx%d", (const void*)emap, ew, eh, ec);
+    return PF_OK;
+}
+
+static int fuse_impl(pf_ctx* c, const float* emap, int ew, int eh, int ec, const float* tiles,
+                     const float* coeffs, int batch, int out_w, int out_h, float zr0,
+                     float zr1, uint16_t* out)
+{
+    int rc;
+    if ((rc = prepare_levels(c, out_w, out_h, zr0, zr1))) return rc;
+    const long long plane = (long long)out_w * out_h;
+    for (int k = 0; k < 3; k++)
+        if ((rc = ensure(c, c->buf[k], sizeof(float) * plane * batch))) return rc;
+    if ((rc = ensure(c, c->lnorm, sizeof(float) * plane * batch))) return rc;
+    const long long estride = (long long)ew * eh * ec;
+    float* bufs[3] = {(float*)c->buf[0].p, (float*)c->buf[1].p, (float*)c->buf[2].p};
+    float* prev = nullptr;
+    LevelCache& lc = c->lc;
+    for (int l = 0; l < lc.nlevels; l++) {
+        const LevelDims& L = lc.dims[l];
+        const long long st = (long long)L.w * L.h;
+        float* a = nullptr;
+        float* b = nullptr;
+        for (int k = 0; k < 3; k++) {
+            if (bufs[k] == prev) continue;
+            if (!a) a = bufs[k];
+            else if (!b) b = bufs[k];
+        }
+        const double B = (double)batch;
+        const double band = (double)L.w * (L.h1 - L.h0 + 1);
+        {
+            // algorithmic bytes: write the level, read the source
+            double src = l == 0 ? (double)(L.h1 - L.h0 + 1) * L.w * 4.0 : (double)st;
+            StageTimer t(c, PF_STAGE_SEED, B * (4.0 * st + src), 1);
+            if (l == 0)
+                launch_seed0(c->stream, emap, ew, eh, ec, estride, (const GridCol*)lc.cols[0].p,
+                             (const GridRow*)lc.rows[0].p, L, a, st, batch);
+            else
+                launch_upsample(c->stream, prev, (long long)lc.dims[l - 1].w * lc.dims[l - 1].h, L,
+                                a, st, batch);
+        }
+        {
+            StageTimer t(c, PF_STAGE_TARGETS, B * (4.0 * band + 4.0 * (double)c->tile_elems), 1);
+            launch_targets(c->stream, (const TileGeom*)c->geom.p, (const TileBox*)lc.box[l].p, 0,
+                           c->ntiles, (const GridCol*)lc.cols[l].p, (const GridRow*)lc.rows[l].p,
+                           tiles, c->tile_elems, coeffs, c->ntiles, L, (float*)c->lnorm.p, st,
+                           batch);
+        }
+        HIPCHK(c, hipMemcpyAsync(b, a, sizeof(float) * st * batch, hipMemcpyDeviceToDevice,
+                                 c->stream));
+        float* res = nullptr;
+        {
+            // 12 B per pixel-update: read b, read L, write b' 
+            StageTimer t(c, PF_STAGE_JACOBI, B * 12.0 * band * L.iters, L.iters);
+            launch_jacobi(c->stream, a, b, (const float*)c->lnorm.p, st, L, L.iters, batch, &res);
+        }
+        if (l == lc.nlevels - 1) {
+            StageTimer t(c, PF_STAGE_QUANTIZE, B * 6.0 * st, 1);
+            launch_quantize(c->stream, res, st, (int)st, out, plane, batch);
+        }
+        prev = res;
+    }
+    HIPCHK(c, hipGetLastError());
+    return PF_OK;
+}
+
+extern "C" {
+
+int pf_register(pf_ctx* c, const float* emap, int ew, int eh, int ec, float* tiles, int batch,
+                float zr0, float zr1, int degree, int apply, float* coeffs, double* coeffs64)
+{
+    int rc;
+    if ((rc = check_common(c, batch))) return rc;
+    if ((rc = check_emap(c, emap, ew, eh, ec))) return rc;
+    if (!tiles) return fail(c, PF_EINVAL, "tiles is NULL");
+    if (degree < 0 || degree > 3) return fail(c, PF_EINVAL, "degree %d not in [0,3]", degree);
+    if ((rc = prepare_registration(c, zr0, zr1))) return rc;
+    float* cf = coeffs;
+    if (!cf) {
+        if ((rc = ensure(c, c->coeffs, sizeof(float) * 4 * c->ntiles * batch))) return rc;
+        cf = (float*)c->coeffs.p;
+    }
+    double nsamp = 0;
+    for (const RegGrid& g : c->reg_h) nsamp += (double)(g.cols + 1) * (g.rows + 1);
+    {
+        StageTimer t(c, PF_STAGE_REGISTER,
+                     batch * (8.0 * nsamp + (apply ? 8.0 * (double)c->tile_elems / c->tile_c : 0.0)),
+                     apply ? 2 : 1);
+        launch_register(c->stream, (const TileGeom*)c->geom.p, (const RegGrid*)c->reg.p,
+                        (const GridCol*)c->rcols.p, (const GridRow*)c->rrows.p, c->ntiles, emap,
+                        ew, eh, ec, (long long)ew * eh * ec, tiles, c->tile_elems, degree, cf,
+                        coeffs64, batch);
+        if (apply)
+            launch_apply_cubic(c->stream, (const TileGeom*)c->geom.p, c->ntiles,
+                               c->tile_elems / c->tile_c, tiles, c->tile_elems, cf, batch);
+    }
+    HIPCHK(c, hipGetLastError());
+    return PF_OK;
+}
+
+int pf_fuse(pf_ctx* c, const float* emap, int ew, int eh, int ec, const float* tiles,
+            const float* coeffs, int batch, int out_w, int out_h, float zr0, float zr1,
+            uint16_t* out)
+{
+    int rc;
+    if ((rc = check_common(c, batch))) return rc;
+    if ((rc = check_emap(c, emap, ew, eh, ec))) return rc;
+    if (!tiles || !out) return fail(c, PF_EINVAL, "tiles/out is NULL");
+    return fuse_impl(c, emap, ew, eh, ec, tiles, coeffs, batch, out_w, out_h, zr0, zr1, out);
+}
+
+int pf_merge(pf_ctx* c, const float* emap, int ew, int eh, int ec, const float* tiles, int batch,
+             int out_w, float zr0, float zr1, float* coeffs, uint16_t* out)
+{
+    int rc;
+    if ((rc = check_common(c, batch))) return rc;
+    if ((rc = check_emap(c, emap, ew, eh, ec))) return rc;
+    if (!tiles || !out) return fail(c, PF_EINVAL, "tiles/out is NULL");
+    float* cf = coeffs;
+    if (!cf) {
+        if ((rc = ensure(c, c->coeffs, sizeof(float) * 4 * c->ntiles * batch))) return rc;
+        cf = (float*)c->coeffs.p;
+    }
+    if ((rc = pf_register(c, emap, ew, eh, ec, const_cast<float*>(tiles), batch, zr0, zr1, 3, 0,
+                          cf, nullptr)))
+        return rc;
+    return fuse_impl(c, emap, ew, eh, ec, tiles, cf, batch, out_w, out_w / 2, zr0, zr1, out);
+}
+
+int pf_warp_depth(pf_ctx* c, const float* pano, int pw, int ph, int batch,
+                  const pf_response* resp, float* tiles)
+{
+    int rc;
+    if ((rc = check_common(c, batch))) return rc;
+    if (!pano || !tiles || pw < 2 || ph < 2)
+        return fail(c, PF_EINVAL, "bad pano %p %dx%d", (const void*)pano, pw, ph);
+    static_assert(sizeof(pf_response) == sizeof(Resp), "pf_response layout");
+    StageTimer t(c, PF_STAGE_WARP,
+                 batch * (4.0 * pw * ph + 4.0 * (double)c->tile_elems / c->tile_c), 1);
+    launch_warp_depth(c->stream, (const TileGeom*)c->geom.p, c->ntiles, c->npix_max, pano, pw,
+                      ph, (long long)pw * ph, (const Resp*)resp, tiles, c->tile_elems, batch);
+    HIPCHK(c, hipGetLastError());
+    return PF_OK;
+}
+
+int pf_warp_rgb(pf_ctx* c, const uint8_t* pano, int pw, int ph, int batch, uint8_t* tiles)
+{
+    int rc;
+    if ((rc = check_common(c, batch))) return rc;
+    if (!pano || !tiles || pw < 2 || ph < 2)
+        return fail(c, PF_EINVAL, "bad pano %p %dx%d", (const void*)pano, pw, ph);
+    StageTimer t(c, PF_STAGE_WARP, batch * (3.0 * pw * ph + (double)c->rgb_elems), 1);
+    launch_warp_rgb(c->stream, (const RgbCam*)c->cams.p, (const TileGeom*)c->geom.p, c->ntiles,
+                    c->npix_max, nullptr, (const long long*)c->rgb_off.p, pano, pw, ph,
+                    (long long)pw * ph * 3, tiles, c->rgb_elems, batch);
+    HIPCHK(c, hipGetLastError());
+    return PF_OK;
+}
+
+int pf_fuse_partial(pf_ctx* c, const float* tiles, const float* coeffs, int t0, int t1,
+                    int out_w, int out_h, float zr0, float zr1, int level, float* lsum,
+                    float* cnt)
+{
+    int rc;
+    if ((rc = check_common(c, 1))) return rc;
+    if (!tiles || !lsum || !cnt) return fail(c, PF_EINVAL, "NULL buffer");
+    if (t0 < 0 || t1 > c->ntiles || t0 > t1)
+        return fail(c, PF_EINVAL, "tile range [%d,%d) outside [0,%d)", t0, t1, c->ntiles);
+    if ((rc = prepare_levels(c, out_w, out_h, zr0, zr1))) return rc;
+    LevelCache& lc = c->lc;
+    if (level < 0 || level >= lc.nlevels) return fail(c, PF_EINVAL, "bad level %d", level);
+    const LevelDims& L = lc.dims[level];
+    HIPCHK(c, hipMemsetAsync(lsum, 0, sizeof(float) * L.w * L.h, c->stream));
+    HIPCHK(c, hipMemsetAsync(cnt, 0, sizeof(float) * L.w * L.h, c->stream));
+    launch_targets_partial(c->stream, (const TileGeom*)c->geom.p, (const TileBox*)lc.box[level].p,
+                           t0, t1, (const GridCol*)lc.cols[level].p,
+                           (const GridRow*)lc.rows[level].p, tiles, coeffs, L, lsum, cnt);
+    HIPCHK(c, hipGetLastError());
+    return PF_OK;
+}
+
+int pf_fuse_seed(pf_ctx* c, const float* emap, int ew, int eh, int ec, const float* prev,
+                 int out_w, int out_h, float zr0, float zr1, int level, float* buf)
+{
+    int rc;
+    if ((rc = check_common(c, 1))) return rc;
+    if (!buf) return fail(c, PF_EINVAL, "NULL buffer");
+    if ((rc = prepare_levels(c, out_w, out_h, zr0, zr1))) return rc;
+    LevelCache& lc = c->lc;
+    if (level < 0 || level >= lc.nlevels) return fail(c, PF_EINVAL, "bad level %d", level);
+    const LevelDims& L = lc.dims[level];
+    if (level == 0) {
+        if ((rc = check_emap(c, emap, ew, eh, ec))) return rc;
+        launch_seed0(c->stream, emap, ew, eh, ec, 0, (const GridCol*)lc.cols[0].p,
+                     (const GridRow*)lc.rows[0].p, L, buf, 0, 1);
+    } else {
+        if (!prev) return fail(c, PF_EINVAL, "level %d needs the previous level's buffer", level);
+        launch_upsample(c->stream, prev, 0, L, buf, 0, 1);
+    }
+    HIPCHK(c, hipGetLastError());
+    return PF_OK;
+}
+
+int pf_fuse_finish_level(pf_ctx* c, const float* lsum, const float* cnt, int out_w, int out_h,
+                         float zr0, float zr1, int level, float* buf, uint16_t* out)
+{
+    int rc;
+    if ((rc = check_common(c, 1))) return rc;
+    if (!lsum || !cnt || !buf) return fail(c, PF_EINVAL, "NULL buffer");
+    if ((rc = prepare_levels(c, out_w, out_h, zr0, zr1))) return rc;
+    LevelCache& lc = c->lc;
+    if (level < 0 || level >= lc.nlevels) return fail(c, PF_EINVAL, "bad level %d", level);
+    const LevelDims& L = lc.dims[level];
+    const long long st = (long long)L.w * L.h;
+    if ((rc = ensure(c, c->lnorm, sizeof(float) * st))) return rc;
+    if ((rc = ensure(c, c->lsum_ws, sizeof(float) * st))) return rc;
+    launch_normalize(c->stream, lsum, cnt, L, (float*)c->lnorm.p);
+    float* other = (float*)c->lsum_ws.p;
+    HIPCHK(c, hipMemcpyAsync(other, buf, sizeof(float) * st, hipMemcpyDeviceToDevice, c->stream));
+    float* res = nullptr;
+    launch_jacobi(c->stream, buf, other, (const float*)c->lnorm.p, st, L, L.iters, 1, &res);
+    if (res != buf)
+        HIPCHK(c, hipMemcpyAsync(buf, res, sizeof(float) * st, hipMemcpyDeviceToDevice, c->stream));
+    if (level == lc.nlevels - 1 && out) launch_quantize(c->stream, buf, st, (int)st, out, st, 1);
+    HIPCHK(c, hipGetLastError());
+    return PF_OK;
+}
+
+int pf_probe_taps(pf_ctx* c, int out_w, int out_h, float zr0, float zr1, int level,
+                  int32_t* tap_index)
+{
+    int rc;
+    if ((rc = check_common(c, 1))) return rc;
+    if (!tap_index) return fail(c, PF_EINVAL, "NULL buffer");
+    if ((rc = prepare_levels(c, out_w, out_h, zr0, zr1))) return rc;
+    LevelCache& lc = c->lc;
+    if (level < 0 || level >= lc.nlevels) return fail(c, PF_EINVAL, "bad level %d", level);
+    launch_probe_taps(c->stream, (const TileGeom*)c->geom.p, (const TileBox*)lc.box[level].p,
+                      c->ntiles, (const GridCol*)lc.cols[level].p, (const GridRow*)lc.rows[level].p,
+                      lc.dims[level], tap_index);
+    HIPCHK(c, hipGetLastError());
+    return PF_OK;
+}
+
+}  // extern "C"

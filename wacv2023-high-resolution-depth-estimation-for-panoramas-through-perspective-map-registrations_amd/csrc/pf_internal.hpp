@@ -1,0 +1,151 @@
+// pf_internal.hpp -- shared declarations of the panofuse HIP library (host + device).
+//
+// Numeric contract: every float expression that the reference evaluates
+// in fp32 is evaluated here in fp32, in the reference's operand order, with separately rounded
+// multiplies and adds (built with -ffp-contract=off and correctly rounded fp32 div/sqrt).
+// Transcendentals of the fusion grid and registration grid are separable (a column term and a
+// row term), so they are tabulated on the host with the same glibc sincosf the reference calls
+// and uploaded once per layout/level; the device never evaluates sin/cos on the parity path.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <cstdint>
+
+#pragma clang fp contract(off)
+
+#define PF_MYPI 3.14159265359  // Basic.h:11
+#define PF_NAN_MARKER 0x7FBADBADu  // "un-windowed pixel" tag in the target array (sNaN payload)
+#define PF_MAX_COVER 40            // normalised stencil weights are exactly {1,-0.25} up to here
+
+namespace pf {
+
+// Per-tile projection constants: PerspectiveMap's cached window (Depth.h:85-92) plus the
+// loop-invariant pieces of SphericalTo2D (|hedge|, |vedge|, (middle-0).middle).
+struct TileGeom {
+    float middle[3], hedge[3], vedge[3], corner0[3];
+    float mm, hl, vl, pad;
+    int w, h, c, pad2;
+    long long off;  // float offset of the tile inside one panorama's tile block
+};
+
+// Tile box at one fusion level (Depth.cpp:1497-1562) after the clamps.
+struct TileBox {
+    int x0, x1, y0, y1, xs, pad[3];
+};
+
+struct GridCol { float az, ca, sa, pad; };   // column xx (index xx+1): az, cos az, sin az
+struct GridRow { float zen, sz, cz, pad; };  // row yy (index yy+1): zen, sin zen, cos zen
+
+// Registration grid of one tile (Depth.cpp:1298-1335).
+struct RegGrid {
+    int cols, rows, col_off, row_off;  // offsets into the shared GridCol / GridRow tables
+};
+
+// GL camera of SaveCubeMap (Main.cpp:246-269) per tile, evaluated on the host in double.
+struct RgbCam {
+    double f[3], s[3], u[3];
+    double tx, ty;
+};
+
+// Synthetic depth-net response (same layout as pf_response in panofuse.h).
+struct Resp {
+    float alpha, kappa, beta, sigma;
+    uint32_t seed, pad;
+};
+
+struct LevelDims {
+    int w, h, h0, h1, iters, nlevels;
+};
+
+// ------------------------------------------------------------------------------------------
+// Imath Vec3<float> arithmetic in source order (ImathVec.h:1467-1486, 1631-1700).
+__host__ __device__ inline float dot3(const float* a, const float* b)
+{
+    return a[0] * b[0] + a[1] * b[1] + a[2] * b[2];
+}
+
+// SphericalTo2D (Depth.cpp:168-182) with dir = SphericalToWorld(az, zen) (Depth.cpp:2955-2958)
+// given as the tabulated (sin zen, cos zen, cos az, sin az).  LinePlaneIntersection
+// (Depth.cpp:34-42) with p = 0 and p0 = normal = middle: t = (middle.middle)/(dir.middle),
+// pos = 0 + t*dir.
+__host__ __device__ inline void sph_to_2d(const TileGeom& g, float sz, float cz, float ca,
+                                          float sa, float& x, float& y)
+{
+    float d0 = sz * ca, d1 = sz * sa, d2 = cz;
+    float den = d0 * g.middle[0] + d1 * g.middle[1] + d2 * g.middle[2];
+    float t = g.mm / den;
+    float p0 = 0.0f + t * d0, p1 = 0.0f + t * d1, p2 = 0.0f + t * d2;
+    float e0 = p0 - g.corner0[0], e1 = p1 - g.corner0[1], e2 = p2 - g.corner0[2];
+    float eh = e0 * g.hedge[0] + e1 * g.hedge[1] + e2 * g.hedge[2];
+    float ev = e0 * g.vedge[0] + e1 * g.vedge[1] + e2 * g.vedge[2];
+    x = (eh / g.hl) / g.hl;
+    y = (ev / g.vl) / g.vl;
+}
+
+// PerspectiveMap::Value (Depth.cpp:111-118): truncating nearest lookup; returns the linear
+// element index (Y*W+X)*C.
+__host__ __device__ inline long long tile_index(const TileGeom& g, float x, float y)
+{
+    int X = (int)(x * (float)(g.w - 1));
+    int Y = (int)(y * (float)(g.h - 1));
+    return ((long long)Y * g.w + X) * g.c;
+}
+
+// Depth2DepthTransform's per-pixel map (Depth.cpp:256-271).
+__host__ __device__ inline float cubic_map(float X, float a, float b, float c, float d)
+{
+    if (X < 1e-4) X = (float)1e-4;
+    else if (X > (1 - 1e-4)) X = (float)(1 - 1e-4);
+    float Y = a * X * X * X + b * X * X + c * X + d;
+    if (Y < 0) Y = 0;
+    else if (Y > 1) Y = 1;
+    return Y;
+}
+
+// EquirectangularMap::ValueAtCoord (Depth.cpp:551-556): index math promoted to double by MYPI.
+__host__ __device__ inline long long emap_index(float az, float zen, int w, int h, int c)
+{
+    int x = (int)((double)az / (PF_MYPI * 2) * (double)(float)(w - 1));
+    int y = (int)((double)zen / PF_MYPI * (double)(float)(h - 1));
+    return ((long long)y * w + x) * c;
+}
+
+// ------------------------------------------------------------------------------------------
+// Kernel launchers (pf_kernels.hip).  All are asynchronous on `stream`.
+void launch_seed0(hipStream_t s, const float* emap, int ew, int eh, int ec, long long estride,
+                  const GridCol* cols, const GridRow* rows, LevelDims L, float* buf,
+                  long long bstride, int batch);
+void launch_upsample(hipStream_t s, const float* prev, long long pstride, LevelDims L,
+                     float* buf, long long bstride, int batch);
+void launch_targets(hipStream_t s, const TileGeom* geom, const TileBox* box, int t0, int t1,
+                    const GridCol* cols, const GridRow* rows, const float* tiles,
+                    long long tstride, const float* coeffs, int ntiles_total, LevelDims L,
+                    float* lnorm, long long lstride, int batch);
+void launch_targets_partial(hipStream_t s, const TileGeom* geom, const TileBox* box, int t0,
+                            int t1, const GridCol* cols, const GridRow* rows,
+                            const float* tiles, const float* coeffs, LevelDims L, float* lsum,
+                            float* cnt);
+void launch_normalize(hipStream_t s, const float* lsum, const float* cnt, LevelDims L,
+                      float* lnorm);
+void launch_probe_taps(hipStream_t s, const TileGeom* geom, const TileBox* box, int ntiles,
+                       const GridCol* cols, const GridRow* rows, LevelDims L, int32_t* out);
+void launch_jacobi(hipStream_t s, float* buf_a, float* buf_b, const float* lnorm,
+                   long long stride, LevelDims L, int iters, int batch, float** result);
+void launch_quantize(hipStream_t s, const float* buf, long long bstride, int n, uint16_t* out,
+                     long long ostride, int batch);
+void launch_register(hipStream_t s, const TileGeom* geom, const RegGrid* grids,
+                     const GridCol* rcols, const GridRow* rrows, int ntiles, const float* emap,
+                     int ew, int eh, int ec, long long estride, const float* tiles,
+                     long long tstride, int degree, float* coeffs, double* coeffs64,
+                     int batch);
+void launch_apply_cubic(hipStream_t s, const TileGeom* geom, int ntiles, long long tile_elems,
+                        float* tiles, long long tstride, const float* coeffs, int batch);
+void launch_warp_depth(hipStream_t s, const TileGeom* geom, int ntiles, long long npix_max,
+                       const float* pano, int pw, int ph, long long pstride, const Resp* resp,
+                       float* tiles, long long tstride, int batch);
+void launch_warp_rgb(hipStream_t s, const RgbCam* cams, const TileGeom* geom, int ntiles,
+                     long long npix_total, const long long* pix_prefix,
+                     const long long* rgb_off, const uint8_t* pano, int pw, int ph,
+                     long long pstride, uint8_t* tiles, long long tstride, int batch);
+
+}  // namespace pf

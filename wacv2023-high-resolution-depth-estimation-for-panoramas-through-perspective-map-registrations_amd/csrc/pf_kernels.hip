@@ -1,0 +1,652 @@
+// pf_kernels.hip -- gfx950 kernels of the panorama-depth fusion path.
+//
+// Every kernel is HBM/L2-bandwidth or VALU bound; there is no dense contraction, so no MFMA.
+// Layout: batch-major planes, row-major pixels; one workgroup-grid dimension walks pixels
+// (coalesced 64-lane rows), grid.y walks the batch (or the tile for per-tile work).
+#include "pf_internal.hpp"
+
+#include <cfloat>
+
+namespace pf {
+
+static constexpr int kBlock = 256;
+
+__device__ __forceinline__ float bits_f(uint32_t u) { return __uint_as_float(u); }
+__device__ __forceinline__ uint32_t f_bits(float f) { return __float_as_uint(f); }
+
+// ---------------------------------------------------------------------------------------------
+// Level-0 seed (Depth.cpp:1442-1465): rows [h0,h1] take ValueAtCoord of the pixel's spherical
+// coordinate, other rows 0.
+__global__ void __launch_bounds__(kBlock) k_seed0(const float* __restrict__ emap, int ew, int eh,
+                                                  int ec, long long estride,
+                                                  const GridCol* __restrict__ cols,
+                                                  const GridRow* __restrict__ rows,
+                                                  LevelDims L, float* __restrict__ buf,
+                                                  long long bstride)
+{
+    long long i = (long long)blockIdx.x * kBlock + threadIdx.x;
+    long long n = (long long)L.w * L.h;
+    if (i >= n) return;
+    int b = blockIdx.y;
+    int y = (int)(i / L.w), x = (int)(i - (long long)y * L.w);
+    float v = 0.0f;
+    if (y >= L.h0 && y <= L.h1) {
+        long long e = emap_index(cols[x + 1].az, rows[y + 1].zen, ew, eh, ec);
+        v = emap[b * estride + e];
+    }
+    buf[b * bstride + i] = v;
+}
+
+// Nearest 2x upsample of the previous level (Depth.cpp:1467-1485).
+__global__ void __launch_bounds__(kBlock) k_upsample(const float* __restrict__ prev,
+                                                     long long pstride, LevelDims L,
+                                                     float* __restrict__ buf, long long bstride)
+{
+    long long i = (long long)blockIdx.x * kBlock + threadIdx.x;
+    long long n = (long long)L.w * L.h;
+    if (i >= n) return;
+    int b = blockIdx.y;
+    int y = (int)(i / L.w), x = (int)(i - (long long)y * L.w);
+    int wp = L.w / 2;
+    buf[b * bstride + i] = prev[b * pstride + (long long)(y / 2) * wp + x / 2];
+}
+
+// ---------------------------------------------------------------------------------------------
+// Laplacian target of tile p at pixel (X, Y): the 5-point mask in std::map key order
+// (X-1,Y), (X,Y-1), (X,Y), (X,Y+1), (X+1,Y) with weights -1/4,-1/4,1,-1/4,-1/4, each tap
+// projected through SphericalTo2D and read with Value() (Depth.cpp:1570-1606).  A tap whose
+// linear index leaves the tile is clamped (the reference reads out of bounds there).
+__device__ __forceinline__ float tap_value(const TileGeom& g, const float* __restrict__ tile,
+                                           const GridCol& c, const GridRow& r, bool xform,
+                                           float4 abcd)
+{
+    float x, y;
+    sph_to_2d(g, r.sz, r.cz, c.ca, c.sa, x, y);
+    long long idx = tile_index(g, x, y);
+    long long lim = (long long)g.w * g.h * g.c;
+    if (idx < 0) idx = 0;
+    if (idx >= lim) idx = lim - g.c;
+    float v = tile[idx];
+    if (xform) v = cubic_map(v, abcd.x, abcd.y, abcd.z, abcd.w);
+    return v;
+}
+
+__device__ __forceinline__ float target_one(const TileGeom& g, const float* __restrict__ tile,
+                                            const GridCol* __restrict__ cols,
+                                            const GridRow* __restrict__ rows, int X, int Y,
+                                            bool xform, float4 abcd)
+{
+    float Lp = 0;
+    Lp += tap_value(g, tile, cols[X], rows[Y + 1], xform, abcd) * -0.25f;      // (X-1, Y)
+    Lp += tap_value(g, tile, cols[X + 1], rows[Y], xform, abcd) * -0.25f;      // (X, Y-1)
+    Lp += tap_value(g, tile, cols[X + 1], rows[Y + 1], xform, abcd) * 1.0f;    // (X, Y)
+    Lp += tap_value(g, tile, cols[X + 1], rows[Y + 2], xform, abcd) * -0.25f;  // (X, Y+1)
+    Lp += tap_value(g, tile, cols[X + 2], rows[Y + 1], xform, abcd) * -0.25f;  // (X+1, Y)
+    return Lp;
+}
+
+// X iterates x0, x0+xs, ... and stops before x1 (Depth.cpp:1565-1623).
+__device__ __forceinline__ bool in_box(const TileBox& bx, int X, int Y)
+{
+    if (Y < bx.y0 || Y > bx.y1) return false;
+    return bx.xs > 0 ? (X >= bx.x0 && X < bx.x1) : (X <= bx.x0 && X > bx.x1);
+}
+
+// Targets + normalisation for the band rows [h0, h1] (Depth.cpp:1487-1647).  Gather form of
+// the reference's scatter: each pixel visits the tiles in index order, which is the reference's
+// single-thread accumulation order (and bit-identical to any order for coverage <= 2).
+// Output: normalised target, or PF_NAN_MARKER for an un-windowed pixel.
+__global__ void __launch_bounds__(kBlock) k_targets(const TileGeom* __restrict__ geom,
+                                                    const TileBox* __restrict__ box, int t0,
+                                                    int t1, const GridCol* __restrict__ cols,
+                                                    const GridRow* __restrict__ rows,
+                                                    const float* __restrict__ tiles,
+                                                    long long tstride,
+                                                    const float* __restrict__ coeffs,
+                                                    int ntiles_total, LevelDims L,
+                                                    float* __restrict__ lnorm,
+                                                    long long lstride)
+{
+    long long i = (long long)blockIdx.x * kBlock + threadIdx.x;
+    long long nband = (long long)L.w * (L.h1 - L.h0 + 1);
+    if (i >= nband) return;
+    int b = blockIdx.y;
+    int Y = (int)(i / L.w) + L.h0, X = (int)(i - (long long)(Y - L.h0) * L.w);
+    const float* tb = tiles + b * tstride;
+    float acc = 0.0f;
+    int n = 0;
+    if (Y > L.h0 && Y < L.h1) {
+        for (int p = t0; p < t1; p++) {
+            TileBox bx = box[p];
+            if (!in_box(bx, X, Y)) continue;
+            const TileGeom& g = geom[p];
+            float4 abcd = make_float4(0, 0, 0, 0);
+            bool xf = coeffs != nullptr;
+            if (xf) abcd = *reinterpret_cast<const float4*>(coeffs + ((long long)b * ntiles_total + p) * 4);
+            acc += target_one(g, tb + g.off, cols, rows, X, Y, xf, abcd);
+            n++;
+        }
+    }
+    float out;
+    if (n == 0) out = bits_f(PF_NAN_MARKER);
+    else if (n == 1) out = acc;
+    else {
+        float center = 0.0f;
+        for (int k = 0; k < n; k++) center += 1.0f;
+        out = acc * (1.0f / center);
+    }
+    lnorm[b * lstride + (long long)Y * L.w + X] = out;
+}
+
+// Partial scatter for the sharded single-panorama case: (sum L, n) of tiles [t0, t1).
+__global__ void __launch_bounds__(kBlock) k_targets_partial(
+    const TileGeom* __restrict__ geom, const TileBox* __restrict__ box, int t0, int t1,
+    const GridCol* __restrict__ cols, const GridRow* __restrict__ rows,
+    const float* __restrict__ tiles, const float* __restrict__ coeffs, LevelDims L,
+    float* __restrict__ lsum, float* __restrict__ cnt)
+{
+    long long i = (long long)blockIdx.x * kBlock + threadIdx.x;
+    long long nband = (long long)L.w * (L.h1 - L.h0 + 1);
+    if (i >= nband) return;
+    int Y = (int)(i / L.w) + L.h0, X = (int)(i - (long long)(Y - L.h0) * L.w);
+    float acc = 0.0f, n = 0.0f;
+    if (Y > L.h0 && Y < L.h1) {
+        for (int p = t0; p < t1; p++) {
+            TileBox bx = box[p];
+            if (!in_box(bx, X, Y)) continue;
+            const TileGeom& g = geom[p];
+            float4 abcd = make_float4(0, 0, 0, 0);
+            bool xf = coeffs != nullptr;
+            if (xf) abcd = *reinterpret_cast<const float4*>(coeffs + (long long)p * 4);
+            acc += target_one(g, tiles + g.off, cols, rows, X, Y, xf, abcd);
+            n += 1.0f;
+        }
+    }
+    long long o = (long long)Y * L.w + X;
+    lsum[o] = acc;
+    cnt[o] = n;
+}
+
+__global__ void __launch_bounds__(kBlock) k_normalize(const float* __restrict__ lsum,
+                                                      const float* __restrict__ cnt,
+                                                      LevelDims L, float* __restrict__ lnorm)
+{
+    long long i = (long long)blockIdx.x * kBlock + threadIdx.x;
+    long long nband = (long long)L.w * (L.h1 - L.h0 + 1);
+    if (i >= nband) return;
+    long long o = (long long)L.h0 * L.w + i;
+    int Y = (int)(o / L.w);
+    float n = cnt[o];
+    float out;
+    if (Y <= L.h0 || Y >= L.h1 || n == 0.0f) out = bits_f(PF_NAN_MARKER);
+    else if (n == 1.0f) out = lsum[o];
+    else out = lsum[o] * (1.0f / n);
+    lnorm[o] = out;
+}
+
+// Parity probe: linear tile index of each tap of the first covering tile.
+__global__ void __launch_bounds__(kBlock) k_probe_taps(const TileGeom* __restrict__ geom,
+                                                       const TileBox* __restrict__ box,
+                                                       int ntiles,
+                                                       const GridCol* __restrict__ cols,
+                                                       const GridRow* __restrict__ rows,
+                                                       LevelDims L, int32_t* __restrict__ out)
+{
+    long long i = (long long)blockIdx.x * kBlock + threadIdx.x;
+    long long n = (long long)L.w * L.h;
+    if (i >= n) return;
+    int Y = (int)(i / L.w), X = (int)(i - (long long)Y * L.w);
+    int32_t r[5] = {-1, -1, -1, -1, -1};
+    if (Y > L.h0 && Y < L.h1) {
+        for (int p = 0; p < ntiles; p++) {
+            if (!in_box(box[p], X, Y)) continue;
+            const TileGeom& g = geom[p];
+            const int dc[5] = {0, 1, 1, 1, 2}, dr[5] = {1, 0, 1, 2, 1};
+            for (int k = 0; k < 5; k++) {
+                float x, y;
+                const GridCol& c = cols[X + dc[k]];
+                const GridRow& rr = rows[Y + dr[k]];
+                sph_to_2d(g, rr.sz, rr.cz, c.ca, c.sa, x, y);
+                r[k] = (int32_t)tile_index(g, x, y);
+            }
+            break;
+        }
+    }
+    for (int k = 0; k < 5; k++) out[i * 5 + k] = r[k];
+}
+
+// ---------------------------------------------------------------------------------------------
+// One damped Jacobi sweep over the band rows (Depth.cpp:1680-1717).  Taps are read by linear
+// index so the east tap of column w-1 is pixel (0, Y+1), exactly like buffer[yy*width+xx].
+__global__ void __launch_bounds__(kBlock) k_jacobi(const float* __restrict__ src,
+                                                   float* __restrict__ dst,
+                                                   const float* __restrict__ lnorm,
+                                                   long long stride, LevelDims L)
+{
+    long long i = (long long)blockIdx.x * kBlock + threadIdx.x;
+    long long nband = (long long)L.w * (L.h1 - L.h0 + 1);
+    if (i >= nband) return;
+    long long base = (long long)blockIdx.y * stride;
+    long long o = (long long)L.h0 * L.w + i;
+    const float* s = src + base;
+    float Lt = lnorm[base + o];
+    float b = s[o];
+    float cur = 0.0f, tgt = 0.0f;
+    if (f_bits(Lt) != PF_NAN_MARKER) {
+        tgt = Lt;
+        cur += s[o - 1] * -0.25f;
+        cur += s[o - L.w] * -0.25f;
+        cur += b * 1.0f;
+        cur += s[o + L.w] * -0.25f;
+        cur += s[o + 1] * -0.25f;
+    }
+    const float reg = (float)1e-4;
+    const float reg_ = 1 - reg;
+    float target_val = b + (tgt - cur) * 0.5f;
+    float v = target_val * reg_ + b * reg;
+    if (v < 0) v = 0;
+    else if (v > 1) v = 1;
+    dst[base + o] = v;
+}
+
+__global__ void __launch_bounds__(kBlock) k_quantize(const float* __restrict__ buf,
+                                                     long long bstride, int n,
+                                                     uint16_t* __restrict__ out,
+                                                     long long ostride)
+{
+    long long i = (long long)blockIdx.x * kBlock + threadIdx.x;
+    if (i >= n) return;
+    int b = blockIdx.y;
+    float v = buf[b * bstride + i];
+    if (v < 0) v = 0;
+    if (v > 1) v = 1;
+    out[b * ostride + i] = (uint16_t)(v * 65535.0f);
+}
+
+// ---------------------------------------------------------------------------------------------
+// Registration: one workgroup per (tile, panorama).  Lane l accumulates the 14 fp64 sums of
+// J^T J / J^T y over samples l, l+256, ... (J = (x^3, x^2, x, 1) of FunctorDepth2Depth3,
+// Depth.cpp:1122-1138), then a fixed pairwise tree; lane 0 solves the normal equations.  The
+// order is fixed, so the result is reproducible and identical to the oracle's restatement.
+static constexpr int kRegLanes = 256;
+static constexpr int kRegSums = 14;
+
+__device__ __forceinline__ double clamp_depth(double v)
+{
+    if (v < 1e-4) v = 1e-4;
+    else if (v > (1 - 1e-4)) v = 1 - 1e-4;
+    return v;
+}
+
+__device__ int solve_normal(const double* S, int degree, double* coef)
+{
+    const int idx[4][4] = {{0, 1, 2, 3}, {1, 4, 5, 6}, {2, 5, 7, 8}, {3, 6, 8, 9}};
+    int n = degree + 1, off = 3 - degree;
+    double A[4][5];
+    for (int i = 0; i < n; i++) {
+        for (int j = 0; j < n; j++) A[i][j] = S[idx[i + off][j + off]];
+        A[i][n] = S[10 + i + off];
+    }
+    for (int k = 0; k < n; k++) {
+        int piv = k;
+        double best = fabs(A[k][k]);
+        for (int i = k + 1; i < n; i++)
+            if (fabs(A[i][k]) > best) { best = fabs(A[i][k]); piv = i; }
+        if (!(best > 0.0)) return -1;
+        if (piv != k)
+            for (int j = 0; j <= n; j++) { double t = A[k][j]; A[k][j] = A[piv][j]; A[piv][j] = t; }
+        for (int i = k + 1; i < n; i++) {
+            double f = A[i][k] / A[k][k];
+            for (int j = k; j <= n; j++) A[i][j] = A[i][j] - f * A[k][j];
+        }
+    }
+    for (int i = n - 1; i >= 0; i--) {
+        double s = A[i][n];
+        for (int j = i + 1; j < n; j++) s = s - A[i][j] * coef[j];
+        coef[i] = s / A[i][i];
+    }
+    return 0;
+}
+
+__global__ void __launch_bounds__(kRegLanes) k_register(
+    const TileGeom* __restrict__ geom, const RegGrid* __restrict__ grids,
+    const GridCol* __restrict__ rcols, const GridRow* __restrict__ rrows, int ntiles,
+    const float* __restrict__ emap, int ew, int eh, int ec, long long estride,
+    const float* __restrict__ tiles, long long tstride, int degree, float* __restrict__ coeffs,
+    double* __restrict__ coeffs64)
+{
+    __shared__ double part[kRegSums][kRegLanes];
+    const int p = blockIdx.x, b = blockIdx.y, l = threadIdx.x;
+    const TileGeom g = geom[p];
+    const RegGrid rg = grids[p];
+    const float* tile = tiles + b * tstride + g.off;
+    const float* em = emap + b * estride;
+    const int ncol = rg.cols + 1;
+    const int ns = ncol * (rg.rows + 1);
+    double acc[kRegSums];
+#pragma unroll
+    for (int k = 0; k < kRegSums; k++) acc[k] = 0.0;
+    for (int s = l; s < ns; s += kRegLanes) {
+        int r = s / ncol, c = s - r * ncol;
+        const GridCol cc = rcols[rg.col_off + c];
+        const GridRow rr = rrows[rg.row_off + r];
+        float x, y;
+        sph_to_2d(g, rr.sz, rr.cz, cc.ca, cc.sa, x, y);
+        if (x < 0) x = 0;
+        if (x > 1) x = 1;
+        if (y < 0) y = 0;
+        if (y > 1) y = 1;
+        double X = clamp_depth((double)tile[tile_index(g, x, y)]);
+        double Yv = clamp_depth((double)em[emap_index(cc.az, rr.zen, ew, eh, ec)]);
+        double X2 = X * X, X3 = X * X * X;
+        acc[0] = acc[0] + X3 * X3; acc[1] = acc[1] + X3 * X2; acc[2] = acc[2] + X3 * X;
+        acc[3] = acc[3] + X3;      acc[4] = acc[4] + X2 * X2; acc[5] = acc[5] + X2 * X;
+        acc[6] = acc[6] + X2;      acc[7] = acc[7] + X * X;   acc[8] = acc[8] + X;
+        acc[9] = acc[9] + 1.0;
+        acc[10] = acc[10] + X3 * Yv; acc[11] = acc[11] + X2 * Yv; acc[12] = acc[12] + X * Yv;
+        acc[13] = acc[13] + Yv;
+    }
+#pragma unroll
+    for (int k = 0; k < kRegSums; k++) part[k][l] = acc[k];
+    __syncthreads();
+    for (int stride = kRegLanes / 2; stride >= 1; stride >>= 1) {
+        if (l < stride)
+            for (int k = 0; k < kRegSums; k++) part[k][l] = part[k][l] + part[k][l + stride];
+        __syncthreads();
+    }
+    if (l == 0) {
+        double S[kRegSums];
+        for (int k = 0; k < kRegSums; k++) S[k] = part[k][0];
+        double coef[4] = {0, 0, 0, 0};
+        int d = degree, rc = -1;
+        while (d >= 0 && (rc = solve_normal(S, d, coef)) != 0) d--;
+        if (rc != 0) { coef[0] = 0.0; d = 0; }
+        double full[4] = {0, 0, 0, 0};
+        for (int i = 0; i <= d; i++) full[3 - d + i] = coef[i];
+        long long o = ((long long)b * ntiles + p) * 4;
+        for (int i = 0; i < 4; i++) {
+            if (coeffs) coeffs[o + i] = (float)full[i];
+            if (coeffs64) coeffs64[o + i] = full[i];
+        }
+    }
+}
+
+// Depth2DepthTransform on all tiles (channel 0), in place.
+__global__ void __launch_bounds__(kBlock) k_apply_cubic(const TileGeom* __restrict__ geom,
+                                                        int ntiles, float* __restrict__ tiles,
+                                                        long long tstride,
+                                                        const float* __restrict__ coeffs)
+{
+    const int p = blockIdx.y, b = blockIdx.z;
+    const TileGeom g = geom[p];
+    long long npx = (long long)g.w * g.h;
+    const float4 abcd = *reinterpret_cast<const float4*>(coeffs + ((long long)b * ntiles + p) * 4);
+    float* t = tiles + b * tstride + g.off;
+    for (long long i = (long long)blockIdx.x * kBlock + threadIdx.x; i < npx;
+         i += (long long)gridDim.x * kBlock)
+        t[i * g.c] = cubic_map(t[i * g.c], abcd.x, abcd.y, abcd.z, abcd.w);
+}
+
+// ---------------------------------------------------------------------------------------------
+// E->P depth warp (a5 mapping).  The spherical coordinate of a tile pixel does not depend on
+// the panorama, so each thread computes it once and loops over the batch.
+__device__ __forceinline__ void world_to_sph(float p0, float p1, float p2, float& az,
+                                             float& zen)
+{  // Depth.cpp:2960-2971, Imath normalize/length; atan2 evaluated in fp64 and rounded
+    float l2 = p0 * p0 + p1 * p1 + p2 * p2;
+    float l;
+    if (l2 < 2.0f * FLT_MIN) {
+        float ax = fabsf(p0), ay = fabsf(p1), az_ = fabsf(p2);
+        float mx = ax;
+        if (mx < ay) mx = ay;
+        if (mx < az_) mx = az_;
+        if (mx == 0.0f) l = 0.0f;
+        else { ax /= mx; ay /= mx; az_ /= mx; l = mx * sqrtf(ax * ax + ay * ay + az_ * az_); }
+    } else
+        l = sqrtf(l2);
+    if (l != 0.0f) { p0 /= l; p1 /= l; p2 /= l; }
+    float a = (float)atan2((double)p1, (double)p0);
+    float azf = (float)fmod((double)a, 2 * PF_MYPI);
+    if (azf < 0) azf = (float)((double)azf + 2 * PF_MYPI);
+    float q2 = p0 * p0 + p1 * p1;
+    float ql;
+    if (q2 < 2.0f * FLT_MIN) {
+        float ax = fabsf(p0), ay = fabsf(p1);
+        float mx = ax < ay ? ay : ax;
+        if (mx == 0.0f) ql = 0.0f;
+        else { ax /= mx; ay /= mx; ql = mx * sqrtf(ax * ax + ay * ay); }
+    } else
+        ql = sqrtf(q2);
+    az = azf;
+    zen = (float)atan2((double)ql, (double)p2);
+}
+
+__device__ __forceinline__ uint32_t hash32(uint32_t seed, uint32_t tile, uint32_t idx)
+{
+    uint64_t z = ((uint64_t)seed << 32) ^ ((uint64_t)tile << 24) ^ (uint64_t)idx;
+    z += 0x9E3779B97F4A7C15ull;
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    z ^= z >> 31;
+    return (uint32_t)(z >> 32);
+}
+
+__global__ void __launch_bounds__(kBlock) k_warp_depth(const TileGeom* __restrict__ geom,
+                                                       int ntiles, const float* __restrict__ pano,
+                                                       int pw, int ph, long long pstride,
+                                                       const Resp* __restrict__ resp,
+                                                       float* __restrict__ tiles,
+                                                       long long tstride, int batch)
+{
+    const int p = blockIdx.y;
+    const TileGeom g = geom[p];
+    long long npx = (long long)g.w * g.h;
+    long long i = (long long)blockIdx.x * kBlock + threadIdx.x;
+    if (i >= npx) return;
+    int Y = (int)(i / g.w), X = (int)(i - (long long)Y * g.w);
+    float xf = (float)X / (float)(g.w - 1), yf = (float)Y / (float)(g.h - 1);
+    float q0 = g.corner0[0] + g.hedge[0] * xf, q1 = g.corner0[1] + g.hedge[1] * xf,
+          q2 = g.corner0[2] + g.hedge[2] * xf;
+    q0 = q0 + g.vedge[0] * yf; q1 = q1 + g.vedge[1] * yf; q2 = q2 + g.vedge[2] * yf;
+    float az, zen;
+    world_to_sph(q0, q1, q2, az, zen);
+    float px = (float)((double)az / (2 * PF_MYPI) * (double)(pw - 1));
+    float py = (float)((double)zen / PF_MYPI * (double)(ph - 1));
+    int x0 = (int)floorf(px), y0 = (int)floorf(py);
+    float fx = px - (float)x0, fy = py - (float)y0;
+    if (x0 < 0) { x0 = 0; fx = 0; }
+    if (y0 < 0) { y0 = 0; fy = 0; }
+    if (x0 > pw - 1) { x0 = pw - 1; fx = 0; }
+    if (y0 > ph - 1) { y0 = ph - 1; fy = 0; }
+    int x1 = x0 + 1 < pw ? x0 + 1 : pw - 1;
+    int y1 = y0 + 1 < ph ? y0 + 1 : ph - 1;
+    long long o00 = (long long)y0 * pw + x0, o01 = (long long)y0 * pw + x1;
+    long long o10 = (long long)y1 * pw + x0, o11 = (long long)y1 * pw + x1;
+    float wx0 = 1.0f - fx, wy0 = 1.0f - fy;
+    for (int b = 0; b < batch; b++) {
+        const float* pp = pano + b * pstride;
+        float top = pp[o00] * wx0 + pp[o01] * fx;
+        float bot = pp[o10] * wx0 + pp[o11] * fx;
+        float v = top * wy0 + bot * fy;
+        if (resp) {
+            const Resp r = resp[(long long)b * ntiles + p];
+            uint32_t h = hash32(r.seed, (uint32_t)p, (uint32_t)i);
+            float u = (float)(h >> 8) * (1.0f / 16777216.0f);
+            float nz = u * 2.0f - 1.0f;
+            float t = r.alpha * v;
+            t = t + (r.kappa * v) * v;
+            t = t + r.beta;
+            t = t + r.sigma * nz;
+            if (t < 0) t = 0;
+            else if (t > 1) t = 1;
+            v = t;
+        }
+        tiles[b * tstride + g.off + i * g.c] = v;
+    }
+}
+
+// E->P RGB warp with the GL camera (a18).
+__global__ void __launch_bounds__(kBlock) k_warp_rgb(const RgbCam* __restrict__ cams,
+                                                     const TileGeom* __restrict__ geom,
+                                                     const long long* __restrict__ rgb_off,
+                                                     const uint8_t* __restrict__ pano, int pw,
+                                                     int ph, long long pstride,
+                                                     uint8_t* __restrict__ tiles,
+                                                     long long tstride, int batch)
+{
+    const int p = blockIdx.y;
+    const int W = geom[p].w, H = geom[p].h;
+    long long i = (long long)blockIdx.x * kBlock + threadIdx.x;
+    if (i >= (long long)W * H) return;
+    const RgbCam cam = cams[p];
+    int r = (int)(i / W), c = (int)(i - (long long)r * W);
+    double xn = 2.0 * (c + 0.5) / W - 1.0, yn = 1.0 - 2.0 * (r + 0.5) / H;
+    double d[3];
+    for (int k = 0; k < 3; k++) d[k] = cam.f[k] + cam.s[k] * (xn * cam.tx) + cam.u[k] * (yn * cam.ty);
+    double az = fmod(atan2(d[1], d[0]), 2 * PF_MYPI);
+    if (az < 0) az += 2 * PF_MYPI;
+    double zen = atan2(sqrt(d[0] * d[0] + d[1] * d[1]), d[2]);
+    float uu = (float)(az / (2 * PF_MYPI)), vv = (float)(zen / PF_MYPI);
+    float sx = uu * (float)pw - 0.5f, sy = vv * (float)ph - 0.5f;
+    int ix = (int)floorf(sx), iy = (int)floorf(sy);
+    float ax = sx - (float)ix, ay = sy - (float)iy;
+    int ix0 = ((ix % pw) + pw) % pw, ix1 = (((ix + 1) % pw) + pw) % pw;
+    int iy0 = ((iy % ph) + ph) % ph, iy1 = (((iy + 1) % ph) + ph) % ph;
+    long long a00 = ((long long)iy0 * pw + ix0) * 3, a01 = ((long long)iy0 * pw + ix1) * 3;
+    long long a10 = ((long long)iy1 * pw + ix0) * 3, a11 = ((long long)iy1 * pw + ix1) * 3;
+    for (int b = 0; b < batch; b++) {
+        const uint8_t* pp = pano + b * pstride;
+        uint8_t* out = tiles + b * tstride + rgb_off[p] + i * 3;
+        for (int ch = 0; ch < 3; ch++) {
+            float t00 = pp[a00 + ch], t01 = pp[a01 + ch], t10 = pp[a10 + ch], t11 = pp[a11 + ch];
+            float top = t00 * (1.0f - ax) + t01 * ax;
+            float bot = t10 * (1.0f - ax) + t11 * ax;
+            float v = top * (1.0f - ay) + bot * ay;
+            int q = (int)floorf(v + 0.5f);
+            q = q < 0 ? 0 : (q > 255 ? 255 : q);
+            out[ch] = (uint8_t)q;
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------------------------
+// Launchers.
+static inline unsigned nblocks(long long n) { return (unsigned)((n + kBlock - 1) / kBlock); }
+
+void launch_seed0(hipStream_t s, const float* emap, int ew, int eh, int ec, long long estride,
+                  const GridCol* cols, const GridRow* rows, LevelDims L, float* buf,
+                  long long bstride, int batch)
+{
+    dim3 grid(nblocks((long long)L.w * L.h), batch);
+    hipLaunchKernelGGL(k_seed0, grid, dim3(kBlock), 0, s, emap, ew, eh, ec, estride, cols, rows,
+                       L, buf, bstride);
+}
+
+void launch_upsample(hipStream_t s, const float* prev, long long pstride, LevelDims L,
+                     float* buf, long long bstride, int batch)
+{
+    dim3 grid(nblocks((long long)L.w * L.h), batch);
+    hipLaunchKernelGGL(k_upsample, grid, dim3(kBlock), 0, s, prev, pstride, L, buf, bstride);
+}
+
+void launch_targets(hipStream_t s, const TileGeom* geom, const TileBox* box, int t0, int t1,
+                    const GridCol* cols, const GridRow* rows, const float* tiles,
+                    long long tstride, const float* coeffs, int ntiles_total, LevelDims L,
+                    float* lnorm, long long lstride, int batch)
+{
+    dim3 grid(nblocks((long long)L.w * (L.h1 - L.h0 + 1)), batch);
+    hipLaunchKernelGGL(k_targets, grid, dim3(kBlock), 0, s, geom, box, t0, t1, cols, rows, tiles,
+                       tstride, coeffs, ntiles_total, L, lnorm, lstride);
+}
+
+void launch_targets_partial(hipStream_t s, const TileGeom* geom, const TileBox* box, int t0,
+                            int t1, const GridCol* cols, const GridRow* rows,
+                            const float* tiles, const float* coeffs, LevelDims L, float* lsum,
+                            float* cnt)
+{
+    dim3 grid(nblocks((long long)L.w * (L.h1 - L.h0 + 1)));
+    hipLaunchKernelGGL(k_targets_partial, grid, dim3(kBlock), 0, s, geom, box, t0, t1, cols,
+                       rows, tiles, coeffs, L, lsum, cnt);
+}
+
+void launch_normalize(hipStream_t s, const float* lsum, const float* cnt, LevelDims L,
+                      float* lnorm)
+{
+    dim3 grid(nblocks((long long)L.w * (L.h1 - L.h0 + 1)));
+    hipLaunchKernelGGL(k_normalize, grid, dim3(kBlock), 0, s, lsum, cnt, L, lnorm);
+}
+
+void launch_probe_taps(hipStream_t s, const TileGeom* geom, const TileBox* box, int ntiles,
+                       const GridCol* cols, const GridRow* rows, LevelDims L, int32_t* out)
+{
+    dim3 grid(nblocks((long long)L.w * L.h));
+    hipLaunchKernelGGL(k_probe_taps, grid, dim3(kBlock), 0, s, geom, box, ntiles, cols, rows, L,
+                       out);
+}
+
+void launch_jacobi(hipStream_t s, float* buf_a, float* buf_b, const float* lnorm,
+                   long long stride, LevelDims L, int iters, int batch, float** result)
+{
+    dim3 grid(nblocks((long long)L.w * (L.h1 - L.h0 + 1)), batch);
+    float* src = buf_a;
+    float* dst = buf_b;
+    for (int it = 0; it < iters; it++) {
+        hipLaunchKernelGGL(k_jacobi, grid, dim3(kBlock), 0, s, src, dst, lnorm, stride, L);
+        float* t = src;
+        src = dst;
+        dst = t;
+    }
+    *result = src;
+}
+
+void launch_quantize(hipStream_t s, const float* buf, long long bstride, int n, uint16_t* out,
+                     long long ostride, int batch)
+{
+    dim3 grid(nblocks(n), batch);
+    hipLaunchKernelGGL(k_quantize, grid, dim3(kBlock), 0, s, buf, bstride, n, out, ostride);
+}
+
+void launch_register(hipStream_t s, const TileGeom* geom, const RegGrid* grids,
+                     const GridCol* rcols, const GridRow* rrows, int ntiles, const float* emap,
+                     int ew, int eh, int ec, long long estride, const float* tiles,
+                     long long tstride, int degree, float* coeffs, double* coeffs64, int batch)
+{
+    dim3 grid(ntiles, batch);
+    hipLaunchKernelGGL(k_register, grid, dim3(kRegLanes), 0, s, geom, grids, rcols, rrows,
+                       ntiles, emap, ew, eh, ec, estride, tiles, tstride, degree, coeffs,
+                       coeffs64);
+}
+
+void launch_apply_cubic(hipStream_t s, const TileGeom* geom, int ntiles, long long tile_elems,
+                        float* tiles, long long tstride, const float* coeffs, int batch)
+{
+    long long per = tile_elems / (ntiles > 0 ? ntiles : 1);
+    unsigned gx = nblocks(per);
+    if (gx > 1024) gx = 1024;
+    if (gx == 0) gx = 1;
+    dim3 grid(gx, ntiles, batch);
+    hipLaunchKernelGGL(k_apply_cubic, grid, dim3(kBlock), 0, s, geom, ntiles, tiles, tstride,
+                       coeffs);
+}
+
+void launch_warp_depth(hipStream_t s, const TileGeom* geom, int ntiles, long long npix_max,
+                       const float* pano, int pw, int ph, long long pstride, const Resp* resp,
+                       float* tiles, long long tstride, int batch)
+{
+    dim3 grid(nblocks(npix_max), ntiles);
+    hipLaunchKernelGGL(k_warp_depth, grid, dim3(kBlock), 0, s, geom, ntiles, pano, pw, ph,
+                       pstride, resp, tiles, tstride, batch);
+}
+
+void launch_warp_rgb(hipStream_t s, const RgbCam* cams, const TileGeom* geom, int ntiles,
+                     long long npix_max, const long long* pix_prefix, const long long* rgb_off,
+                     const uint8_t* pano, int pw, int ph, long long pstride, uint8_t* tiles,
+                     long long tstride, int batch)
+{
+    (void)pix_prefix;
+    dim3 grid(nblocks(npix_max), ntiles);
+    hipLaunchKernelGGL(k_warp_rgb, grid, dim3(kBlock), 0, s, cams, geom, rgb_off, pano, pw, ph,
+                       pstride, tiles, tstride, batch);
+}
+
+}  // namespace pf

@@ -1,0 +1,245 @@
+"""Python host binding of libpanofuse (include/panofuse.h) over ctypes.
+
+This is the host-side mirror of the reference's DepthNamespace entry points for the fused path
+(``Depth.h:286-307``): ``Fuser.register`` ~ SolveDepthToDepth + Depth2DepthTransform,
+``Fuser.fuse`` ~ SolveDepthAll, ``Fuser.merge`` ~ MergeDepthMaps' compute core.  Tensors are
+torch device tensors (PyTorch is used only for device memory and streams); the compute is the
+hand-written HIP in csrc/.  There is no CPU fallback: if lib/libpanofuse.so is missing or no GPU
+is present, every call raises.
+"""
+import ctypes as C
+import os
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "lib", "libpanofuse.so")
+
+PF_OK, PF_EINVAL, PF_ENOMEM, PF_EHIP, PF_ESTATE, PF_EDEGENERATE = 0, -1, -2, -3, -4, -5
+
+# Every symbol declared in include/panofuse.h.
+EXPORTS = [
+    "pf_create", "pf_destroy", "pf_last_error", "pf_set_stream", "pf_synchronize",
+    "pf_version", "pf_set_tiles", "pf_register", "pf_fuse", "pf_merge", "pf_warp_depth",
+    "pf_warp_rgb", "pf_level_info", "pf_fuse_partial", "pf_fuse_seed", "pf_fuse_finish_level",
+    "pf_probe_taps", "pf_profile_enable", "pf_profile_read",
+]
+
+STAGES = ["warp", "register", "seed", "targets", "jacobi", "quantize"]
+
+
+class PanofuseError(RuntimeError):
+    def __init__(self, code, msg):
+        super().__init__(f"panofuse error {code}: {msg}")
+        self.code = code
+
+
+class Window(C.Structure):
+    _fields_ = [("az_left", C.c_float), ("az_right", C.c_float),
+                ("zen_top", C.c_float), ("zen_down", C.c_float)]
+
+
+class Response(C.Structure):
+    _fields_ = [("alpha", C.c_float), ("kappa", C.c_float), ("beta", C.c_float),
+                ("sigma", C.c_float), ("seed", C.c_uint32), ("pad", C.c_uint32)]
+
+
+_lib = None
+
+
+def load():
+    """Load libpanofuse.so; raises if it was not built (no fallback path exists)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise RuntimeError(f"libpanofuse.so not built at {LIB_PATH}: run "
+                           f"`python -c 'import __graft_entry__ as g; g.build()'`")
+    L = C.CDLL(LIB_PATH)
+    vp, fp, ip = C.c_void_p, C.c_float, C.c_int
+    L.pf_create.argtypes = [ip, C.POINTER(vp)]
+    L.pf_destroy.argtypes = [vp]
+    L.pf_destroy.restype = None
+    L.pf_last_error.argtypes = [vp]
+    L.pf_last_error.restype = C.c_char_p
+    L.pf_set_stream.argtypes = [vp, vp]
+    L.pf_synchronize.argtypes = [vp]
+    L.pf_version.restype = C.c_char_p
+    L.pf_set_tiles.argtypes = [vp, C.POINTER(Window), C.POINTER(Window), ip,
+                               C.POINTER(C.c_int), C.POINTER(C.c_int), ip, ip]
+    L.pf_register.argtypes = [vp, vp, ip, ip, ip, vp, ip, fp, fp, ip, ip, vp, vp]
+    L.pf_fuse.argtypes = [vp, vp, ip, ip, ip, vp, vp, ip, ip, ip, fp, fp, vp]
+    L.pf_merge.argtypes = [vp, vp, ip, ip, ip, vp, ip, ip, fp, fp, vp, vp]
+    L.pf_warp_depth.argtypes = [vp, vp, ip, ip, ip, vp, vp]
+    L.pf_warp_rgb.argtypes = [vp, vp, ip, ip, ip, vp]
+    L.pf_level_info.argtypes = [ip, ip, fp, fp, ip] + [C.POINTER(C.c_int)] * 6
+    L.pf_fuse_partial.argtypes = [vp, vp, vp, ip, ip, ip, ip, fp, fp, ip, vp, vp]
+    L.pf_fuse_seed.argtypes = [vp, vp, ip, ip, ip, vp, ip, ip, fp, fp, ip, vp]
+    L.pf_fuse_finish_level.argtypes = [vp, vp, vp, ip, ip, fp, fp, ip, vp, vp]
+    L.pf_probe_taps.argtypes = [vp, ip, ip, fp, fp, ip, vp]
+    L.pf_profile_enable.argtypes = [vp, ip]
+    L.pf_profile_read.argtypes = [vp, C.POINTER(C.c_double), C.POINTER(C.c_double),
+                                  C.POINTER(C.c_longlong)]
+    for name in EXPORTS:
+        if not hasattr(L, name):
+            raise RuntimeError(f"libpanofuse.so lacks {name}")
+    _lib = L
+    return L
+
+
+def level_info(out_w, out_h, zr, level):
+    """(w, h, h0, h1, iters, nlevels) of a fusion level (Depth.cpp:1420-1437, 1650-1675)."""
+    vals = [C.c_int(0) for _ in range(6)]
+    rc = load().pf_level_info(out_w, out_h, float(zr[0]), float(zr[1]), level,
+                              *[C.byref(v) for v in vals])
+    if rc != PF_OK:
+        raise PanofuseError(rc, "pf_level_info")
+    return tuple(v.value for v in vals)
+
+
+def _ptr(t):
+    if t is None:
+        return None
+    if not t.is_cuda:
+        raise ValueError("panofuse takes device tensors only")
+    if not t.is_contiguous():
+        raise ValueError("panofuse takes contiguous tensors")
+    return C.c_void_p(t.data_ptr())
+
+
+def _emap_dims(emap):
+    # emap: [B, eh, ew] or [B, eh, ew, ec]
+    if emap.dim() == 3:
+        return emap.shape[2], emap.shape[1], 1
+    return emap.shape[2], emap.shape[1], emap.shape[3]
+
+
+class Fuser:
+    """One context = one device + one stream (pf_ctx)."""
+
+    def __init__(self, device=0, stream=None):
+        import torch
+        if not torch.cuda.is_available():
+            raise RuntimeError("panofuse needs a ROCm GPU (torch.cuda.is_available() is False)")
+        self.L = load()
+        self.device = device
+        h = C.c_void_p()
+        rc = self.L.pf_create(device, C.byref(h))
+        if rc != PF_OK:
+            raise PanofuseError(rc, "pf_create failed")
+        self.h = h
+        self.layout = None
+        self.set_stream(stream)
+
+    def set_stream(self, stream=None):
+        import torch
+        if stream is None:
+            stream = torch.cuda.current_stream(self.device)
+        self.stream = stream
+        self._check(self.L.pf_set_stream(self.h, C.c_void_p(stream.cuda_stream)))
+
+    def close(self):
+        if getattr(self, "h", None):
+            self.L.pf_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def _check(self, rc):
+        if rc != PF_OK:
+            raise PanofuseError(rc, self.L.pf_last_error(self.h).decode())
+
+    def set_tiles(self, layout, channels=1, cap_ranges=True):
+        n = layout.ntiles
+        fov = (Window * n)(*[Window(*map(float, layout.fovs[i])) for i in range(n)])
+        rng = (Window * n)(*[Window(*map(float, layout.ranges[i])) for i in range(n)])
+        tw = (C.c_int * n)(*[int(v) for v in layout.tile_w])
+        th = (C.c_int * n)(*[int(v) for v in layout.tile_h])
+        self._check(self.L.pf_set_tiles(self.h, fov, rng, n, tw, th, channels,
+                                        1 if cap_ranges else 0))
+        self.layout = layout
+        self.channels = channels
+        self.tile_elems = int(sum(int(layout.tile_w[i]) * int(layout.tile_h[i])
+                                  for i in range(n))) * channels
+
+    def register(self, emap, tiles, zr, degree=3, apply=True, coeffs=None, coeffs64=None):
+        ew, eh, ec = _emap_dims(emap)
+        B = emap.shape[0]
+        self._check(self.L.pf_register(self.h, _ptr(emap), ew, eh, ec, _ptr(tiles), B,
+                                       float(zr[0]), float(zr[1]), degree, 1 if apply else 0,
+                                       _ptr(coeffs), _ptr(coeffs64)))
+
+    def fuse(self, emap, tiles, out, zr, coeffs=None):
+        ew, eh, ec = _emap_dims(emap)
+        B, oh, ow = out.shape
+        self._check(self.L.pf_fuse(self.h, _ptr(emap), ew, eh, ec, _ptr(tiles), _ptr(coeffs),
+                                   B, ow, oh, float(zr[0]), float(zr[1]), _ptr(out)))
+
+    def merge(self, emap, tiles, out, zr, coeffs=None):
+        ew, eh, ec = _emap_dims(emap)
+        B, oh, ow = out.shape
+        if oh != ow // 2:
+            raise ValueError("MergeDepthMaps output height is out_w/2")
+        self._check(self.L.pf_merge(self.h, _ptr(emap), ew, eh, ec, _ptr(tiles), B, ow,
+                                    float(zr[0]), float(zr[1]), _ptr(coeffs), _ptr(out)))
+
+    def warp_depth(self, pano, tiles, resp=None):
+        B, ph, pw = pano.shape
+        self._check(self.L.pf_warp_depth(self.h, _ptr(pano), pw, ph, B, _ptr(resp),
+                                         _ptr(tiles)))
+
+    def warp_rgb(self, pano, tiles):
+        B, ph, pw, _ = pano.shape
+        self._check(self.L.pf_warp_rgb(self.h, _ptr(pano), pw, ph, B, _ptr(tiles)))
+
+    def probe_taps(self, out_w, zr, level):
+        import torch
+        w, h = level_info(out_w, out_w // 2, zr, level)[:2]
+        out = torch.empty((h, w, 5), dtype=torch.int32, device=f"cuda:{self.device}")
+        self._check(self.L.pf_probe_taps(self.h, out_w, out_w // 2, float(zr[0]), float(zr[1]),
+                                         level, _ptr(out)))
+        return out
+
+    def fuse_partial(self, tiles, coeffs, t0, t1, out_w, zr, level, lsum, cnt):
+        self._check(self.L.pf_fuse_partial(self.h, _ptr(tiles), _ptr(coeffs), t0, t1, out_w,
+                                           out_w // 2, float(zr[0]), float(zr[1]), level,
+                                           _ptr(lsum), _ptr(cnt)))
+
+    def fuse_seed(self, emap, prev, out_w, zr, level, buf):
+        ew, eh, ec = _emap_dims(emap) if emap is not None else (0, 0, 0)
+        self._check(self.L.pf_fuse_seed(self.h, _ptr(emap), ew, eh, ec, _ptr(prev), out_w,
+                                        out_w // 2, float(zr[0]), float(zr[1]), level,
+                                        _ptr(buf)))
+
+    def fuse_finish_level(self, lsum, cnt, out_w, zr, level, buf, out=None):
+        self._check(self.L.pf_fuse_finish_level(self.h, _ptr(lsum), _ptr(cnt), out_w,
+                                                out_w // 2, float(zr[0]), float(zr[1]), level,
+                                                _ptr(buf), _ptr(out)))
+
+    def profile(self, on=True):
+        """Enable/disable per-stage hipEvent timing (resets the accumulators)."""
+        self._check(self.L.pf_profile_enable(self.h, 1 if on else 0))
+
+    def profile_read(self):
+        """{stage: (ms, algorithmic_bytes, launches)} accumulated since the last read."""
+        n = len(STAGES)
+        ms, by, ln = (C.c_double * n)(), (C.c_double * n)(), (C.c_longlong * n)()
+        self._check(self.L.pf_profile_read(self.h, ms, by, ln))
+        return {STAGES[i]: (ms[i], by[i], ln[i]) for i in range(n)}
+
+    def synchronize(self):
+        self._check(self.L.pf_synchronize(self.h))
+
+
+def make_responses(params, device):
+    """[B, ntiles] pf_response array on the device from (alpha, kappa, beta, sigma, seed)."""
+    import torch
+    p = np.asarray(params, dtype=np.float64).reshape(-1, 5)
+    raw = np.zeros((p.shape[0], 6), np.uint32)
+    raw[:, 0:4] = p[:, 0:4].astype(np.float32).view(np.uint32)
+    raw[:, 4] = p[:, 4].astype(np.uint64).astype(np.uint32)
+    return torch.from_numpy(raw.view(np.int32).copy()).to(device)
