@@ -1,0 +1,125 @@
+"""World-size-2 gloo tests (CPU) of the multi-GPU decompositions in pf_dist.py.
+
+The per-rank compute here is the CPU oracle (no GPU in this container); on the GPU box the same
+driver runs with the HIP backend over RCCL (bench.py --mode c5)."""
+import os
+import socket
+
+import numpy as np
+import pytest
+
+torch = pytest.importorskip("torch")
+import torch.distributed as dist  # noqa: E402
+import torch.multiprocessing as mp  # noqa: E402
+
+import pf_dist  # noqa: E402
+
+
+def test_shard_range_partitions():
+    for n in (1, 5, 20, 80, 81):
+        for world in (1, 2, 3, 8):
+            seen = []
+            for r in range(world):
+                lo, hi = pf_dist.shard_range(n, r, world)
+                seen.extend(range(lo, hi))
+            assert seen == list(range(n))
+
+
+def test_panorama_blocks_disjoint():
+    a = pf_dist.panorama_block(64, 0)
+    b = pf_dist.panorama_block(64, 1)
+    assert len(set(a) | set(b)) == 128
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+class OracleBackend:
+    """CPU stand-in for the GPU backend: the oracle computes each rank's share."""
+
+    def __init__(self, O, PL, out_w, emap, tiles, data):
+        self.O, self.PL, self.out_w = O, PL, out_w
+        self.emap, self.tiles, self.data = emap, tiles, data
+        self.zr = PL.ZENITH_RANGE
+
+    def _lv(self, level):
+        return self.O.level_dims(self.out_w, self.out_w // 2, self.zr, level)
+
+    def partial(self, level, t0, t1):
+        lv = self._lv(level)
+        if t1 > t0:
+            Ls, n = self.O.targets_subset(self.tiles, t0, t1, self.data, lv)
+        else:
+            Ls = np.zeros((lv.h, lv.w), np.float32)
+            n = np.zeros((lv.h, lv.w), np.int32)
+        return torch.from_numpy(Ls.copy()), torch.from_numpy(n.astype(np.float32))
+
+    def seed(self, level, prev):
+        lv = self._lv(level)
+        if level == 0:
+            return self.O.seed_level0(self.emap, lv)
+        return self.O.upsample(prev, lv)
+
+    def finish(self, level, lsum, cnt, buf, last):
+        lv = self._lv(level)
+        Ln = self.O.normalize(lsum.numpy(), cnt.numpy().astype(np.int32), lv)
+        return self.O.jacobi(buf, Ln, lv, lv.iters)
+
+
+def _worker(rank, world, port, q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        import pf_layouts as PL
+        import pf_synth
+        import pyoracle as O
+        lay = PL.config_layout("C1")
+        tiles, total = O.make_tiles(lay)
+        seeds = pf_synth.seeds_for(1, 31337)
+        emap = pf_synth.baseline_emap(seeds, 128, 64)[0].numpy()
+        data = np.random.RandomState(2).rand(total).astype(np.float32)
+        be = OracleBackend(O, PL, 512, emap, tiles, data)
+        final = pf_dist.fuse_tile_sharded(be, 3, lay.ntiles, rank, world, dist)
+        # every rank also checks the reduced level-2 targets against the single-rank sums
+        lv = be._lv(2)
+        ls, n = be.partial(2, *pf_dist.shard_range(lay.ntiles, rank, world))
+        dist.all_reduce(ls)
+        dist.all_reduce(n)
+        full_l, full_n = O.targets_subset(tiles, 0, lay.ntiles, data, lv)
+        ok_targets = bool(np.array_equal(ls.numpy().view(np.uint32), full_l.view(np.uint32))
+                          and np.array_equal(n.numpy(), full_n.astype(np.float32)))
+        if rank == 0:
+            ref, _ = O.solve_depth_all(emap, tiles, data, 512, PL.ZENITH_RANGE)
+            got = O.quantize(final)
+            q.put(("final", bool(np.array_equal(got, ref))))
+        q.put(("targets", ok_targets))
+        # batch sharding: the timing reduction is a MAX over ranks
+        t = torch.tensor([1.0 + rank], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        q.put(("max", float(t.item())))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_tile_sharded_fusion_gloo_world2():
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(240)
+        assert p.exitcode == 0
+    res = []
+    while not q.empty():
+        res.append(q.get())
+    assert ("final", True) in res
+    assert res.count(("targets", True)) == 2
+    assert res.count(("max", 2.0)) == 2

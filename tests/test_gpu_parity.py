@@ -232,9 +232,9 @@ def test_error_paths(fuser):
     fuser.set_tiles(lay)
     emap = torch.zeros((1, 64, 128), dtype=torch.float32, device=DEV)
     tiles = torch.zeros((1, fuser.tile_elems), dtype=torch.float32, device=DEV)
-    out = torch.zeros((1, 256, 500), dtype=torch.int16, device=DEV)
+    out = torch.zeros((1, 251, 502), dtype=torch.int16, device=DEV)
     with pytest.raises(panofuse.PanofuseError) as e:
-        fuser.fuse(emap, tiles, out, ZR)  # 500 is not divisible by 4
+        fuser.fuse(emap, tiles, out, ZR)  # 502 does not halve twice (levels 125/251/502)
     assert e.value.code == panofuse.PF_EINVAL
     with pytest.raises(panofuse.PanofuseError) as e:
         fuser.register(emap, tiles, ZR, degree=7)
@@ -248,3 +248,20 @@ def test_error_paths(fuser):
     with pytest.raises(panofuse.PanofuseError) as e:
         fuser.fuse(emap, tiles[:, : 256 * 256].contiguous(), out, ZR)
     assert e.value.code == panofuse.PF_EDEGENERATE
+
+
+@pytest.mark.parametrize("zr_deg", [(3.0, 177.0), (12.0, 150.0)])
+def test_fuse_bit_exact_wide_zenith(fuser, zr_deg):
+    """Zenith bands reaching near the poles: levels whose band leaves too little room for the
+    streaming engine's halo rows take the per-sweep kernel; both must match the oracle."""
+    zr = (np.float32(PL.D2R(zr_deg[0])), np.float32(PL.D2R(zr_deg[1])))
+    lay = PL.band_layout(5, 4, 256, 256, 3, 12, "wide", z_lo=zr_deg[0] + 1, z_hi=zr_deg[1] - 1)
+    fuser.set_tiles(lay)
+    tiles, total = O.make_tiles(lay)
+    rs = np.random.RandomState(11)
+    data = rs.rand(total).astype(np.float32)
+    emap = rs.rand(128, 256).astype(np.float32)
+    out = torch.zeros((1, 512, 1024), dtype=torch.int16, device=DEV)
+    fuser.fuse(_dev(emap)[None], _dev(data)[None].contiguous(), out, zr)
+    ref, _ = O.solve_depth_all(emap, tiles, data, 1024, zr)
+    assert int((out.cpu().numpy().view(np.uint16)[0] != ref).sum()) == 0

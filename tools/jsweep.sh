@@ -1,0 +1,20 @@
+#!/bin/bash
+# Jacobi engine tuning sweep on the GPU box: one bench process per setting "T:waves:minrows".
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+mkdir -p gpurun_out
+for cfg in ${SWEEP:-10:8192:0 5:8192:0}; do
+  IFS=: read -r T W R <<< "$cfg"
+  PF_JT=$T PF_JWAVES=$W PF_JROWS=$R timeout -k 10 300 python bench.py --steps 5 --warmup 2 \
+    --no-cpu-baseline > gpurun_out/sweep_$cfg.log 2>&1; rc=$?
+  python - "$cfg" gpurun_out/sweep_$cfg.log <<'PY'
+import json, sys
+try:
+    d = json.loads(open(sys.argv[2]).read().strip().splitlines()[-1])
+    j = d["stages"]["jacobi"]
+    print(sys.argv[1], "value=%.1f" % d["value"], "jacobi_ms=%.3f" % j["ms_per_step"],
+          "GBps=%.0f" % j["GBps"], "targets_ms=%.3f" % d["stages"]["targets"]["ms_per_step"])
+except Exception as e:
+    print(sys.argv[1], "FAILED", e)
+PY
+  [ $rc -eq 0 ] || exit $rc
+done

@@ -12,6 +12,7 @@
 #include <cmath>
 #include <cstdarg>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -38,6 +39,7 @@ struct LevelCache {
 
 struct pf_ctx {
     int device = 0;
+    int num_cu = 256;
     hipStream_t stream = nullptr;
     std::string err;
     // layout
@@ -293,6 +295,9 @@ int pf_create(int device, pf_ctx** out)
     if (hipSetDevice(device) != hipSuccess) return PF_EHIP;
     pf_ctx* c = new pf_ctx();
     c->device = device;
+    hipDeviceProp_t prop;
+    if (hipGetDeviceProperties(&prop, device) == hipSuccess && prop.multiProcessorCount > 0)
+        c->num_cu = prop.multiProcessorCount;
     *out = c;
     return PF_OK;
 }
@@ -572,6 +577,106 @@ static int check_emap(pf_ctx* c, const float* emap, int ew, int eh, int ec)
     return PF_OK;
 }
 
+// Jacobi pass geometry: lanes own C columns, strips carry a Tp-column halo (Tp >= T, rounded to
+// 4 so float4 rows stay aligned), row chunks sized so a level puts ~8 waves on every SIMD.
+struct JacobiTuning {
+    int C = 2, Tmax = 10, waves_target = 0, min_rows = 0, rounds = 1;
+};
+
+static JacobiTuning jacobi_tuning()
+{
+    JacobiTuning t;
+#if PF_JACOBI_C4
+    if (const char* e = getenv("PF_JC")) t.C = atoi(e) == 4 ? 4 : 2;
+#endif
+    if (const char* e = getenv("PF_JT")) t.Tmax = atoi(e);
+    if (const char* e = getenv("PF_JWAVES")) t.waves_target = atoi(e);
+    if (const char* e = getenv("PF_JROWS")) t.min_rows = atoi(e);
+    if (const char* e = getenv("PF_JROUNDS")) t.rounds = atoi(e) > 0 ? atoi(e) : 1;
+    if (!jstream_supported_T(t.Tmax)) t.Tmax = 10;
+    return t;
+}
+
+static int pick_T(int remaining, int Tmax)
+{
+    static const int menu[] = {10, 8, 5, 4, 2, 1};
+    for (int T : menu)
+        if (T <= Tmax && T <= remaining) return T;
+    return 1;
+}
+
+// Runs L.iters sweeps.  The first pass reads `first` (SRC_SEED: emap, SRC_UPSAMPLE: prev level,
+// SRC_BUF: buffer a); passes ping-pong between a and b.  With out != nullptr the last pass stores
+// the u16 quantisation instead of floats.  Returns the buffer holding the result (unused when
+// out is given).
+// Largest sweep depth the streaming engine may use on this level: its halo rows must stay inside
+// [1, h-2] (loads clamp rows into that range) and a strip (plus halo) must fit in a row.
+static int jacobi_tcap(const LevelDims& L)
+{
+    static const JacobiTuning tune = jacobi_tuning();
+    int cap = tune.Tmax;
+    if (L.h0 - 1 < cap) cap = L.h0 - 1;
+    if (L.h - 2 - L.h1 < cap) cap = L.h - 2 - L.h1;
+    while (cap >= 1) {
+        int Tp = (cap + 3) / 4 * 4;
+        if (128 - Tp <= L.w && L.w % 2 == 0) break;
+        cap--;
+    }
+    return cap;
+}
+
+static float* run_jacobi(pf_ctx* c, const LevelDims& L, int first, const float* emap, int ew,
+                         int eh, int ec, long long estride, const GridCol* cols,
+                         const GridRow* rows, const float* prev, long long pstride,
+                         const float* lnorm, float* a, float* b, uint16_t* out,
+                         long long ostride, int batch)
+{
+    static const JacobiTuning tune = jacobi_tuning();
+    const long long st = (long long)L.w * L.h;
+    const int C = (L.w % 4 == 0 && L.w >= 512) ? tune.C : 2;
+    JacobiPass P{};
+    P.prev = prev; P.pstride = pstride;
+    P.emap = emap; P.estride = estride; P.ew = ew; P.eh = eh; P.ec = ec;
+    P.cols = cols; P.rows = rows;
+    P.lnorm = lnorm; P.lstride = st;
+    P.sstride = st; P.dstride = st;
+    P.out = out; P.ostride = ostride;
+    P.w = L.w; P.h = L.h; P.h0 = L.h0; P.h1 = L.h1;
+    const int band_rows = L.h1 - L.h0 + 1;
+    float* src = (first == 0) ? a : nullptr;
+    float* dst = (first == 0) ? b : a;
+    int remaining = L.iters, pass = 0;
+    while (remaining > 0) {
+        int T = pick_T(remaining, jacobi_tcap(L));
+        P.Tp = (T + 3) / 4 * 4;
+        P.V = 64 * C - 2 * P.Tp;
+        P.nstrips = (L.w + P.V - 1) / P.V;
+        long long per = (long long)P.nstrips * batch;
+        // size the grid to whole rounds of resident waves (a partial last round idles SIMDs)
+        long long target = tune.waves_target > 0
+                               ? tune.waves_target
+                               : (long long)jstream_waves_per_cu(T) * c->num_cu * tune.rounds;
+        int nchunks = (int)((target + per / 2) / per);
+        int min_rows = tune.min_rows > 0 ? tune.min_rows : 4 * T;
+        int max_chunks = band_rows / min_rows;
+        if (max_chunks < 1) max_chunks = 1;
+        if (nchunks > max_chunks) nchunks = max_chunks;
+        if (nchunks < 1) nchunks = 1;
+        P.rows_per_chunk = (band_rows + nchunks - 1) / nchunks;
+        P.nchunks = (band_rows + P.rows_per_chunk - 1) / P.rows_per_chunk;
+        P.src_mode = pass == 0 ? first : 0;
+        P.src = src;
+        P.dst = dst;
+        remaining -= T;
+        P.out_mode = (remaining == 0 && out) ? 1 : 0;
+        launch_jstream(c->stream, P, C, T, batch);
+        src = dst;
+        dst = (dst == a) ? b : a;
+        pass++;
+    }
+    return src;
+}
+
 static int fuse_impl(pf_ctx* c, const float* emap, int ew, int eh, int ec, const float* tiles,
                      const float* coeffs, int batch, int out_w, int out_h, float zr0,
                      float zr1, uint16_t* out)
@@ -586,9 +691,12 @@ static int fuse_impl(pf_ctx* c, const float* emap, int ew, int eh, int ec, const
     float* bufs[3] = {(float*)c->buf[0].p, (float*)c->buf[1].p, (float*)c->buf[2].p};
     float* prev = nullptr;
     LevelCache& lc = c->lc;
+    static const bool naive = getenv("PF_JACOBI") && strcmp(getenv("PF_JACOBI"), "naive") == 0;
     for (int l = 0; l < lc.nlevels; l++) {
         const LevelDims& L = lc.dims[l];
         const long long st = (long long)L.w * L.h;
+        const bool last = l == lc.nlevels - 1;
+        const long long pst = l > 0 ? (long long)lc.dims[l - 1].w * lc.dims[l - 1].h : 0;
         float* a = nullptr;
         float* b = nullptr;
         for (int k = 0; k < 3; k++) {
@@ -598,35 +706,50 @@ static int fuse_impl(pf_ctx* c, const float* emap, int ew, int eh, int ec, const
         }
         const double B = (double)batch;
         const double band = (double)L.w * (L.h1 - L.h0 + 1);
-        {
-            // algorithmic bytes: write the level, read the source
-            double src = l == 0 ? (double)(L.h1 - L.h0 + 1) * L.w * 4.0 : (double)st;
-            StageTimer t(c, PF_STAGE_SEED, B * (4.0 * st + src), 1);
-            if (l == 0)
-                launch_seed0(c->stream, emap, ew, eh, ec, estride, (const GridCol*)lc.cols[0].p,
-                             (const GridRow*)lc.rows[0].p, L, a, st, batch);
-            else
-                launch_upsample(c->stream, prev, (long long)lc.dims[l - 1].w * lc.dims[l - 1].h, L,
-                                a, st, batch);
-        }
+        const GridCol* cols = (const GridCol*)lc.cols[l].p;
+        const GridRow* rows = (const GridRow*)lc.rows[l].p;
         {
             StageTimer t(c, PF_STAGE_TARGETS, B * (4.0 * band + 4.0 * (double)c->tile_elems), 1);
             launch_targets(c->stream, (const TileGeom*)c->geom.p, (const TileBox*)lc.box[l].p, 0,
-                           c->ntiles, (const GridCol*)lc.cols[l].p, (const GridRow*)lc.rows[l].p,
-                           tiles, c->tile_elems, coeffs, c->ntiles, L, (float*)c->lnorm.p, st,
-                           batch);
+                           c->ntiles, cols, rows, tiles, c->tile_elems, coeffs, c->ntiles, L,
+                           (float*)c->lnorm.p, st, batch);
         }
-        HIPCHK(c, hipMemcpyAsync(b, a, sizeof(float) * st * batch, hipMemcpyDeviceToDevice,
-                                 c->stream));
         float* res = nullptr;
-        {
-            // 12 B per pixel-update: read b, read L, write b' 
-            StageTimer t(c, PF_STAGE_JACOBI, B * 12.0 * band * L.iters, L.iters);
-            launch_jacobi(c->stream, a, b, (const float*)c->lnorm.p, st, L, L.iters, batch, &res);
-        }
-        if (l == lc.nlevels - 1) {
-            StageTimer t(c, PF_STAGE_QUANTIZE, B * 6.0 * st, 1);
-            launch_quantize(c->stream, res, st, (int)st, out, plane, batch);
+        if (naive || jacobi_tcap(L) < 1) {
+            {
+                double srcb = l == 0 ? band * 4.0 : (double)st;
+                StageTimer t(c, PF_STAGE_SEED, B * (4.0 * st + srcb), 1);
+                if (l == 0)
+                    launch_seed0(c->stream, emap, ew, eh, ec, estride, cols, rows, L, a, st, batch);
+                else
+                    launch_upsample(c->stream, prev, pst, L, a, st, batch);
+            }
+            HIPCHK(c, hipMemcpyAsync(b, a, sizeof(float) * st * batch, hipMemcpyDeviceToDevice,
+                                     c->stream));
+            {
+                StageTimer t(c, PF_STAGE_JACOBI, B * 12.0 * band * L.iters, L.iters);
+                launch_jacobi(c->stream, a, b, (const float*)c->lnorm.p, st, L, L.iters, batch,
+                              &res);
+            }
+            if (last) {
+                StageTimer t(c, PF_STAGE_QUANTIZE, B * 6.0 * st, 1);
+                launch_quantize(c->stream, res, st, (int)st, out, plane, batch);
+            }
+        } else {
+            {
+                // out-of-band rows: zero / upsampled copy (u16 on the last level)
+                double nb = (double)st - band;
+                StageTimer t(c, PF_STAGE_SEED, B * nb * (last ? 3.0 : 9.0), 1);
+                launch_border(c->stream, l == 0 ? nullptr : prev, pst, L, a, b, st,
+                              last ? out : nullptr, plane, batch);
+            }
+            {
+                // 12 B per pixel-update (read b, read L, write b'), SURVEY.md 8d
+                StageTimer t(c, PF_STAGE_JACOBI, B * 12.0 * band * L.iters, L.iters);
+                res = run_jacobi(c, L, l == 0 ? 2 : 1, emap, ew, eh, ec, estride, cols, rows,
+                                 prev, pst, (const float*)c->lnorm.p, a, b, last ? out : nullptr,
+                                 plane, batch);
+            }
         }
         prev = res;
     }
@@ -788,7 +911,11 @@ int pf_fuse_finish_level(pf_ctx* c, const float* lsum, const float* cnt, int out
     float* other = (float*)c->lsum_ws.p;
     HIPCHK(c, hipMemcpyAsync(other, buf, sizeof(float) * st, hipMemcpyDeviceToDevice, c->stream));
     float* res = nullptr;
-    launch_jacobi(c->stream, buf, other, (const float*)c->lnorm.p, st, L, L.iters, 1, &res);
+    if (jacobi_tcap(L) >= 1)
+        res = run_jacobi(c, L, 0, nullptr, 0, 0, 0, 0, nullptr, nullptr, nullptr, 0,
+                         (const float*)c->lnorm.p, buf, other, nullptr, 0, 1);
+    else
+        launch_jacobi(c->stream, buf, other, (const float*)c->lnorm.p, st, L, L.iters, 1, &res);
     if (res != buf)
         HIPCHK(c, hipMemcpyAsync(buf, res, sizeof(float) * st, hipMemcpyDeviceToDevice, c->stream));
     if (level == lc.nlevels - 1 && out) launch_quantize(c->stream, buf, st, (int)st, out, st, 1);

@@ -110,8 +110,28 @@ __host__ __device__ inline long long emap_index(float az, float zen, int w, int 
     return ((long long)y * w + x) * c;
 }
 
+// One temporally blocked Jacobi pass (pf_jacobi.hip).
+struct JacobiPass {
+    const float* src; long long sstride;    // SRC_BUF input
+    const float* prev; long long pstride;   // SRC_UPSAMPLE input (previous level, w/2 x h/2)
+    const float* emap; long long estride;   // SRC_SEED input
+    int ew, eh, ec, src_mode;
+    const GridCol* cols; const GridRow* rows;
+    const float* lnorm; long long lstride;
+    float* dst; long long dstride;
+    uint16_t* out; long long ostride;
+    int out_mode;
+    int w, h, h0, h1;
+    int V, Tp, nstrips, nchunks, rows_per_chunk;
+};
+
 // ------------------------------------------------------------------------------------------
-// Kernel launchers (pf_kernels.hip).  All are asynchronous on `stream`.
+// Kernel launchers (pf_kernels.hip, pf_jacobi.hip).  All are asynchronous on `stream`.
+bool jstream_supported_T(int T);
+int jstream_waves_per_cu(int T);
+void launch_jstream(hipStream_t s, const JacobiPass& P, int C, int T, int batch);
+void launch_border(hipStream_t s, const float* prev, long long pstride, LevelDims L, float* a,
+                   float* b, long long stride, uint16_t* out, long long ostride, int batch);
 void launch_seed0(hipStream_t s, const float* emap, int ew, int eh, int ec, long long estride,
                   const GridCol* cols, const GridRow* rows, LevelDims L, float* buf,
                   long long bstride, int batch);
