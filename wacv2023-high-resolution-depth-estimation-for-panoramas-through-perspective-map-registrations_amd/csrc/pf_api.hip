@@ -31,7 +31,7 @@ struct LevelCache {
     uint32_t zr0 = 0, zr1 = 0;
     int nlevels = 0;
     LevelDims dims[4];
-    DevBuf box[4], cols[4], rows[4];
+    DevBuf box[4], cols[4], rows[4], tapbox[4], tapmap[4];
     std::vector<TileBox> box_h[4];
 };
 
@@ -314,6 +314,8 @@ void pf_destroy(pf_ctx* c)
         release(c->lc.box[l]);
         release(c->lc.cols[l]);
         release(c->lc.rows[l]);
+        release(c->lc.tapbox[l]);
+        release(c->lc.tapmap[l]);
     }
     for (auto& s : c->spans) {
         (void)hipEventDestroy(s.a);
@@ -552,6 +554,31 @@ static int prepare_levels(pf_ctx* c, int out_w, int out_h, float zr0, float zr1)
         if ((rc = upload(c, lc.box[l], boxes))) return rc;
         if ((rc = upload(c, lc.cols[l], cols))) return rc;
         if ((rc = upload(c, lc.rows[l], rows))) return rc;
+        // tap-index maps: every tile's box plus a one-pixel ring (pf_targets.hip)
+        std::vector<TapBox> tbs(c->ntiles);
+        long long moff = 0, maxpts = 0;
+        for (int p = 0; p < c->ntiles; p++) {
+            const TileBox& b = boxes[p];
+            TapBox t{};
+            if (b.y0 <= b.y1) {
+                int xlo = b.xs > 0 ? b.x0 : b.x1 + 1, xhi = b.xs > 0 ? b.x1 - 1 : b.x0;
+                t.xmin = xlo - 1;
+                t.ymin = b.y0 - 1;
+                t.nx = xhi - xlo + 3;
+                t.ny = b.y1 - b.y0 + 3;
+            }
+            t.off = moff;
+            long long np = (long long)t.nx * t.ny;
+            moff += np;
+            if (np > maxpts) maxpts = np;
+            tbs[p] = t;
+        }
+        if ((rc = upload(c, lc.tapbox[l], tbs))) return rc;
+        if ((rc = ensure(c, lc.tapmap[l], sizeof(int32_t) * (moff + 1)))) return rc;
+        launch_tapmap(c->stream, (const TileGeom*)c->geom.p, (const TapBox*)lc.tapbox[l].p,
+                      c->ntiles, maxpts, (const GridCol*)lc.cols[l].p,
+                      (const GridRow*)lc.rows[l].p, (int32_t*)lc.tapmap[l].p);
+        HIPCHK(c, hipGetLastError());
     }
     lc.nlevels = nl;
     lc.out_w = out_w;
@@ -710,9 +737,17 @@ static int fuse_impl(pf_ctx* c, const float* emap, int ew, int eh, int ec, const
         const GridRow* rows = (const GridRow*)lc.rows[l].p;
         {
             StageTimer t(c, PF_STAGE_TARGETS, B * (4.0 * band + 4.0 * (double)c->tile_elems), 1);
-            launch_targets(c->stream, (const TileGeom*)c->geom.p, (const TileBox*)lc.box[l].p, 0,
-                           c->ntiles, cols, rows, tiles, c->tile_elems, coeffs, c->ntiles, L,
-                           (float*)c->lnorm.p, st, batch);
+            static const bool direct =
+                getenv("PF_TARGETS") && strcmp(getenv("PF_TARGETS"), "direct") == 0;
+            if (direct)
+                launch_targets(c->stream, (const TileGeom*)c->geom.p, (const TileBox*)lc.box[l].p,
+                               0, c->ntiles, cols, rows, tiles, c->tile_elems, coeffs, c->ntiles,
+                               L, (float*)c->lnorm.p, st, batch);
+            else
+                launch_targets_map(c->stream, (const TileGeom*)c->geom.p,
+                                   (const TileBox*)lc.box[l].p, (const TapBox*)lc.tapbox[l].p,
+                                   c->ntiles, (const int32_t*)lc.tapmap[l].p, tiles,
+                                   c->tile_elems, coeffs, L, (float*)c->lnorm.p, st, batch);
         }
         float* res = nullptr;
         if (naive || jacobi_tcap(L) < 1) {

@@ -33,6 +33,13 @@ struct TileBox {
     int x0, x1, y0, y1, xs, pad[3];
 };
 
+// Tap-index map extent of one tile at one level: its box plus a one-pixel ring, row-major,
+// starting at element `off` of the level's map.
+struct TapBox {
+    int xmin, ymin, nx, ny;
+    long long off;
+};
+
 struct GridCol { float az, ca, sa, pad; };   // column xx (index xx+1): az, cos az, sin az
 struct GridRow { float zen, sz, cz, pad; };  // row yy (index yy+1): zen, sin zen, cos zen
 
@@ -127,6 +134,12 @@ struct JacobiPass {
 
 // ------------------------------------------------------------------------------------------
 // Kernel launchers (pf_kernels.hip, pf_jacobi.hip).  All are asynchronous on `stream`.
+void launch_tapmap(hipStream_t s, const TileGeom* geom, const TapBox* tb, int ntiles,
+                   long long max_points, const GridCol* cols, const GridRow* rows, int32_t* map);
+void launch_targets_map(hipStream_t s, const TileGeom* geom, const TileBox* box,
+                        const TapBox* tb, int ntiles, const int32_t* map, const float* tiles,
+                        long long tstride, const float* coeffs, LevelDims L, float* lnorm,
+                        long long lstride, int batch);
 bool jstream_supported_T(int T);
 int jstream_waves_per_cu(int T);
 void launch_jstream(hipStream_t s, const JacobiPass& P, int C, int T, int batch);

@@ -37,7 +37,7 @@
 #define PF_JLAG_STAGEWISE 1
 #endif
 #ifndef PF_JLAG_TOUCH
-#define PF_JLAG_TOUCH 4  // steps of lead for the L2 touch loads (0 = off)
+#define PF_JLAG_TOUCH 0  // steps of lead for L2 touch loads (0 = off; measured slower)
 #endif
 
 namespace pf {

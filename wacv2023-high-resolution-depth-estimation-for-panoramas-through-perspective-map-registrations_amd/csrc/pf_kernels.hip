@@ -10,6 +10,7 @@
 namespace pf {
 
 static constexpr int kBlock = 256;
+static constexpr int kWarpBatch = 8;  // panoramas per thread in the E->P warps
 
 __device__ __forceinline__ float bits_f(uint32_t u) { return __uint_as_float(u); }
 __device__ __forceinline__ uint32_t f_bits(float f) { return __float_as_uint(f); }
@@ -463,10 +464,25 @@ __global__ void __launch_bounds__(kBlock) k_warp_depth(const TileGeom* __restric
     long long o00 = (long long)y0 * pw + x0, o01 = (long long)y0 * pw + x1;
     long long o10 = (long long)y1 * pw + x0, o11 = (long long)y1 * pw + x1;
     float wx0 = 1.0f - fx, wy0 = 1.0f - fy;
-    for (int b = 0; b < batch; b++) {
+    // kWarpBatch panoramas per thread (grid.z walks the batch): all their gathers are issued
+    // before the first use so each wave keeps 4*kWarpBatch loads in flight.
+    const int bbeg = blockIdx.z * kWarpBatch;
+    float t00[kWarpBatch], t01[kWarpBatch], t10[kWarpBatch], t11[kWarpBatch];
+#pragma unroll
+    for (int q = 0; q < kWarpBatch; q++) {
+        const int b = bbeg + q < batch ? bbeg + q : batch - 1;
         const float* pp = pano + b * pstride;
-        float top = pp[o00] * wx0 + pp[o01] * fx;
-        float bot = pp[o10] * wx0 + pp[o11] * fx;
+        t00[q] = pp[o00];
+        t01[q] = pp[o01];
+        t10[q] = pp[o10];
+        t11[q] = pp[o11];
+    }
+#pragma unroll
+    for (int q = 0; q < kWarpBatch; q++) {
+        const int b = bbeg + q;
+        if (b >= batch) break;
+        float top = t00[q] * wx0 + t01[q] * fx;
+        float bot = t10[q] * wx0 + t11[q] * fx;
         float v = top * wy0 + bot * fy;
         if (resp) {
             const Resp r = resp[(long long)b * ntiles + p];
@@ -633,7 +649,7 @@ void launch_warp_depth(hipStream_t s, const TileGeom* geom, int ntiles, long lon
                        const float* pano, int pw, int ph, long long pstride, const Resp* resp,
                        float* tiles, long long tstride, int batch)
 {
-    dim3 grid(nblocks(npix_max), ntiles);
+    dim3 grid(nblocks(npix_max), ntiles, (batch + kWarpBatch - 1) / kWarpBatch);
     hipLaunchKernelGGL(k_warp_depth, grid, dim3(kBlock), 0, s, geom, ntiles, pano, pw, ph,
                        pstride, resp, tiles, tstride, batch);
 }
