@@ -601,14 +601,21 @@ int pfo_merge(const float* emap, int ew, int eh, int ec, const pfo_tile* tiles, 
 }
 
 /* ---------------- warps ---------------- */
+static inline uint32_t mix32(uint32_t x)
+{ /* lowbias32 finaliser */
+    x ^= x >> 16;
+    x *= 0x7FEB352Du;
+    x ^= x >> 15;
+    x *= 0x846CA68Bu;
+    x ^= x >> 16;
+    return x;
+}
+
 uint32_t pfo_hash32(uint32_t seed, uint32_t tile, uint32_t idx)
-{ /* splitmix64 finaliser over (seed, tile, pixel) */
-    uint64_t z = ((uint64_t)seed << 32) ^ ((uint64_t)tile << 24) ^ (uint64_t)idx;
-    z += 0x9E3779B97F4A7C15ull;
-    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
-    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
-    z ^= z >> 31;
-    return (uint32_t)(z >> 32);
+{ /* counter-based noise keyed by (seed, tile, pixel): the (seed, tile) key is mixed once, the
+   * pixel counter once more (the GPU evaluates the key on its scalar unit) */
+    uint32_t key = mix32(seed ^ mix32(tile + 0x9E3779B9u));
+    return mix32(idx ^ key);
 }
 
 static inline float response(const pfo_response* r, uint32_t tile, uint32_t idx, float d)

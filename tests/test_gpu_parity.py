@@ -189,6 +189,26 @@ def test_warp_depth_tolerance(fuser, cfg):
     assert (diff > 0).mean() < 0.25
 
 
+def test_warp_depth_ragged_batch_and_resize(fuser):
+    """Batch 19 (one full 16-panorama chunk + a ragged one), distinct responses per panorama,
+    then a different panorama size on the same context (the cached warp map must follow)."""
+    lay = PL.config_layout("C1")
+    fuser.set_tiles(lay)
+    tiles, total = O.make_tiles(lay)
+    B = 19
+    seeds = pf_synth.seeds_for(B, 777)
+    resp = pf_synth.responses(seeds, lay.ntiles)
+    for (pw, ph) in ((512, 256), (300, 150)):
+        gt = pf_synth.scene_depth(seeds, pw, ph).numpy()
+        out = torch.zeros((B, total), dtype=torch.float32, device=DEV)
+        fuser.warp_depth(_dev(gt), out, panofuse.make_responses(resp, DEV))
+        got = out.cpu().numpy()
+        for b in (0, 15, 16, 18):
+            nt = lay.ntiles
+            ref = O.warp_depth(gt[b], tiles, total, O.responses(resp[b * nt:(b + 1) * nt]))
+            assert np.max(np.abs(got[b] - ref)) <= WARP_TOL, (pw, b)
+
+
 def test_warp_rgb_tolerance(fuser):
     lay = PL.config_layout("C1")
     fuser.set_tiles(lay)

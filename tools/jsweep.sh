@@ -12,7 +12,9 @@ try:
     d = json.loads(open(sys.argv[2]).read().strip().splitlines()[-1])
     j = d["stages"]["jacobi"]
     print(sys.argv[1], "value=%.1f" % d["value"], "jacobi_ms=%.3f" % j["ms_per_step"],
-          "GBps=%.0f" % j["GBps"], "targets_ms=%.3f" % d["stages"]["targets"]["ms_per_step"])
+          "GBps=%.0f" % j["GBps"], "targets_ms=%.3f" % d["stages"]["targets"]["ms_per_step"],
+          "warp_ms=%.3f" % d["stages"]["warp"]["ms_per_step"],
+          "warp_GBps=%.0f" % d["stages"]["warp"]["GBps"])
 except Exception as e:
     print(sys.argv[1], "FAILED", e)
 PY

@@ -52,6 +52,10 @@ struct pf_ctx {
     LevelCache lc;
     bool reg_valid = false;
     uint32_t reg_zr0 = 0, reg_zr1 = 0;
+    // E->P depth-warp map for one panorama size: per tile pixel the packed bilinear corner
+    // index and the (fx, fy) weights (k_warpmap), built on first use
+    int wmap_pw = 0, wmap_ph = 0;
+    DevBuf wmap, wfxy;
     // workspace
     DevBuf buf[3], lnorm, coeffs, lsum_ws;
     // stage profiling
@@ -308,7 +312,8 @@ void pf_destroy(pf_ctx* c)
     (void)hipSetDevice(c->device);
     (void)hipStreamSynchronize(c->stream);
     DevBuf* all[] = {&c->geom, &c->reg, &c->rcols, &c->rrows, &c->cams, &c->rgb_off,
-                     &c->buf[0], &c->buf[1], &c->buf[2], &c->lnorm, &c->coeffs, &c->lsum_ws};
+                     &c->buf[0], &c->buf[1], &c->buf[2], &c->lnorm, &c->coeffs, &c->lsum_ws,
+                     &c->wmap, &c->wfxy};
     for (DevBuf* b : all) release(*b);
     for (int l = 0; l < 4; l++) {
         release(c->lc.box[l]);
@@ -421,7 +426,10 @@ int pf_set_tiles(pf_ctx* c, const pf_window* fovs, const pf_window* ranges, int 
         if (!(g.hl > 0.0f) || !(g.vl > 0.0f))
             return fail(c, PF_EINVAL, "tile %d: degenerate window (pole or zero FOV)", i);
         g.off = off;
+        g.pix_off = (int)(off / tile_c);
         off += (long long)tile_w[i] * tile_h[i] * tile_c;
+        if (off / tile_c > INT32_MAX)
+            return fail(c, PF_EINVAL, "layout has more than 2^31 tile pixels");
         rgb_off[i] = roff;
         roff += (long long)tile_w[i] * tile_h[i] * 3;
         long long np = (long long)tile_w[i] * tile_h[i];
@@ -453,6 +461,7 @@ int pf_set_tiles(pf_ctx* c, const pf_window* fovs, const pf_window* ranges, int 
     c->npix_max = npmax;
     c->lc.out_w = 0;  // boxes and registration grids depend on the ranges: rebuild lazily
     c->reg_valid = false;
+    c->wmap_pw = c->wmap_ph = 0;
     int rc;
     if ((rc = upload(c, c->geom, c->geom_h))) return rc;
     if ((rc = upload(c, c->cams, cams))) return rc;
@@ -605,7 +614,7 @@ static int check_emap(pf_ctx* c, const float* emap, int ew, int eh, int ec)
 }
 
 // Jacobi pass geometry: lanes own C columns, strips carry a Tp-column halo (Tp >= T, rounded to
-// 4 so float4 rows stay aligned), row chunks sized so a level puts ~8 waves on every SIMD.
+// C so vector rows stay aligned), row chunks sized to whole rounds of resident waves.
 struct JacobiTuning {
     int C = 2, Tmax = 10, waves_target = 0, min_rows = 0, rounds = 1;
 };
@@ -675,7 +684,7 @@ static float* run_jacobi(pf_ctx* c, const LevelDims& L, int first, const float* 
     int remaining = L.iters, pass = 0;
     while (remaining > 0) {
         int T = pick_T(remaining, jacobi_tcap(L));
-        P.Tp = (T + 3) / 4 * 4;
+        P.Tp = (T + C - 1) / C * C;  // keeps colbase (and each lane's C-vector) aligned
         P.V = 64 * C - 2 * P.Tp;
         P.nstrips = (L.w + P.V - 1) / P.V;
         long long per = (long long)P.nstrips * batch;
@@ -863,10 +872,22 @@ int pf_warp_depth(pf_ctx* c, const float* pano, int pw, int ph, int batch,
     if (!pano || !tiles || pw < 2 || ph < 2)
         return fail(c, PF_EINVAL, "bad pano %p %dx%d", (const void*)pano, pw, ph);
     static_assert(sizeof(pf_response) == sizeof(Resp), "pf_response layout");
-    StageTimer t(c, PF_STAGE_WARP,
-                 batch * (4.0 * pw * ph + 4.0 * (double)c->tile_elems / c->tile_c), 1);
-    launch_warp_depth(c->stream, (const TileGeom*)c->geom.p, c->ntiles, c->npix_max, pano, pw,
-                      ph, (long long)pw * ph, (const Resp*)resp, tiles, c->tile_elems, batch);
+    if ((long long)pw * ph >= (1ll << 30))
+        return fail(c, PF_EINVAL, "pano %dx%d: more than 2^30 pixels", pw, ph);
+    const long long npix = c->tile_elems / c->tile_c;
+    if (c->wmap_pw != pw || c->wmap_ph != ph) {
+        if ((rc = ensure(c, c->wmap, sizeof(uint32_t) * npix))) return rc;
+        if ((rc = ensure(c, c->wfxy, sizeof(float) * 2 * npix))) return rc;
+        launch_warpmap(c->stream, (const TileGeom*)c->geom.p, c->ntiles, c->npix_max, pw, ph,
+                       (uint32_t*)c->wmap.p, (float*)c->wfxy.p);
+        HIPCHK(c, hipGetLastError());
+        c->wmap_pw = pw;
+        c->wmap_ph = ph;
+    }
+    StageTimer t(c, PF_STAGE_WARP, batch * (4.0 * pw * ph + 4.0 * (double)npix), 1);
+    launch_warp_depth(c->stream, (const TileGeom*)c->geom.p, c->ntiles, c->npix_max,
+                      (const uint32_t*)c->wmap.p, (const float*)c->wfxy.p, pano, pw, ph,
+                      (long long)pw * ph, (const Resp*)resp, tiles, c->tile_elems, batch);
     HIPCHK(c, hipGetLastError());
     return PF_OK;
 }

@@ -24,7 +24,8 @@ namespace pf {
 struct TileGeom {
     float middle[3], hedge[3], vedge[3], corner0[3];
     float mm, hl, vl, pad;
-    int w, h, c, pad2;
+    int w, h, c;
+    int pix_off;    // first pixel of the tile in layout-wide per-pixel tables (warp map)
     long long off;  // float offset of the tile inside one panorama's tile block
 };
 
@@ -173,9 +174,12 @@ void launch_register(hipStream_t s, const TileGeom* geom, const RegGrid* grids,
                      int batch);
 void launch_apply_cubic(hipStream_t s, const TileGeom* geom, int ntiles, long long tile_elems,
                         float* tiles, long long tstride, const float* coeffs, int batch);
+void launch_warpmap(hipStream_t s, const TileGeom* geom, int ntiles, long long npix_max, int pw,
+                    int ph, uint32_t* wmap, float* wfxy);
 void launch_warp_depth(hipStream_t s, const TileGeom* geom, int ntiles, long long npix_max,
-                       const float* pano, int pw, int ph, long long pstride, const Resp* resp,
-                       float* tiles, long long tstride, int batch);
+                       const uint32_t* wmap, const float* wfxy, const float* pano, int pw,
+                       int ph, long long pstride, const Resp* resp, float* tiles,
+                       long long tstride, int batch);
 void launch_warp_rgb(hipStream_t s, const RgbCam* cams, const TileGeom* geom, int ntiles,
                      long long npix_total, const long long* pix_prefix,
                      const long long* rgb_off, const uint8_t* pano, int pw, int ph,

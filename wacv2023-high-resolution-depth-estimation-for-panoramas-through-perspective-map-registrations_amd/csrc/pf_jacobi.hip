@@ -36,6 +36,9 @@
 #ifndef PF_JLAG_STAGEWISE
 #define PF_JLAG_STAGEWISE 1
 #endif
+#ifndef PF_JLAG_LDSL
+#define PF_JLAG_LDSL 1  // L rows through a per-wave LDS ring (1) or per-level registers (0)
+#endif
 #ifndef PF_JLAG_TOUCH
 #define PF_JLAG_TOUCH 0  // steps of lead for L2 touch loads (0 = off; measured slower)
 #endif
@@ -234,7 +237,17 @@ template <int C, int T, int SRC, bool OUT16>
 struct JLag {
     Row<C> H[T][3];   // H[t][r % 3] = level t row r
     Row<C> In[2];     // input row r lands in In[r & 1] (loaded at step r, used from r + 1)
+#if PF_JLAG_LDSL
+    // L rows live in a per-wave LDS ring of R = 2T+1 rows (row r in slot r % R): each L row is
+    // loaded from memory once (one step ahead, into Lin) and read T times from LDS, instead of
+    // T global loads per step held in 2*T*C registers.
+    static constexpr int R = 2 * T + 1;
+    Row<C> Lin[2];    // L row r lands in Lin[r & 1] during step r-1, is stored to LDS at step r
+    float* lring;     // this wave's ring: R rows of 64*C floats
+    int lane_c;       // lane * C (LDS column offset)
+#else
     Row<C> Lb[2][T];  // Lb[k & 1][t-1] = L row k-2t, for step k
+#endif
 #if PF_JLAG_TOUCH
     Row<C> Tch[2][2];      // touch-load landing registers (input row, L row)
     uint32_t touch_acc;    // keeps the touch loads alive; never meaningful
@@ -298,11 +311,54 @@ struct JLag {
 
     static constexpr int slot(int ph, int a) { return ((ph - a) % 3 + 3) % 3; }
 
+#if PF_JLAG_LDSL
+    // LDS ring slot of row (group base + d); kb = group base mod R (wave-uniform, SALU).
+    __device__ __forceinline__ float* lslot(int kb, int d) const
+    {
+        const int s = (kb + d + 2 * R) % R;  // d >= -2T > -2R
+        return lring + s * (64 * C) + lane_c;
+    }
+    __device__ __forceinline__ void lds_put(float* p, const Row<C>& r) const
+    {
+        if constexpr (C == 2) *reinterpret_cast<float2*>(p) = make_float2(r.v[0], r.v[1]);
+        else if constexpr (C == 4) *reinterpret_cast<float4*>(p) = make_float4(r.v[0], r.v[1], r.v[2], r.v[3]);
+        else {
+#pragma unroll
+            for (int j = 0; j < C; j++) p[j] = r.v[j];
+        }
+    }
+    __device__ __forceinline__ Row<C> lds_get(const float* p) const
+    {
+        Row<C> r;
+        if constexpr (C == 2) {
+            float2 q = *reinterpret_cast<const float2*>(p);
+            r.v[0] = q.x; r.v[1] = q.y;
+        } else if constexpr (C == 4) {
+            float4 q = *reinterpret_cast<const float4*>(p);
+            r.v[0] = q.x; r.v[1] = q.y; r.v[2] = q.z; r.v[3] = q.w;
+        } else {
+#pragma unroll
+            for (int j = 0; j < C; j++) r.v[j] = p[j];
+        }
+        return r;
+    }
+#endif
+
+    // Step k = (group base) + PH; kb = group base mod R (used by the LDS L ring only).
     template <int PH>
-    __device__ __forceinline__ void step(int k)
+    __device__ __forceinline__ void step(int k, int kb)
     {
         // level-0 row k-1 (loaded last step) joins the ring
         H[0][slot(PH, 1)] = In[(PH + 1) & 1];
+#if PF_JLAG_LDSL
+        // L row k (landed in Lin last step) goes to its ring slot; fetch L row k+1.  The slot
+        // is reused by row k+R > k, after every level has read row k (last read at k + 2T).
+        lds_put(lslot(kb, PH), Lin[PH & 1]);
+        Lin[(PH + 1) & 1] = load_row(lnorm, k + 1);
+        Row<C> Lv[T];
+#pragma unroll
+        for (int t = 1; t <= T; t++) Lv[t - 1] = lds_get(lslot(kb, PH - 2 * t));
+#endif
 #if PF_JLAG_TOUCH
         // Touch loads: bring the input and L rows PF_JLAG_TOUCH steps ahead into L2 (their
         // first use would otherwise wait on HBM with only one step of lead).  The values are
@@ -318,8 +374,11 @@ struct JLag {
 #endif
         // loads for the next step: input row k, L rows (k+1) - 2t
         In[PH & 1] = load_input(k);
+#if !PF_JLAG_LDSL
 #pragma unroll
         for (int t = 1; t <= T; t++) Lb[(PH + 1) & 1][t - 1] = load_row(lnorm, k + 1 - 2 * t);
+        const Row<C>* Lv = Lb[PH & 1];
+#endif
         Row<C> nw[T];
 #if PF_JLAG_STAGEWISE
         // Stage-wise over the T*C independent updates of this step, so consecutive VALU
@@ -361,9 +420,9 @@ struct JLag {
         for (int t = 1; t <= T; t++)
 #pragma unroll
             for (int j = 0; j < C; j++) {
-                const float Lv = Lb[PH & 1][t - 1].v[j];
-                float d = Lv - cur[t - 1][j];
-                uint32_t m = __float_as_uint(Lv) == PF_NAN_MARKER ? 0u : 0xFFFFFFFFu;
+                const float Lx = Lv[t - 1].v[j];
+                float d = Lx - cur[t - 1][j];
+                uint32_t m = __float_as_uint(Lx) == PF_NAN_MARKER ? 0u : 0xFFFFFFFFu;
                 cur[t - 1][j] = __uint_as_float(__float_as_uint(d) & m);
             }
 #pragma unroll
@@ -379,7 +438,7 @@ struct JLag {
 #pragma unroll
         for (int t = 1; t <= T; t++)
             nw[t - 1] = sweep_row<C>(H[t - 1][slot(PH, 2 * t + 1)], H[t - 1][slot(PH, 2 * t)],
-                                     H[t - 1][slot(PH, 2 * t - 1)], Lb[PH & 1][t - 1]);
+                                     H[t - 1][slot(PH, 2 * t - 1)], Lv[t - 1]);
 #endif
 #pragma unroll
         for (int t = 1; t < T; t++) H[t][slot(PH, 2 * t)] = nw[t - 1];
@@ -442,11 +501,22 @@ __global__ void __launch_bounds__(256, PF_JLAG_WAVES) k_jlag(JacobiPass P)
     for (int q = 0; q < 2; q++) {
 #pragma unroll
         for (int j = 0; j < C; j++) S.In[q].v[j] = 0.0f;
+#if PF_JLAG_LDSL
+#pragma unroll
+        for (int j = 0; j < C; j++) S.Lin[q].v[j] = 0.0f;
+#else
 #pragma unroll
         for (int t = 0; t < T; t++)
 #pragma unroll
             for (int j = 0; j < C; j++) S.Lb[q][t].v[j] = 0.0f;
+#endif
     }
+#if PF_JLAG_LDSL
+    constexpr int R = JLag<C, T, SRC, OUT16>::R;
+    __shared__ float lds_l[4 * R * 64 * C];  // per-wave private rings, no barriers needed
+    S.lring = lds_l + wave * (R * 64 * C);
+    S.lane_c = lane * C;
+#endif
 #if PF_JLAG_TOUCH
     S.touch_acc = 0;
 #pragma unroll
@@ -461,16 +531,27 @@ __global__ void __launch_bounds__(256, PF_JLAG_WAVES) k_jlag(JacobiPass P)
     int kfirst = S.r0 - T - 1;
     int k0 = kfirst - (((kfirst % 6) + 6) % 6);
     int kend = S.r1 + 2 * T;
-    // prime: L rows of step k0 (the rest are loaded one step ahead inside step())
+    // prime the L rows of step k0 (the rest are loaded one step ahead inside step()).  With the
+    // LDS ring the slots of rows before k0 stay unwritten: they only feed halo/stale cells,
+    // exactly like the zero-initialised level rows.
+#if PF_JLAG_LDSL
+    S.Lin[0] = S.load_row(S.lnorm, k0);  // k0 is even
+    int kb = ((k0 % R) + R) % R;
+#else
 #pragma unroll
     for (int t = 1; t <= T; t++) S.Lb[0][t - 1] = S.load_row(S.lnorm, k0 - 2 * t);
+    const int kb = 0;
+#endif
     for (int k = k0; k < kend; k += 6) {
-        S.template step<0>(k);
-        S.template step<1>(k + 1);
-        S.template step<2>(k + 2);
-        S.template step<3>(k + 3);
-        S.template step<4>(k + 4);
-        S.template step<5>(k + 5);
+        S.template step<0>(k, kb);
+        S.template step<1>(k + 1, kb);
+        S.template step<2>(k + 2, kb);
+        S.template step<3>(k + 3, kb);
+        S.template step<4>(k + 4, kb);
+        S.template step<5>(k + 5, kb);
+#if PF_JLAG_LDSL
+        kb = (kb + 6) % R;
+#endif
     }
 #if PF_JLAG_TOUCH
     // never true for real data (P.w > 0); keeps the touch loads from being optimised away

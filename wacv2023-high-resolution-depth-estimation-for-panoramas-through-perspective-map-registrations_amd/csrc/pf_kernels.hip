@@ -10,7 +10,13 @@
 namespace pf {
 
 static constexpr int kBlock = 256;
-static constexpr int kWarpBatch = 8;  // panoramas per thread in the E->P warps
+#ifndef PF_WARP_BATCH
+#define PF_WARP_BATCH 16
+#endif
+#ifndef PF_WARP_SWIZZLE
+#define PF_WARP_SWIZZLE 1
+#endif
+static constexpr int kWarpBatch = PF_WARP_BATCH;  // panoramas per thread in the E->P warps
 
 __device__ __forceinline__ float bits_f(uint32_t u) { return __uint_as_float(u); }
 __device__ __forceinline__ uint32_t f_bits(float f) { return __float_as_uint(f); }
@@ -422,22 +428,23 @@ __device__ __forceinline__ void world_to_sph(float p0, float p1, float p2, float
     zen = (float)atan2((double)ql, (double)p2);
 }
 
-__device__ __forceinline__ uint32_t hash32(uint32_t seed, uint32_t tile, uint32_t idx)
-{
-    uint64_t z = ((uint64_t)seed << 32) ^ ((uint64_t)tile << 24) ^ (uint64_t)idx;
-    z += 0x9E3779B97F4A7C15ull;
-    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
-    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
-    z ^= z >> 31;
-    return (uint32_t)(z >> 32);
+__device__ __forceinline__ uint32_t mix32(uint32_t x)
+{  // lowbias32 finaliser (the oracle's pfo_hash32)
+    x ^= x >> 16;
+    x *= 0x7FEB352Du;
+    x ^= x >> 15;
+    x *= 0x846CA68Bu;
+    x ^= x >> 16;
+    return x;
 }
 
-__global__ void __launch_bounds__(kBlock) k_warp_depth(const TileGeom* __restrict__ geom,
-                                                       int ntiles, const float* __restrict__ pano,
-                                                       int pw, int ph, long long pstride,
-                                                       const Resp* __restrict__ resp,
-                                                       float* __restrict__ tiles,
-                                                       long long tstride, int batch)
+// Warp map, once per (layout, panorama size): for every tile pixel the bilinear footprint of
+// its ToSphericalCoord direction (Depth.cpp:157-166) in the panorama at ValueAtCoord's pixel
+// convention.  wmap = y0*pw + x0 | (x1 != x0) << 31 | (y1 != y0) << 30;  wfxy = (fx, fy).
+// The per-panorama warp then does no trigonometry at all.
+__global__ void __launch_bounds__(kBlock) k_warpmap(const TileGeom* __restrict__ geom, int pw,
+                                                    int ph, uint32_t* __restrict__ wmap,
+                                                    float2* __restrict__ wfxy)
 {
     const int p = blockIdx.y;
     const TileGeom g = geom[p];
@@ -461,12 +468,46 @@ __global__ void __launch_bounds__(kBlock) k_warp_depth(const TileGeom* __restric
     if (y0 > ph - 1) { y0 = ph - 1; fy = 0; }
     int x1 = x0 + 1 < pw ? x0 + 1 : pw - 1;
     int y1 = y0 + 1 < ph ? y0 + 1 : ph - 1;
-    long long o00 = (long long)y0 * pw + x0, o01 = (long long)y0 * pw + x1;
-    long long o10 = (long long)y1 * pw + x0, o11 = (long long)y1 * pw + x1;
-    float wx0 = 1.0f - fx, wy0 = 1.0f - fy;
-    // kWarpBatch panoramas per thread (grid.z walks the batch): all their gathers are issued
-    // before the first use so each wave keeps 4*kWarpBatch loads in flight.
-    const int bbeg = blockIdx.z * kWarpBatch;
+    wmap[g.pix_off + i] = (uint32_t)(y0 * pw + x0) | (x1 != x0 ? 1u << 31 : 0u) |
+                          (y1 != y0 ? 1u << 30 : 0u);
+    wfxy[g.pix_off + i] = make_float2(fx, fy);
+}
+
+// E->P depth warp (a5 as a gather) + the synthetic depth-net response.  One thread owns one
+// tile pixel for kWarpBatch panoramas: it reads its warp-map entry once and issues all
+// 4*kWarpBatch corner gathers before the first use.  The 1-D grid is walked in an XCD-aware
+// order: blocks are dealt round-robin to the 8 XCDs, so logical block (x-range of one tile,
+// one batch chunk) ids are remapped to give every XCD a contiguous range -- the panorama
+// region a tile reads is then fetched into one XCD's L2, not all eight.
+__global__ void __launch_bounds__(kBlock) k_warp_depth(const TileGeom* __restrict__ geom,
+                                                       int ntiles, int nbx,
+                                                       const uint32_t* __restrict__ wmap,
+                                                       const float2* __restrict__ wfxy,
+                                                       const float* __restrict__ pano, int pw,
+                                                       long long pstride,
+                                                       const Resp* __restrict__ resp,
+                                                       float* __restrict__ tiles,
+                                                       long long tstride, int batch)
+{
+    const unsigned n = gridDim.x, bid = blockIdx.x;
+    const unsigned q8 = n / 8, r8 = n % 8, xcd = bid % 8;
+    const unsigned lid = PF_WARP_SWIZZLE
+                             ? (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + bid / 8
+                             : bid;
+    const int bx = (int)(lid % (unsigned)nbx);
+    const int p = (int)((lid / (unsigned)nbx) % (unsigned)ntiles);
+    const int z = (int)(lid / ((unsigned)nbx * (unsigned)ntiles));
+    const TileGeom& g = geom[p];
+    const int i = bx * kBlock + (int)threadIdx.x;
+    if (i >= g.w * g.h) return;
+    const uint32_t m = wmap[g.pix_off + i];
+    const float2 f = wfxy[g.pix_off + i];
+    const uint32_t o00 = m & 0x3FFFFFFFu, dx = m >> 31;
+    const uint32_t o10 = o00 + (((m >> 30) & 1u) ? (uint32_t)pw : 0u);
+    const uint32_t o01 = o00 + dx, o11 = o10 + dx;
+    const float fx = f.x, fy = f.y;
+    const float wx0 = 1.0f - fx, wy0 = 1.0f - fy;
+    const int bbeg = z * kWarpBatch;
     float t00[kWarpBatch], t01[kWarpBatch], t10[kWarpBatch], t11[kWarpBatch];
 #pragma unroll
     for (int q = 0; q < kWarpBatch; q++) {
@@ -486,7 +527,8 @@ __global__ void __launch_bounds__(kBlock) k_warp_depth(const TileGeom* __restric
         float v = top * wy0 + bot * fy;
         if (resp) {
             const Resp r = resp[(long long)b * ntiles + p];
-            uint32_t h = hash32(r.seed, (uint32_t)p, (uint32_t)i);
+            const uint32_t key = mix32(r.seed ^ mix32((uint32_t)p + 0x9E3779B9u));  // scalar
+            uint32_t h = mix32((uint32_t)i ^ key);
             float u = (float)(h >> 8) * (1.0f / 16777216.0f);
             float nz = u * 2.0f - 1.0f;
             float t = r.alpha * v;
@@ -497,7 +539,7 @@ __global__ void __launch_bounds__(kBlock) k_warp_depth(const TileGeom* __restric
             else if (t > 1) t = 1;
             v = t;
         }
-        tiles[b * tstride + g.off + i * g.c] = v;
+        (tiles + b * tstride + g.off)[i * g.c] = v;
     }
 }
 
@@ -645,13 +687,23 @@ void launch_apply_cubic(hipStream_t s, const TileGeom* geom, int ntiles, long lo
                        coeffs);
 }
 
-void launch_warp_depth(hipStream_t s, const TileGeom* geom, int ntiles, long long npix_max,
-                       const float* pano, int pw, int ph, long long pstride, const Resp* resp,
-                       float* tiles, long long tstride, int batch)
+void launch_warpmap(hipStream_t s, const TileGeom* geom, int ntiles, long long npix_max, int pw,
+                    int ph, uint32_t* wmap, float* wfxy)
 {
-    dim3 grid(nblocks(npix_max), ntiles, (batch + kWarpBatch - 1) / kWarpBatch);
-    hipLaunchKernelGGL(k_warp_depth, grid, dim3(kBlock), 0, s, geom, ntiles, pano, pw, ph,
-                       pstride, resp, tiles, tstride, batch);
+    dim3 grid(nblocks(npix_max), ntiles);
+    hipLaunchKernelGGL(k_warpmap, grid, dim3(kBlock), 0, s, geom, pw, ph, wmap, (float2*)wfxy);
+}
+
+void launch_warp_depth(hipStream_t s, const TileGeom* geom, int ntiles, long long npix_max,
+                       const uint32_t* wmap, const float* wfxy, const float* pano, int pw,
+                       int ph, long long pstride, const Resp* resp, float* tiles,
+                       long long tstride, int batch)
+{
+    (void)ph;
+    const int nbx = (int)nblocks(npix_max);
+    const long long n = (long long)nbx * ntiles * ((batch + kWarpBatch - 1) / kWarpBatch);
+    hipLaunchKernelGGL(k_warp_depth, dim3((unsigned)n), dim3(kBlock), 0, s, geom, ntiles, nbx, wmap,
+                       (const float2*)wfxy, pano, pw, pstride, resp, tiles, tstride, batch);
 }
 
 void launch_warp_rgb(hipStream_t s, const RgbCam* cams, const TileGeom* geom, int ntiles,
