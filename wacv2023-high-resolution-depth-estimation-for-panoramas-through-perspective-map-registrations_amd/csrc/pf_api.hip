@@ -52,10 +52,11 @@ struct pf_ctx {
     LevelCache lc;
     bool reg_valid = false;
     uint32_t reg_zr0 = 0, reg_zr1 = 0;
-    // E->P depth-warp map for one panorama size: per tile pixel the packed bilinear corner
-    // index and the (fx, fy) weights (k_warpmap), built on first use
-    int wmap_pw = 0, wmap_ph = 0;
-    DevBuf wmap, wfxy;
+    // E->P depth warp for one panorama size (pf_warp.hip): tile patches with their panorama
+    // boxes, per tile pixel the corner index in its box and the (fx, fy) weights; built on
+    // first use
+    int wmap_pw = 0, wmap_ph = 0, npatch = 0;
+    DevBuf wmap, wfxy, wpatch;
     // workspace
     DevBuf buf[3], lnorm, coeffs, lsum_ws;
     // stage profiling
@@ -313,7 +314,7 @@ void pf_destroy(pf_ctx* c)
     (void)hipStreamSynchronize(c->stream);
     DevBuf* all[] = {&c->geom, &c->reg, &c->rcols, &c->rrows, &c->cams, &c->rgb_off,
                      &c->buf[0], &c->buf[1], &c->buf[2], &c->lnorm, &c->coeffs, &c->lsum_ws,
-                     &c->wmap, &c->wfxy};
+                     &c->wmap, &c->wfxy, &c->wpatch};
     for (DevBuf* b : all) release(*b);
     for (int l = 0; l < 4; l++) {
         release(c->lc.box[l]);
@@ -462,7 +463,14 @@ int pf_set_tiles(pf_ctx* c, const pf_window* fovs, const pf_window* ranges, int 
     c->lc.out_w = 0;  // boxes and registration grids depend on the ranges: rebuild lazily
     c->reg_valid = false;
     c->wmap_pw = c->wmap_ph = 0;
+    std::vector<WarpPatch> patches;
+    const int pe = warp_patch_edge();
+    for (int i = 0; i < ntiles; i++)
+        for (int y = 0; y < tile_h[i]; y += pe)
+            for (int x = 0; x < tile_w[i]; x += pe) patches.push_back(WarpPatch{i, x, y, 0, 0, 0, 0, 0});
+    c->npatch = (int)patches.size();
     int rc;
+    if ((rc = upload(c, c->wpatch, patches))) return rc;
     if ((rc = upload(c, c->geom, c->geom_h))) return rc;
     if ((rc = upload(c, c->cams, cams))) return rc;
     if ((rc = upload(c, c->rgb_off, rgb_off))) return rc;
@@ -616,7 +624,7 @@ static int check_emap(pf_ctx* c, const float* emap, int ew, int eh, int ec)
 // Jacobi pass geometry: lanes own C columns, strips carry a Tp-column halo (Tp >= T, rounded to
 // C so vector rows stay aligned), row chunks sized to whole rounds of resident waves.
 struct JacobiTuning {
-    int C = 2, Tmax = 10, waves_target = 0, min_rows = 0, rounds = 1;
+    int C = 2, Tmax = 5, waves_target = 0, min_rows = 0, rounds = 1;
 };
 
 static JacobiTuning jacobi_tuning()
@@ -629,7 +637,7 @@ static JacobiTuning jacobi_tuning()
     if (const char* e = getenv("PF_JWAVES")) t.waves_target = atoi(e);
     if (const char* e = getenv("PF_JROWS")) t.min_rows = atoi(e);
     if (const char* e = getenv("PF_JROUNDS")) t.rounds = atoi(e) > 0 ? atoi(e) : 1;
-    if (!jstream_supported_T(t.Tmax)) t.Tmax = 10;
+    if (!jstream_supported_T(t.Tmax)) t.Tmax = 5;
     return t;
 }
 
@@ -872,22 +880,24 @@ int pf_warp_depth(pf_ctx* c, const float* pano, int pw, int ph, int batch,
     if (!pano || !tiles || pw < 2 || ph < 2)
         return fail(c, PF_EINVAL, "bad pano %p %dx%d", (const void*)pano, pw, ph);
     static_assert(sizeof(pf_response) == sizeof(Resp), "pf_response layout");
-    if ((long long)pw * ph >= (1ll << 30))
-        return fail(c, PF_EINVAL, "pano %dx%d: more than 2^30 pixels", pw, ph);
+    if ((long long)pw * ph >= (1ll << 30) || pw >= 65536 || ph >= 65536)
+        return fail(c, PF_EINVAL, "pano %dx%d: too large (< 2^30 pixels, sides < 65536)", pw, ph);
     const long long npix = c->tile_elems / c->tile_c;
     if (c->wmap_pw != pw || c->wmap_ph != ph) {
         if ((rc = ensure(c, c->wmap, sizeof(uint32_t) * npix))) return rc;
         if ((rc = ensure(c, c->wfxy, sizeof(float) * 2 * npix))) return rc;
-        launch_warpmap(c->stream, (const TileGeom*)c->geom.p, c->ntiles, c->npix_max, pw, ph,
-                       (uint32_t*)c->wmap.p, (float*)c->wfxy.p);
+        launch_warp_prepare(c->stream, (const TileGeom*)c->geom.p, c->ntiles, c->npix_max,
+                            (WarpPatch*)c->wpatch.p, c->npatch, pw, ph, (uint32_t*)c->wmap.p,
+                            (float*)c->wfxy.p);
         HIPCHK(c, hipGetLastError());
         c->wmap_pw = pw;
         c->wmap_ph = ph;
     }
     StageTimer t(c, PF_STAGE_WARP, batch * (4.0 * pw * ph + 4.0 * (double)npix), 1);
-    launch_warp_depth(c->stream, (const TileGeom*)c->geom.p, c->ntiles, c->npix_max,
-                      (const uint32_t*)c->wmap.p, (const float*)c->wfxy.p, pano, pw, ph,
-                      (long long)pw * ph, (const Resp*)resp, tiles, c->tile_elems, batch);
+    launch_warp_depth(c->stream, (const TileGeom*)c->geom.p, c->ntiles,
+                      (const WarpPatch*)c->wpatch.p, c->npatch, (const uint32_t*)c->wmap.p,
+                      (const float*)c->wfxy.p, pano, pw, ph, (long long)pw * ph,
+                      (const Resp*)resp, tiles, c->tile_elems, batch);
     HIPCHK(c, hipGetLastError());
     return PF_OK;
 }

@@ -61,6 +61,14 @@ struct Resp {
     uint32_t seed, pad;
 };
 
+// One square patch of a tile for the E->P depth warp (pf_warp.hip): its tile pixels and the
+// azimuth-unwrapped panorama box their bilinear corners fall in (filled on the device).
+struct WarpPatch {
+    int tile, X0, Y0;
+    int gx0, gy0, bw, bh;  // box origin (column mod pw, row) and size, +1 row/column
+    int wide;              // box larger than the LDS staging capacity: direct gathers
+};
+
 struct LevelDims {
     int w, h, h0, h1, iters, nlevels;
 };
@@ -174,11 +182,13 @@ void launch_register(hipStream_t s, const TileGeom* geom, const RegGrid* grids,
                      int batch);
 void launch_apply_cubic(hipStream_t s, const TileGeom* geom, int ntiles, long long tile_elems,
                         float* tiles, long long tstride, const float* coeffs, int batch);
-void launch_warpmap(hipStream_t s, const TileGeom* geom, int ntiles, long long npix_max, int pw,
-                    int ph, uint32_t* wmap, float* wfxy);
-void launch_warp_depth(hipStream_t s, const TileGeom* geom, int ntiles, long long npix_max,
-                       const uint32_t* wmap, const float* wfxy, const float* pano, int pw,
-                       int ph, long long pstride, const Resp* resp, float* tiles,
+int warp_patch_edge();
+void launch_warp_prepare(hipStream_t s, const TileGeom* geom, int ntiles, long long npix_max,
+                         WarpPatch* patches, int npatch, int pw, int ph, uint32_t* wloc,
+                         float* wfxy);
+void launch_warp_depth(hipStream_t s, const TileGeom* geom, int ntiles, const WarpPatch* patches,
+                       int npatch, const uint32_t* wloc, const float* wfxy, const float* pano,
+                       int pw, int ph, long long pstride, const Resp* resp, float* tiles,
                        long long tstride, int batch);
 void launch_warp_rgb(hipStream_t s, const RgbCam* cams, const TileGeom* geom, int ntiles,
                      long long npix_total, const long long* pix_prefix,

@@ -39,6 +39,9 @@
 #ifndef PF_JLAG_LDSL
 #define PF_JLAG_LDSL 1  // L rows through a per-wave LDS ring (1) or per-level registers (0)
 #endif
+#ifndef PF_JLAG_PF
+#define PF_JLAG_PF 2  // steps of lead for the input and L row loads (1 or 2)
+#endif
 #ifndef PF_JLAG_TOUCH
 #define PF_JLAG_TOUCH 0  // steps of lead for L2 touch loads (0 = off; measured slower)
 #endif
@@ -236,13 +239,16 @@ __global__ void __launch_bounds__(256) k_jstream(JacobiPass P)
 template <int C, int T, int SRC, bool OUT16>
 struct JLag {
     Row<C> H[T][3];   // H[t][r % 3] = level t row r
-    Row<C> In[2];     // input row r lands in In[r & 1] (loaded at step r, used from r + 1)
+    // Input rows are loaded PF steps before their first use: row r lands in In[r % NB] (issued
+    // at step r + 1 - PF, consumed at step r + 1).  NB divides the unroll factor 6.
+    static constexpr int PF = PF_JLAG_PF, NB = PF_JLAG_PF + 1;
+    Row<C> In[NB];
 #if PF_JLAG_LDSL
     // L rows live in a per-wave LDS ring of R = 2T+1 rows (row r in slot r % R): each L row is
     // loaded from memory once (one step ahead, into Lin) and read T times from LDS, instead of
     // T global loads per step held in 2*T*C registers.
     static constexpr int R = 2 * T + 1;
-    Row<C> Lin[2];    // L row r lands in Lin[r & 1] during step r-1, is stored to LDS at step r
+    Row<C> Lin[NB];   // L row r lands in Lin[r % NB] (issued at step r - PF), stored to LDS at step r
     float* lring;     // this wave's ring: R rows of 64*C floats
     int lane_c;       // lane * C (LDS column offset)
 #else
@@ -349,12 +355,12 @@ struct JLag {
     __device__ __forceinline__ void step(int k, int kb)
     {
         // level-0 row k-1 (loaded last step) joins the ring
-        H[0][slot(PH, 1)] = In[(PH + 1) & 1];
+        H[0][slot(PH, 1)] = In[(PH + NB - 1) % NB];
 #if PF_JLAG_LDSL
         // L row k (landed in Lin last step) goes to its ring slot; fetch L row k+1.  The slot
         // is reused by row k+R > k, after every level has read row k (last read at k + 2T).
-        lds_put(lslot(kb, PH), Lin[PH & 1]);
-        Lin[(PH + 1) & 1] = load_row(lnorm, k + 1);
+        lds_put(lslot(kb, PH), Lin[PH % NB]);
+        Lin[(PH + PF) % NB] = load_row(lnorm, k + PF);
         Row<C> Lv[T];
 #pragma unroll
         for (int t = 1; t <= T; t++) Lv[t - 1] = lds_get(lslot(kb, PH - 2 * t));
@@ -373,7 +379,7 @@ struct JLag {
         Tch[PH & 1][1] = load_row(lnorm, k + PF_JLAG_TOUCH);
 #endif
         // loads for the next step: input row k, L rows (k+1) - 2t
-        In[PH & 1] = load_input(k);
+        In[(PH + PF - 1) % NB] = load_input(k + PF - 1);
 #if !PF_JLAG_LDSL
 #pragma unroll
         for (int t = 1; t <= T; t++) Lb[(PH + 1) & 1][t - 1] = load_row(lnorm, k + 1 - 2 * t);
@@ -497,20 +503,24 @@ __global__ void __launch_bounds__(256, PF_JLAG_WAVES) k_jlag(JacobiPass P)
         for (int q = 0; q < 3; q++)
 #pragma unroll
             for (int j = 0; j < C; j++) S.H[t][q].v[j] = 0.0f;
+    constexpr int NB = JLag<C, T, SRC, OUT16>::NB;
 #pragma unroll
-    for (int q = 0; q < 2; q++) {
+    for (int q = 0; q < NB; q++) {
 #pragma unroll
         for (int j = 0; j < C; j++) S.In[q].v[j] = 0.0f;
 #if PF_JLAG_LDSL
 #pragma unroll
         for (int j = 0; j < C; j++) S.Lin[q].v[j] = 0.0f;
-#else
+#endif
+    }
+#if !PF_JLAG_LDSL
+#pragma unroll
+    for (int q = 0; q < 2; q++)
 #pragma unroll
         for (int t = 0; t < T; t++)
 #pragma unroll
             for (int j = 0; j < C; j++) S.Lb[q][t].v[j] = 0.0f;
 #endif
-    }
 #if PF_JLAG_LDSL
     constexpr int R = JLag<C, T, SRC, OUT16>::R;
     __shared__ float lds_l[4 * R * 64 * C];  // per-wave private rings, no barriers needed
@@ -531,11 +541,15 @@ __global__ void __launch_bounds__(256, PF_JLAG_WAVES) k_jlag(JacobiPass P)
     int kfirst = S.r0 - T - 1;
     int k0 = kfirst - (((kfirst % 6) + 6) % 6);
     int kend = S.r1 + 2 * T;
-    // prime the L rows of step k0 (the rest are loaded one step ahead inside step()).  With the
-    // LDS ring the slots of rows before k0 stay unwritten: they only feed halo/stale cells,
-    // exactly like the zero-initialised level rows.
+    // prime the rows the first steps consume before their in-loop loads land (the rest are
+    // loaded PF steps ahead inside step()).  With the LDS ring the slots of rows before k0 stay
+    // unwritten: they only feed halo/stale cells, exactly like the zero-initialised level rows.
+    // k0 is a multiple of 6, so row k0 + r sits in buffer r.
+#pragma unroll
+    for (int r = 0; r + 1 < JLag<C, T, SRC, OUT16>::PF; r++) S.In[r] = S.load_input(k0 + r);
 #if PF_JLAG_LDSL
-    S.Lin[0] = S.load_row(S.lnorm, k0);  // k0 is even
+#pragma unroll
+    for (int r = 0; r < JLag<C, T, SRC, OUT16>::PF; r++) S.Lin[r] = S.load_row(S.lnorm, k0 + r);
     int kb = ((k0 % R) + R) % R;
 #else
 #pragma unroll

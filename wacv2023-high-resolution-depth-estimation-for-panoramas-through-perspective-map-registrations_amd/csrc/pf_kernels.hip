@@ -10,13 +10,6 @@
 namespace pf {
 
 static constexpr int kBlock = 256;
-#ifndef PF_WARP_BATCH
-#define PF_WARP_BATCH 16
-#endif
-#ifndef PF_WARP_SWIZZLE
-#define PF_WARP_SWIZZLE 1
-#endif
-static constexpr int kWarpBatch = PF_WARP_BATCH;  // panoramas per thread in the E->P warps
 
 __device__ __forceinline__ float bits_f(uint32_t u) { return __uint_as_float(u); }
 __device__ __forceinline__ uint32_t f_bits(float f) { return __float_as_uint(f); }
@@ -394,155 +387,6 @@ __global__ void __launch_bounds__(kBlock) k_apply_cubic(const TileGeom* __restri
         t[i * g.c] = cubic_map(t[i * g.c], abcd.x, abcd.y, abcd.z, abcd.w);
 }
 
-// ---------------------------------------------------------------------------------------------
-// E->P depth warp (a5 mapping).  The spherical coordinate of a tile pixel does not depend on
-// the panorama, so each thread computes it once and loops over the batch.
-__device__ __forceinline__ void world_to_sph(float p0, float p1, float p2, float& az,
-                                             float& zen)
-{  // Depth.cpp:2960-2971, Imath normalize/length; atan2 evaluated in fp64 and rounded
-    float l2 = p0 * p0 + p1 * p1 + p2 * p2;
-    float l;
-    if (l2 < 2.0f * FLT_MIN) {
-        float ax = fabsf(p0), ay = fabsf(p1), az_ = fabsf(p2);
-        float mx = ax;
-        if (mx < ay) mx = ay;
-        if (mx < az_) mx = az_;
-        if (mx == 0.0f) l = 0.0f;
-        else { ax /= mx; ay /= mx; az_ /= mx; l = mx * sqrtf(ax * ax + ay * ay + az_ * az_); }
-    } else
-        l = sqrtf(l2);
-    if (l != 0.0f) { p0 /= l; p1 /= l; p2 /= l; }
-    float a = (float)atan2((double)p1, (double)p0);
-    float azf = (float)fmod((double)a, 2 * PF_MYPI);
-    if (azf < 0) azf = (float)((double)azf + 2 * PF_MYPI);
-    float q2 = p0 * p0 + p1 * p1;
-    float ql;
-    if (q2 < 2.0f * FLT_MIN) {
-        float ax = fabsf(p0), ay = fabsf(p1);
-        float mx = ax < ay ? ay : ax;
-        if (mx == 0.0f) ql = 0.0f;
-        else { ax /= mx; ay /= mx; ql = mx * sqrtf(ax * ax + ay * ay); }
-    } else
-        ql = sqrtf(q2);
-    az = azf;
-    zen = (float)atan2((double)ql, (double)p2);
-}
-
-__device__ __forceinline__ uint32_t mix32(uint32_t x)
-{  // lowbias32 finaliser (the oracle's pfo_hash32)
-    x ^= x >> 16;
-    x *= 0x7FEB352Du;
-    x ^= x >> 15;
-    x *= 0x846CA68Bu;
-    x ^= x >> 16;
-    return x;
-}
-
-// Warp map, once per (layout, panorama size): for every tile pixel the bilinear footprint of
-// its ToSphericalCoord direction (Depth.cpp:157-166) in the panorama at ValueAtCoord's pixel
-// convention.  wmap = y0*pw + x0 | (x1 != x0) << 31 | (y1 != y0) << 30;  wfxy = (fx, fy).
-// The per-panorama warp then does no trigonometry at all.
-__global__ void __launch_bounds__(kBlock) k_warpmap(const TileGeom* __restrict__ geom, int pw,
-                                                    int ph, uint32_t* __restrict__ wmap,
-                                                    float2* __restrict__ wfxy)
-{
-    const int p = blockIdx.y;
-    const TileGeom g = geom[p];
-    long long npx = (long long)g.w * g.h;
-    long long i = (long long)blockIdx.x * kBlock + threadIdx.x;
-    if (i >= npx) return;
-    int Y = (int)(i / g.w), X = (int)(i - (long long)Y * g.w);
-    float xf = (float)X / (float)(g.w - 1), yf = (float)Y / (float)(g.h - 1);
-    float q0 = g.corner0[0] + g.hedge[0] * xf, q1 = g.corner0[1] + g.hedge[1] * xf,
-          q2 = g.corner0[2] + g.hedge[2] * xf;
-    q0 = q0 + g.vedge[0] * yf; q1 = q1 + g.vedge[1] * yf; q2 = q2 + g.vedge[2] * yf;
-    float az, zen;
-    world_to_sph(q0, q1, q2, az, zen);
-    float px = (float)((double)az / (2 * PF_MYPI) * (double)(pw - 1));
-    float py = (float)((double)zen / PF_MYPI * (double)(ph - 1));
-    int x0 = (int)floorf(px), y0 = (int)floorf(py);
-    float fx = px - (float)x0, fy = py - (float)y0;
-    if (x0 < 0) { x0 = 0; fx = 0; }
-    if (y0 < 0) { y0 = 0; fy = 0; }
-    if (x0 > pw - 1) { x0 = pw - 1; fx = 0; }
-    if (y0 > ph - 1) { y0 = ph - 1; fy = 0; }
-    int x1 = x0 + 1 < pw ? x0 + 1 : pw - 1;
-    int y1 = y0 + 1 < ph ? y0 + 1 : ph - 1;
-    wmap[g.pix_off + i] = (uint32_t)(y0 * pw + x0) | (x1 != x0 ? 1u << 31 : 0u) |
-                          (y1 != y0 ? 1u << 30 : 0u);
-    wfxy[g.pix_off + i] = make_float2(fx, fy);
-}
-
-// E->P depth warp (a5 as a gather) + the synthetic depth-net response.  One thread owns one
-// tile pixel for kWarpBatch panoramas: it reads its warp-map entry once and issues all
-// 4*kWarpBatch corner gathers before the first use.  The 1-D grid is walked in an XCD-aware
-// order: blocks are dealt round-robin to the 8 XCDs, so logical block (x-range of one tile,
-// one batch chunk) ids are remapped to give every XCD a contiguous range -- the panorama
-// region a tile reads is then fetched into one XCD's L2, not all eight.
-__global__ void __launch_bounds__(kBlock) k_warp_depth(const TileGeom* __restrict__ geom,
-                                                       int ntiles, int nbx,
-                                                       const uint32_t* __restrict__ wmap,
-                                                       const float2* __restrict__ wfxy,
-                                                       const float* __restrict__ pano, int pw,
-                                                       long long pstride,
-                                                       const Resp* __restrict__ resp,
-                                                       float* __restrict__ tiles,
-                                                       long long tstride, int batch)
-{
-    const unsigned n = gridDim.x, bid = blockIdx.x;
-    const unsigned q8 = n / 8, r8 = n % 8, xcd = bid % 8;
-    const unsigned lid = PF_WARP_SWIZZLE
-                             ? (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + bid / 8
-                             : bid;
-    const int bx = (int)(lid % (unsigned)nbx);
-    const int p = (int)((lid / (unsigned)nbx) % (unsigned)ntiles);
-    const int z = (int)(lid / ((unsigned)nbx * (unsigned)ntiles));
-    const TileGeom& g = geom[p];
-    const int i = bx * kBlock + (int)threadIdx.x;
-    if (i >= g.w * g.h) return;
-    const uint32_t m = wmap[g.pix_off + i];
-    const float2 f = wfxy[g.pix_off + i];
-    const uint32_t o00 = m & 0x3FFFFFFFu, dx = m >> 31;
-    const uint32_t o10 = o00 + (((m >> 30) & 1u) ? (uint32_t)pw : 0u);
-    const uint32_t o01 = o00 + dx, o11 = o10 + dx;
-    const float fx = f.x, fy = f.y;
-    const float wx0 = 1.0f - fx, wy0 = 1.0f - fy;
-    const int bbeg = z * kWarpBatch;
-    float t00[kWarpBatch], t01[kWarpBatch], t10[kWarpBatch], t11[kWarpBatch];
-#pragma unroll
-    for (int q = 0; q < kWarpBatch; q++) {
-        const int b = bbeg + q < batch ? bbeg + q : batch - 1;
-        const float* pp = pano + b * pstride;
-        t00[q] = pp[o00];
-        t01[q] = pp[o01];
-        t10[q] = pp[o10];
-        t11[q] = pp[o11];
-    }
-#pragma unroll
-    for (int q = 0; q < kWarpBatch; q++) {
-        const int b = bbeg + q;
-        if (b >= batch) break;
-        float top = t00[q] * wx0 + t01[q] * fx;
-        float bot = t10[q] * wx0 + t11[q] * fx;
-        float v = top * wy0 + bot * fy;
-        if (resp) {
-            const Resp r = resp[(long long)b * ntiles + p];
-            const uint32_t key = mix32(r.seed ^ mix32((uint32_t)p + 0x9E3779B9u));  // scalar
-            uint32_t h = mix32((uint32_t)i ^ key);
-            float u = (float)(h >> 8) * (1.0f / 16777216.0f);
-            float nz = u * 2.0f - 1.0f;
-            float t = r.alpha * v;
-            t = t + (r.kappa * v) * v;
-            t = t + r.beta;
-            t = t + r.sigma * nz;
-            if (t < 0) t = 0;
-            else if (t > 1) t = 1;
-            v = t;
-        }
-        (tiles + b * tstride + g.off)[i * g.c] = v;
-    }
-}
-
 // E->P RGB warp with the GL camera (a18).
 __global__ void __launch_bounds__(kBlock) k_warp_rgb(const RgbCam* __restrict__ cams,
                                                      const TileGeom* __restrict__ geom,
@@ -685,25 +529,6 @@ void launch_apply_cubic(hipStream_t s, const TileGeom* geom, int ntiles, long lo
     dim3 grid(gx, ntiles, batch);
     hipLaunchKernelGGL(k_apply_cubic, grid, dim3(kBlock), 0, s, geom, ntiles, tiles, tstride,
                        coeffs);
-}
-
-void launch_warpmap(hipStream_t s, const TileGeom* geom, int ntiles, long long npix_max, int pw,
-                    int ph, uint32_t* wmap, float* wfxy)
-{
-    dim3 grid(nblocks(npix_max), ntiles);
-    hipLaunchKernelGGL(k_warpmap, grid, dim3(kBlock), 0, s, geom, pw, ph, wmap, (float2*)wfxy);
-}
-
-void launch_warp_depth(hipStream_t s, const TileGeom* geom, int ntiles, long long npix_max,
-                       const uint32_t* wmap, const float* wfxy, const float* pano, int pw,
-                       int ph, long long pstride, const Resp* resp, float* tiles,
-                       long long tstride, int batch)
-{
-    (void)ph;
-    const int nbx = (int)nblocks(npix_max);
-    const long long n = (long long)nbx * ntiles * ((batch + kWarpBatch - 1) / kWarpBatch);
-    hipLaunchKernelGGL(k_warp_depth, dim3((unsigned)n), dim3(kBlock), 0, s, geom, ntiles, nbx, wmap,
-                       (const float2*)wfxy, pano, pw, pstride, resp, tiles, tstride, batch);
 }
 
 void launch_warp_rgb(hipStream_t s, const RgbCam* cams, const TileGeom* geom, int ntiles,

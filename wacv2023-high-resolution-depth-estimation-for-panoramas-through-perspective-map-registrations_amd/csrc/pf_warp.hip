@@ -1,0 +1,400 @@
+// pf_warp.hip -- E->P depth warp as an LDS-staged gather for gfx950.
+//
+// For every tile pixel (X, Y) the reference mapping is ToSphericalCoord (Depth.cpp:157-166):
+// corner0 + hedge*x + vedge*y -> WorldToSpherical (Depth.cpp:2960-2971) -> a bilinear sample of
+// the panorama at ValueAtCoord's pixel convention (az/2pi*(pw-1), zen/pi*(ph-1)).  That mapping
+// depends only on the layout and the panorama size, so it is evaluated once (three small
+// passes, cached by the context) and the per-call kernel does no trigonometry:
+//
+//  1. k_warp_coords: per tile pixel the bilinear corner (x0, y0) and weights (fx, fy).
+//  2. k_patch_box:   tiles are cut into 32x32-pixel patches; per patch the panorama footprint
+//                    (an azimuth-unwrapped box, <= kCap floats, or "wide").
+//  3. k_warp_local:  per tile pixel the corner's index inside its patch's footprint box (or the
+//                    global index with edge flags for a wide patch).
+//
+// k_warp_depth: one block per (patch, chunk of kNB panoramas).  Per panorama the block copies the
+// footprint box from HBM into LDS with plain coalesced row loads (double-buffered: the loads for
+// panorama q+1 are in flight while panorama q is interpolated), then every pixel reads its four
+// corners from LDS.  The box is ~0.4x the panorama's bytes per panorama (vs ~4 scattered corner
+// loads per tile pixel from L2 in a direct gather), so the kernel is bound by the tile writes.
+//
+// Edge rule: the reference clamps x1 = min(x0+1, pw-1), y1 = min(y0+1, ph-1).  x0 == pw-1 only
+// when px == pw-1 exactly (az < 2*MYPI), i.e. fx == 0, and likewise y0 == ph-1 means fy == 0; the
+// neighbour's weight is then exactly zero, so the box may hold any finite value there (the box
+// wraps in azimuth and clamps rows).  Inputs are depth maps, finite by contract.
+#include "pf_internal.hpp"
+
+#include <cfloat>
+#include <type_traits>
+
+namespace pf {
+
+static constexpr int kWB = 256;                         // threads per block
+static constexpr int kPatch = 32;                       // patch edge in tile pixels
+static constexpr int kPx = kPatch * kPatch / kWB;       // pixels per thread
+#ifndef PF_WARP_CAP
+#define PF_WARP_CAP 3072
+#endif
+static constexpr int kCap = PF_WARP_CAP;                // LDS floats per staged footprint
+static constexpr int kSlots = kCap / kWB;               // staging loads per thread
+#ifndef PF_WARP_BATCH
+#define PF_WARP_BATCH 16
+#endif
+static constexpr int kNB = PF_WARP_BATCH;               // panoramas per block
+
+__device__ __forceinline__ void world_to_sph(float p0, float p1, float p2, float& az,
+                                             float& zen)
+{  // Depth.cpp:2960-2971, Imath normalize/length; atan2 evaluated in fp64 and rounded
+    float l2 = p0 * p0 + p1 * p1 + p2 * p2;
+    float l;
+    if (l2 < 2.0f * FLT_MIN) {
+        float ax = fabsf(p0), ay = fabsf(p1), az_ = fabsf(p2);
+        float mx = ax;
+        if (mx < ay) mx = ay;
+        if (mx < az_) mx = az_;
+        if (mx == 0.0f) l = 0.0f;
+        else { ax /= mx; ay /= mx; az_ /= mx; l = mx * sqrtf(ax * ax + ay * ay + az_ * az_); }
+    } else
+        l = sqrtf(l2);
+    if (l != 0.0f) { p0 /= l; p1 /= l; p2 /= l; }
+    float a = (float)atan2((double)p1, (double)p0);
+    float azf = (float)fmod((double)a, 2 * PF_MYPI);
+    if (azf < 0) azf = (float)((double)azf + 2 * PF_MYPI);
+    float q2 = p0 * p0 + p1 * p1;
+    float ql;
+    if (q2 < 2.0f * FLT_MIN) {
+        float ax = fabsf(p0), ay = fabsf(p1);
+        float mx = ax < ay ? ay : ax;
+        if (mx == 0.0f) ql = 0.0f;
+        else { ax /= mx; ay /= mx; ql = mx * sqrtf(ax * ax + ay * ay); }
+    } else
+        ql = sqrtf(q2);
+    az = azf;
+    zen = (float)atan2((double)ql, (double)p2);
+}
+
+__device__ __forceinline__ uint32_t mix32(uint32_t x)
+{  // lowbias32 finaliser (the oracle's pfo_hash32)
+    x ^= x >> 16;
+    x *= 0x7FEB352Du;
+    x ^= x >> 15;
+    x *= 0x846CA68Bu;
+    x ^= x >> 16;
+    return x;
+}
+
+// Pass 1: bilinear corner and weights of every tile pixel; wxy = x0 | y0 << 16.
+__global__ void __launch_bounds__(kWB) k_warp_coords(const TileGeom* __restrict__ geom, int pw,
+                                                     int ph, uint32_t* __restrict__ wxy,
+                                                     float2* __restrict__ wfxy)
+{
+    const int p = blockIdx.y;
+    const TileGeom g = geom[p];
+    long long npx = (long long)g.w * g.h;
+    long long i = (long long)blockIdx.x * kWB + threadIdx.x;
+    if (i >= npx) return;
+    int Y = (int)(i / g.w), X = (int)(i - (long long)Y * g.w);
+    float xf = (float)X / (float)(g.w - 1), yf = (float)Y / (float)(g.h - 1);
+    float q0 = g.corner0[0] + g.hedge[0] * xf, q1 = g.corner0[1] + g.hedge[1] * xf,
+          q2 = g.corner0[2] + g.hedge[2] * xf;
+    q0 = q0 + g.vedge[0] * yf; q1 = q1 + g.vedge[1] * yf; q2 = q2 + g.vedge[2] * yf;
+    float az, zen;
+    world_to_sph(q0, q1, q2, az, zen);
+    float px = (float)((double)az / (2 * PF_MYPI) * (double)(pw - 1));
+    float py = (float)((double)zen / PF_MYPI * (double)(ph - 1));
+    int x0 = (int)floorf(px), y0 = (int)floorf(py);
+    float fx = px - (float)x0, fy = py - (float)y0;
+    if (x0 < 0) { x0 = 0; fx = 0; }
+    if (y0 < 0) { y0 = 0; fy = 0; }
+    if (x0 > pw - 1) { x0 = pw - 1; fx = 0; }
+    if (y0 > ph - 1) { y0 = ph - 1; fy = 0; }
+    wxy[g.pix_off + i] = (uint32_t)x0 | ((uint32_t)y0 << 16);
+    wfxy[g.pix_off + i] = make_float2(fx, fy);
+}
+
+__device__ __forceinline__ int patch_pixel(const WarpPatch& P, const TileGeom& g, int t, int k,
+                                           int& i)
+{  // thread t, slot k -> tile pixel index i; returns 0 outside the tile
+    const int X = P.X0 + (t & (kPatch - 1)), Y = P.Y0 + t / kPatch + k * (kWB / kPatch);
+    i = Y * g.w + X;
+    return X < g.w && Y < g.h;
+}
+
+__device__ __forceinline__ int wrap_du(int d, int pw)
+{
+    if (d > pw / 2) d -= pw;
+    if (d < -(pw / 2)) d += pw;
+    return d;
+}
+
+// Pass 2: per patch the azimuth-unwrapped footprint box of all its corners (+1 row/column).
+__global__ void __launch_bounds__(kWB) k_patch_box(const TileGeom* __restrict__ geom,
+                                                   WarpPatch* __restrict__ patches, int pw,
+                                                   const uint32_t* __restrict__ wxy)
+{
+    __shared__ int red[4];
+    WarpPatch P = patches[blockIdx.x];
+    const TileGeom& g = geom[P.tile];
+    const int t = threadIdx.x;
+    const int ref = (int)(wxy[g.pix_off + P.Y0 * g.w + P.X0] & 0xFFFFu);
+    if (t == 0) { red[0] = INT32_MAX; red[1] = INT32_MIN; red[2] = INT32_MAX; red[3] = INT32_MIN; }
+    __syncthreads();
+    int umin = INT32_MAX, umax = INT32_MIN, ymin = INT32_MAX, ymax = INT32_MIN;
+#pragma unroll
+    for (int k = 0; k < kPx; k++) {
+        int i;
+        if (!patch_pixel(P, g, t, k, i)) continue;
+        const uint32_t m = wxy[g.pix_off + i];
+        const int du = wrap_du((int)(m & 0xFFFFu) - ref, pw), y = (int)(m >> 16);
+        umin = min(umin, du); umax = max(umax, du);
+        ymin = min(ymin, y); ymax = max(ymax, y);
+    }
+    atomicMin(&red[0], umin); atomicMax(&red[1], umax);
+    atomicMin(&red[2], ymin); atomicMax(&red[3], ymax);
+    __syncthreads();
+    if (t == 0) {
+        int gx0 = ref + red[0];
+        gx0 = gx0 < 0 ? gx0 + pw : (gx0 >= pw ? gx0 - pw : gx0);
+        P.gx0 = gx0;
+        P.gy0 = red[2];
+        P.bw = red[1] - red[0] + 2;
+        P.bh = red[3] - red[2] + 2;
+        P.wide = (P.bw * P.bh > kCap || P.bw > pw / 2) ? 1 : 0;
+        patches[blockIdx.x] = P;
+    }
+}
+
+// Pass 3: per tile pixel the corner index inside its patch's box (or, for a wide patch, the
+// global index | (x1 != x0) << 31 | (y1 != y0) << 30).  In place over wxy.
+__global__ void __launch_bounds__(kWB) k_warp_local(const TileGeom* __restrict__ geom,
+                                                    const WarpPatch* __restrict__ patches,
+                                                    int pw, int ph, uint32_t* __restrict__ wxy)
+{
+    const WarpPatch P = patches[blockIdx.x];
+    const TileGeom& g = geom[P.tile];
+    const int t = threadIdx.x;
+#pragma unroll
+    for (int k = 0; k < kPx; k++) {
+        int i;
+        if (!patch_pixel(P, g, t, k, i)) continue;
+        const uint32_t m = wxy[g.pix_off + i];
+        const int x0 = (int)(m & 0xFFFFu), y0 = (int)(m >> 16);
+        uint32_t o;
+        if (P.wide) {
+            o = (uint32_t)(y0 * pw + x0) | (x0 < pw - 1 ? 1u << 31 : 0u) |
+                (y0 < ph - 1 ? 1u << 30 : 0u);
+        } else {
+            int d = x0 - P.gx0;
+            if (d < 0) d += pw;
+            o = (uint32_t)((y0 - P.gy0) * P.bw + d);
+        }
+        wxy[g.pix_off + i] = o;
+    }
+}
+
+// Per-panorama response of one tile with its noise key, staged in LDS at block start (a scalar
+// load per panorama inside the loop would expose its latency on lgkmcnt with the LDS reads).
+struct RespK {
+    float alpha, kappa, beta, sigma;
+    uint32_t key, on, pad[2];
+};
+
+__device__ __forceinline__ RespK resp_key(const Resp* __restrict__ resp, int b, int ntiles,
+                                          int tile)
+{
+    RespK k{};
+    if (resp) {
+        const Resp r = resp[(long long)b * ntiles + tile];
+        k.alpha = r.alpha; k.kappa = r.kappa; k.beta = r.beta; k.sigma = r.sigma;
+        k.key = mix32(r.seed ^ mix32((uint32_t)tile + 0x9E3779B9u));
+        k.on = 1;
+    }
+    return k;
+}
+
+// Bilinear sample (Depth.cpp-convention weights, no contraction) + the synthetic depth-net
+// response d' = clamp01(alpha*d + (kappa*d)*d + beta + sigma*u), u uniform in [-1, 1).
+__device__ __forceinline__ float warp_value(float t00, float t01, float t10, float t11, float fx,
+                                            float fy, const RespK& rk, uint32_t i)
+{
+    float top = t00 * (1.0f - fx) + t01 * fx;
+    float bot = t10 * (1.0f - fx) + t11 * fx;
+    float v = top * (1.0f - fy) + bot * fy;
+    if (rk.on) {
+        const RespK* r = &rk;
+        const uint32_t key = rk.key;
+        uint32_t h = mix32(i ^ key);
+        float u = (float)(h >> 8) * (1.0f / 16777216.0f);
+        float nz = u * 2.0f - 1.0f;
+        float t = r->alpha * v;
+        t = t + (r->kappa * v) * v;
+        t = t + r->beta;
+        t = t + r->sigma * nz;
+        if (t < 0) t = 0;
+        else if (t > 1) t = 1;
+        v = t;
+    }
+    return v;
+}
+
+struct WarpLanes {  // one thread's kPx pixels
+    const uint32_t* li;
+    const float *fx, *fy;
+    const uint32_t* pix;
+    const bool* ok;
+};
+
+// LDS-staged interpolation of kNB panoramas for a box of at most NS*256 floats.  Every staging
+// load is issued unconditionally (slots past the box reload a valid element, panoramas past the
+// chunk reload the last one), so the loads for panorama q+2 go out before panorama q is
+// interpolated and the wait for panorama q+1's loads -- an in-order vmcnt -- never covers them.
+template <int NS>
+__device__ __forceinline__ void warp_staged(float (*box)[kCap], const RespK* rk,
+                                            const WarpPatch& P, const TileGeom& g, int t,
+                                            const WarpLanes& W, const float* __restrict__ pano,
+                                            int pw, int ph, long long pstride,
+                                            float* __restrict__ tiles, long long tstride,
+                                            int bbeg, int nb)
+{
+    const int bw = P.bw, area = P.bw * P.bh;
+    uint32_t goff[NS];  // element e = t + 256*s of the bw x bh box -> panorama offset
+#pragma unroll
+    for (int s = 0; s < NS; s++) {
+        int e = t + s * kWB;
+        e = e < area ? e : area - 1;
+        const int r = e / bw, c = e - r * bw;
+        int row = P.gy0 + r;
+        row = row < ph ? row : ph - 1;
+        int col = P.gx0 + c;
+        col = col < pw ? col : col - pw;
+        goff[s] = (uint32_t)(row * pw + col);
+    }
+    float stg[2][NS];
+    auto fetch = [&](float* dst, int q) {
+        const float* pp = pano + (long long)(bbeg + (q < nb ? q : nb - 1)) * pstride;
+#pragma unroll
+        for (int s = 0; s < NS; s++) dst[s] = pp[goff[s]];
+    };
+    auto put = [&](float* dst, const float* src) {
+#pragma unroll
+        for (int s = 0; s < NS; s++) dst[t + s * kWB] = src[s];
+    };
+    auto iter = [&](auto parity, int q) {
+        constexpr int PA = decltype(parity)::value;
+        fetch(stg[PA], q + 2);  // panorama q was put into box[PA] last iteration: reuse stg[PA]
+        const float* L = box[PA];
+        const int b = bbeg + q;
+        const RespK r = rk[q];
+        float* out = tiles + b * tstride + g.off;
+#pragma unroll
+        for (int k = 0; k < kPx; k++) {
+            const float* c = L + W.li[k];
+            const float v = warp_value(c[0], c[1], c[bw], c[bw + 1], W.fx[k], W.fy[k], r,
+                                       W.pix[k]);
+            if (W.ok[k]) out[(long long)W.pix[k] * g.c] = v;
+        }
+        put(box[1 - PA], stg[1 - PA]);  // panorama q+1 (a duplicate past the chunk: unread)
+        __syncthreads();
+    };
+    fetch(stg[0], 0);
+    fetch(stg[1], 1);
+    put(box[0], stg[0]);
+    __syncthreads();
+    for (int q = 0; q < nb; q += 2) {
+        iter(std::integral_constant<int, 0>{}, q);
+        if (q + 1 < nb) iter(std::integral_constant<int, 1>{}, q + 1);
+    }
+}
+
+__global__ void __launch_bounds__(kWB) k_warp_depth(const TileGeom* __restrict__ geom,
+                                                    int ntiles,
+                                                    const WarpPatch* __restrict__ patches,
+                                                    int npatch, const uint32_t* __restrict__ wloc,
+                                                    const float2* __restrict__ wfxy,
+                                                    const float* __restrict__ pano, int pw,
+                                                    int ph, long long pstride,
+                                                    const Resp* __restrict__ resp,
+                                                    float* __restrict__ tiles,
+                                                    long long tstride, int batch)
+{
+    __shared__ float box[2][kCap];
+    const int pid = (int)(blockIdx.x % (unsigned)npatch);
+    const int chunk = (int)(blockIdx.x / (unsigned)npatch);
+    const WarpPatch P = patches[pid];
+    const TileGeom& g = geom[P.tile];
+    const int t = threadIdx.x;
+    const int bbeg = chunk * kNB;
+    const int nb = min(kNB, batch - bbeg);
+
+    uint32_t li[kPx], pix[kPx];
+    float fx[kPx], fy[kPx];
+    bool ok[kPx];
+#pragma unroll
+    for (int k = 0; k < kPx; k++) {
+        int i;
+        ok[k] = patch_pixel(P, g, t, k, i);
+        pix[k] = (uint32_t)i;
+        li[k] = 0; fx[k] = 0; fy[k] = 0;
+        if (ok[k]) {
+            li[k] = wloc[g.pix_off + i];
+            const float2 f = wfxy[g.pix_off + i];
+            fx[k] = f.x; fy[k] = f.y;
+        }
+    }
+
+    if (P.wide) {  // footprint too large for LDS (near a pole): direct corner gathers
+        for (int q = 0; q < nb; q++) {
+            const int b = bbeg + q;
+            const float* pp = pano + b * pstride;
+            const RespK r = resp_key(resp, b, ntiles, P.tile);
+            float* out = tiles + b * tstride + g.off;
+#pragma unroll
+            for (int k = 0; k < kPx; k++) {
+                if (!ok[k]) continue;
+                const uint32_t o00 = li[k] & 0x3FFFFFFFu, dx = li[k] >> 31;
+                const uint32_t o10 = o00 + (((li[k] >> 30) & 1u) ? (uint32_t)pw : 0u);
+                const float v = warp_value(pp[o00], pp[o00 + dx], pp[o10], pp[o10 + dx], fx[k],
+                                           fy[k], r, pix[k]);
+                out[(long long)pix[k] * g.c] = v;
+            }
+        }
+        return;
+    }
+
+    __shared__ RespK rk[kNB];  // published by the first barrier inside warp_staged
+    if (t < nb) rk[t] = resp_key(resp, bbeg + t, ntiles, P.tile);
+    const int ns = (P.bw * P.bh + kWB - 1) / kWB;  // uniform: staging loads per thread
+    WarpLanes W{li, fx, fy, pix, ok};
+    if (ns <= 4) warp_staged<4>(box, rk, P, g, t, W, pano, pw, ph, pstride, tiles, tstride, bbeg, nb);
+    else if (ns <= 8) warp_staged<8>(box, rk, P, g, t, W, pano, pw, ph, pstride, tiles, tstride,
+                                     bbeg, nb);
+    else warp_staged<kSlots>(box, rk, P, g, t, W, pano, pw, ph, pstride, tiles, tstride, bbeg, nb);
+}
+
+// ---------------------------------------------------------------------------------------------
+void launch_warp_prepare(hipStream_t s, const TileGeom* geom, int ntiles, long long npix_max,
+                         WarpPatch* patches, int npatch, int pw, int ph, uint32_t* wloc,
+                         float* wfxy)
+{
+    dim3 g1((unsigned)((npix_max + kWB - 1) / kWB), ntiles);
+    hipLaunchKernelGGL(k_warp_coords, g1, dim3(kWB), 0, s, geom, pw, ph, wloc, (float2*)wfxy);
+    hipLaunchKernelGGL(k_patch_box, dim3(npatch), dim3(kWB), 0, s, geom, patches, pw,
+                       (const uint32_t*)wloc);
+    hipLaunchKernelGGL(k_warp_local, dim3(npatch), dim3(kWB), 0, s, geom,
+                       (const WarpPatch*)patches, pw, ph, wloc);
+}
+
+int warp_patch_edge() { return kPatch; }
+
+void launch_warp_depth(hipStream_t s, const TileGeom* geom, int ntiles, const WarpPatch* patches,
+                       int npatch, const uint32_t* wloc, const float* wfxy, const float* pano,
+                       int pw, int ph, long long pstride, const Resp* resp, float* tiles,
+                       long long tstride, int batch)
+{
+    const long long n = (long long)npatch * ((batch + kNB - 1) / kNB);
+    hipLaunchKernelGGL(k_warp_depth, dim3((unsigned)n), dim3(kWB), 0, s, geom, ntiles, patches,
+                       npatch, wloc, (const float2*)wfxy, pano, pw, ph, pstride, resp, tiles,
+                       tstride, batch);
+}
+
+}  // namespace pf
