@@ -1,10 +1,10 @@
 #!/bin/bash
-# Jacobi engine tuning sweep on the GPU box: one bench process per setting "T:waves:minrows".
+# Jacobi engine tuning sweep on the GPU box: one bench process per setting "Tmax:step_overhead:lone_cycles".
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
-for cfg in ${SWEEP:-10:8192:0 5:8192:0}; do
-  IFS=: read -r T W R <<< "$cfg"
-  PF_JT=$T PF_JWAVES=$W PF_JROWS=$R timeout -k 10 300 python bench.py --steps 5 --warmup 2 \
+for cfg in ${SWEEP:-10:3}; do
+  IFS=: read -r T O C1 <<< "$cfg"
+  PF_JT=$T PF_JOVH=${O:-3} PF_JC1=${C1:-6} timeout -k 10 300 python bench.py --steps 5 --warmup 2 \
     --no-cpu-baseline > gpurun_out/sweep_$cfg.log 2>&1; rc=$?
   python - "$cfg" gpurun_out/sweep_$cfg.log <<'PY'
 import json, sys

@@ -100,6 +100,10 @@ struct StageTimer {
     {
         if (idx >= 0) (void)hipEventRecord(c->spans[idx].b, c->stream);
     }
+    void set_launches(long long n)
+    {
+        if (idx >= 0) c->spans[idx].launches = n;
+    }
 };
 }  // namespace
 
@@ -622,9 +626,12 @@ static int check_emap(pf_ctx* c, const float* emap, int ew, int eh, int ec)
 }
 
 // Jacobi pass geometry: lanes own C columns, strips carry a Tp-column halo (Tp >= T, rounded to
-// C so vector rows stay aligned), row chunks sized to whole rounds of resident waves.
+// C so vector rows stay aligned); the sweep depth and row chunking of every pass come from the
+// cost model of plan_level().  Env overrides for tuning runs: PF_JT (largest T), PF_JOVH (per-step
+// overhead in update units), PF_JC=4 (4 columns per lane, builds with PF_JACOBI_C4 only).
 struct JacobiTuning {
-    int C = 2, Tmax = 5, waves_target = 0, min_rows = 0, rounds = 1;
+    int C = 2, Tmax = 10;
+    double step_overhead = 3.0, lone_cycles = 4.0;  // swept on MI355X (tools/jsweep.sh)
 };
 
 static JacobiTuning jacobi_tuning()
@@ -634,19 +641,79 @@ static JacobiTuning jacobi_tuning()
     if (const char* e = getenv("PF_JC")) t.C = atoi(e) == 4 ? 4 : 2;
 #endif
     if (const char* e = getenv("PF_JT")) t.Tmax = atoi(e);
-    if (const char* e = getenv("PF_JWAVES")) t.waves_target = atoi(e);
-    if (const char* e = getenv("PF_JROWS")) t.min_rows = atoi(e);
-    if (const char* e = getenv("PF_JROUNDS")) t.rounds = atoi(e) > 0 ? atoi(e) : 1;
-    if (!jstream_supported_T(t.Tmax)) t.Tmax = 5;
+    if (const char* e = getenv("PF_JOVH")) t.step_overhead = atof(e);
+    if (const char* e = getenv("PF_JC1")) t.lone_cycles = atof(e);
+    if (t.Tmax < 1) t.Tmax = 1;
     return t;
 }
 
-static int pick_T(int remaining, int Tmax)
+// One pass: depth T, nchunks row chunks.  Its nstrips*batch*nchunks waves each run
+// rows_per_chunk + 3T + ~4 steps of T*C updates (lagged levels, halo, 6-step alignment), and
+// they run in ceil(waves / resident) rounds, so the pass costs ~ rounds * steps * (T + o) with o
+// the per-step overhead (loads, LDS ring, store) in update units.  Whole rounds matter: at the
+// small levels a "one wave per slot" grid left the last round 20-80% empty.
+struct PassPlan {
+    int T = 1, nchunks = 1;
+    double cost = 0;
+};
+
+static PassPlan best_chunks(int T, int C, int band_rows, int w, int batch, int per_simd,
+                            int nsimd, double ovh, double c1)
 {
+    PassPlan best;
+    best.T = T;
+    best.cost = 1e300;
+    const int Tp = (T + C - 1) / C * C;
+    const long long per = (long long)((w + 64 * C - 2 * Tp - 1) / (64 * C - 2 * Tp)) * batch;
+    const long long slots = (long long)per_simd * nsimd;
+    for (int n = 1; n <= band_rows; n++) {
+        const int rows = (band_rows + n - 1) / n;
+        if (n > 1 && (band_rows + rows - 1) / rows < n) continue;  // same as a smaller n
+        // rounds of resident waves; in each, a SIMD holding W waves issues one VALU
+        // instruction per 2 cycles shared among them, and a lone wave one per ~c1 cycles
+        const long long waves = per * n;
+        double cyc = 0;
+        for (long long left = waves; left > 0; left -= slots) {
+            const long long in_round = left < slots ? left : slots;
+            const double W = (double)((in_round + nsimd - 1) / nsimd);
+            cyc += (2.0 * W > c1 ? 2.0 * W : c1);
+        }
+        const double cost = cyc * (rows + 3.0 * T + 4.0) * (T + ovh);
+        if (cost < best.cost) {
+            best.cost = cost;
+            best.nchunks = n;
+        }
+    }
+    return best;
+}
+
+// Sweep depths for a level: a shortest-path split of `iters` into passes from the supported
+// menu (<= tcap), each with its best chunking.
+static std::vector<PassPlan> plan_level(pf_ctx* c, const LevelDims& L, int C, int tcap, int batch)
+{
+    static const JacobiTuning tune = jacobi_tuning();
     static const int menu[] = {10, 8, 5, 4, 2, 1};
+    const int band_rows = L.h1 - L.h0 + 1;
+    PassPlan opt[11];
     for (int T : menu)
-        if (T <= Tmax && T <= remaining) return T;
-    return 1;
+        if (T <= tcap && jstream_supported_T(T))
+            opt[T] = best_chunks(T, C, band_rows, L.w, batch, jstream_waves_per_cu(T) / 4,
+                                 4 * c->num_cu, tune.step_overhead, tune.lone_cycles);
+    std::vector<double> dp(L.iters + 1, 1e300);
+    std::vector<int> choice(L.iters + 1, 1);
+    dp[0] = 0;
+    for (int r = 1; r <= L.iters; r++)
+        for (int T : menu) {
+            if (T > r || T > tcap || !jstream_supported_T(T)) continue;
+            const double v = dp[r - T] + opt[T].cost;
+            if (v < dp[r]) {
+                dp[r] = v;
+                choice[r] = T;
+            }
+        }
+    std::vector<PassPlan> plan;
+    for (int r = L.iters; r > 0; r -= choice[r]) plan.push_back(opt[choice[r]]);
+    return plan;
 }
 
 // Runs L.iters sweeps.  The first pass reads `first` (SRC_SEED: emap, SRC_UPSAMPLE: prev level,
@@ -673,7 +740,7 @@ static float* run_jacobi(pf_ctx* c, const LevelDims& L, int first, const float* 
                          int eh, int ec, long long estride, const GridCol* cols,
                          const GridRow* rows, const float* prev, long long pstride,
                          const float* lnorm, float* a, float* b, uint16_t* out,
-                         long long ostride, int batch)
+                         long long ostride, int batch, int* npasses)
 {
     static const JacobiTuning tune = jacobi_tuning();
     const long long st = (long long)L.w * L.h;
@@ -689,35 +756,32 @@ static float* run_jacobi(pf_ctx* c, const LevelDims& L, int first, const float* 
     const int band_rows = L.h1 - L.h0 + 1;
     float* src = (first == 0) ? a : nullptr;
     float* dst = (first == 0) ? b : a;
-    int remaining = L.iters, pass = 0;
-    while (remaining > 0) {
-        int T = pick_T(remaining, jacobi_tcap(L));
+    const std::vector<PassPlan> plan = plan_level(c, L, C, jacobi_tcap(L), batch);
+    static const bool show = getenv("PF_JPLAN") != nullptr;
+    if (show) {
+        fprintf(stderr, "jacobi plan %dx%d band %d iters %d batch %d:", L.w, L.h, band_rows,
+                L.iters, batch);
+        for (const PassPlan& pp : plan) fprintf(stderr, " T%d/n%d", pp.T, pp.nchunks);
+        fprintf(stderr, "\n");
+    }
+    int pass = 0;
+    for (const PassPlan& pp : plan) {
+        const int T = pp.T;
         P.Tp = (T + C - 1) / C * C;  // keeps colbase (and each lane's C-vector) aligned
         P.V = 64 * C - 2 * P.Tp;
         P.nstrips = (L.w + P.V - 1) / P.V;
-        long long per = (long long)P.nstrips * batch;
-        // size the grid to whole rounds of resident waves (a partial last round idles SIMDs)
-        long long target = tune.waves_target > 0
-                               ? tune.waves_target
-                               : (long long)jstream_waves_per_cu(T) * c->num_cu * tune.rounds;
-        int nchunks = (int)((target + per / 2) / per);
-        int min_rows = tune.min_rows > 0 ? tune.min_rows : 4 * T;
-        int max_chunks = band_rows / min_rows;
-        if (max_chunks < 1) max_chunks = 1;
-        if (nchunks > max_chunks) nchunks = max_chunks;
-        if (nchunks < 1) nchunks = 1;
-        P.rows_per_chunk = (band_rows + nchunks - 1) / nchunks;
+        P.rows_per_chunk = (band_rows + pp.nchunks - 1) / pp.nchunks;
         P.nchunks = (band_rows + P.rows_per_chunk - 1) / P.rows_per_chunk;
         P.src_mode = pass == 0 ? first : 0;
         P.src = src;
         P.dst = dst;
-        remaining -= T;
-        P.out_mode = (remaining == 0 && out) ? 1 : 0;
+        P.out_mode = (pass + 1 == (int)plan.size() && out) ? 1 : 0;
         launch_jstream(c->stream, P, C, T, batch);
         src = dst;
         dst = (dst == a) ? b : a;
         pass++;
     }
+    if (npasses) *npasses = pass;
     return src;
 }
 
@@ -798,9 +862,11 @@ static int fuse_impl(pf_ctx* c, const float* emap, int ew, int eh, int ec, const
             {
                 // 12 B per pixel-update (read b, read L, write b'), SURVEY.md 8d
                 StageTimer t(c, PF_STAGE_JACOBI, B * 12.0 * band * L.iters, L.iters);
+                int passes = 0;
                 res = run_jacobi(c, L, l == 0 ? 2 : 1, emap, ew, eh, ec, estride, cols, rows,
                                  prev, pst, (const float*)c->lnorm.p, a, b, last ? out : nullptr,
-                                 plane, batch);
+                                 plane, batch, &passes);
+                t.set_launches(passes);  // k_jlag launches (rocprof's count for that kernel)
             }
         }
         prev = res;
@@ -979,7 +1045,7 @@ int pf_fuse_finish_level(pf_ctx* c, const float* lsum, const float* cnt, int out
     float* res = nullptr;
     if (jacobi_tcap(L) >= 1)
         res = run_jacobi(c, L, 0, nullptr, 0, 0, 0, 0, nullptr, nullptr, nullptr, 0,
-                         (const float*)c->lnorm.p, buf, other, nullptr, 0, 1);
+                         (const float*)c->lnorm.p, buf, other, nullptr, 0, 1, nullptr);
     else
         launch_jacobi(c->stream, buf, other, (const float*)c->lnorm.p, st, L, L.iters, 1, &res);
     if (res != buf)
