@@ -71,6 +71,18 @@ def cpu_baseline(seconds, out_w=2048, ew=512):
                       f" + 3-level fusion, {t_work:.1f} s of work, OpenMP {threads} threads"}
 
 
+def pmc_traffic(family):
+    """HBM bytes per launch of a kernel family from the committed rocprofv3 PMC passes
+    (tools/pmc_round.sh -> tools/pmc_traffic.py -> profiles/pmc_traffic.json), or None."""
+    path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    try:
+        with open(path) as f:
+            rec = json.load(f).get(family)
+        return float(rec["traffic_B"]) if rec else None
+    except (OSError, ValueError, KeyError):
+        return None
+
+
 def main():
     args = parse()
     import numpy as np
@@ -162,13 +174,17 @@ def main():
                        "global_batch": B * world, "out": "2048x1024", "tiles": "20x512x512",
                        "parallelism": f"dp{world} (panorama sharding, no collective)"},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS,
-                         "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": None,
+                         "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
+                         "traffic": pmc_traffic("pf::k_jlag"),
                          "kernel": "k_jlag (all Jacobi passes of the 3 levels, aggregated)",
                          "avg_launch_us": (jms / jlaunch * 1e3) if jlaunch else None,
-                         "bytes_per_launch": (jbytes / jlaunch) if jlaunch else None},
+                         "bytes_per_launch": (jbytes / jlaunch) if jlaunch else None,
+                         "traffic_source": "profiles/pmc_traffic.json (FETCH_SIZE x2 + WRITE_SIZE, "
+                                           "B per launch, averaged over every k_jlag dispatch)"},
             # north_star's named target: >= 60% of the HBM roofline on the warp kernel
             "roofline_warp": {"bound": "hbm", "achieved": wach, "peak": HBM_PEAK_GBS,
-                              "unit": "GB/s", "frac": wach / HBM_PEAK_GBS, "traffic": None,
+                              "unit": "GB/s", "frac": wach / HBM_PEAK_GBS,
+                              "traffic": pmc_traffic("pf::k_warp_depth"),
                               "kernel": "k_warp_depth",
                               "avg_launch_us": (wms / wlaunch * 1e3) if wlaunch else None,
                               "bytes_per_launch": (wbytes / wlaunch) if wlaunch else None},

@@ -285,3 +285,22 @@ def test_fuse_bit_exact_wide_zenith(fuser, zr_deg):
     fuser.fuse(_dev(emap)[None], _dev(data)[None].contiguous(), out, zr)
     ref, _ = O.solve_depth_all(emap, tiles, data, 1024, zr)
     assert int((out.cpu().numpy().view(np.uint16)[0] != ref).sum()) == 0
+
+
+def test_fuse_bit_exact_coverage_holes(fuser):
+    """A layout with uncovered band pixels (two tiles dropped from C2) has no standard-coverage
+    certificate, so every level takes the general (scalar, marker-masked) Jacobi form; the full
+    C2 layout takes the packed form (test_fuse_bit_exact).  Both must match the oracle."""
+    full = PL.config_layout("C2")
+    keep = [i for i in range(full.ntiles) if i not in (6, 13)]
+    lay = PL.Layout("C2-holes", full.fovs[keep], full.ranges[keep], full.tile_w[keep],
+                    full.tile_h[keep])
+    fuser.set_tiles(lay)
+    tiles, total = O.make_tiles(lay)
+    rs = np.random.RandomState(5)
+    data = rs.rand(total).astype(np.float32)
+    emap = rs.rand(256, 512).astype(np.float32)
+    out = torch.zeros((1, 1024, 2048), dtype=torch.int16, device=DEV)
+    fuser.fuse(_dev(emap)[None], _dev(data)[None].contiguous(), out, ZR)
+    ref, _ = O.solve_depth_all(emap, tiles, data, 2048, ZR)
+    assert int((out.cpu().numpy().view(np.uint16)[0] != ref).sum()) == 0

@@ -31,8 +31,12 @@ struct LevelCache {
     uint32_t zr0 = 0, zr1 = 0;
     int nlevels = 0;
     LevelDims dims[4];
-    DevBuf box[4], cols[4], rows[4], tapbox[4], tapmap[4];
+    DevBuf box[4], cols[4], rows[4], tapbox[4], tapmap[4], hcol[4];
     std::vector<TileBox> box_h[4];
+    // separable-coverage certificate of each level: a band pixel is covered iff it lies in rows
+    // h0+1..h1-1 and in a column of a fixed set that excludes column 0.  Enables the packed
+    // Jacobi form (pf_jacobi.hip), with hcol[l][X] = 0.5 on covered columns, 0 elsewhere.
+    bool full[4] = {false, false, false, false};
 };
 
 }  // namespace
@@ -568,11 +572,24 @@ static int prepare_levels(pf_ctx* c, int out_w, int out_h, float zr0, float zr1)
                                     X, Y, PF_MAX_COVER);
         }
         lc.box_h[l] = boxes;
+        std::vector<float> hcol(L.w, 0.0f);
+        bool full = L.h0 + 1 < L.h1;
+        for (int X = 0; X < L.w && full; X++)
+            hcol[X] = cover[(size_t)(L.h0 + 1) * L.w + X] > 0 ? 0.5f : 0.0f;
+        full = full && hcol[0] == 0.0f;
+        for (int Y = L.h0; Y <= L.h1 && full; Y++)
+            for (int X = 0; X < L.w; X++)
+                if ((cover[(size_t)Y * L.w + X] > 0) != (hcol[X] != 0.0f && Y > L.h0 && Y < L.h1)) {
+                    full = false;
+                    break;
+                }
+        lc.full[l] = full;
         std::vector<GridCol> cols;
         std::vector<GridRow> rows;
         grid_tables(L, cols, rows);
         int rc;
         if ((rc = upload(c, lc.box[l], boxes))) return rc;
+        if ((rc = upload(c, lc.hcol[l], hcol))) return rc;
         if ((rc = upload(c, lc.cols[l], cols))) return rc;
         if ((rc = upload(c, lc.rows[l], rows))) return rc;
         // tap-index maps: every tile's box plus a one-pixel ring (pf_targets.hip)
@@ -689,7 +706,8 @@ static PassPlan best_chunks(int T, int C, int band_rows, int w, int batch, int p
 
 // Sweep depths for a level: a shortest-path split of `iters` into passes from the supported
 // menu (<= tcap), each with its best chunking.
-static std::vector<PassPlan> plan_level(pf_ctx* c, const LevelDims& L, int C, int tcap, int batch)
+static std::vector<PassPlan> plan_level(pf_ctx* c, const LevelDims& L, int C, int tcap, int batch,
+                                        bool fast)
 {
     static const JacobiTuning tune = jacobi_tuning();
     static const int menu[] = {10, 8, 5, 4, 2, 1};
@@ -697,7 +715,7 @@ static std::vector<PassPlan> plan_level(pf_ctx* c, const LevelDims& L, int C, in
     PassPlan opt[11];
     for (int T : menu)
         if (T <= tcap && jstream_supported_T(T))
-            opt[T] = best_chunks(T, C, band_rows, L.w, batch, jstream_waves_per_cu(T) / 4,
+            opt[T] = best_chunks(T, C, band_rows, L.w, batch, jstream_waves_per_cu(T, fast) / 4,
                                  4 * c->num_cu, tune.step_overhead, tune.lone_cycles);
     std::vector<double> dp(L.iters + 1, 1e300);
     std::vector<int> choice(L.iters + 1, 1);
@@ -740,11 +758,14 @@ static float* run_jacobi(pf_ctx* c, const LevelDims& L, int first, const float* 
                          int eh, int ec, long long estride, const GridCol* cols,
                          const GridRow* rows, const float* prev, long long pstride,
                          const float* lnorm, float* a, float* b, uint16_t* out,
-                         long long ostride, int batch, int* npasses)
+                         long long ostride, int batch, int* npasses, const float* hcol)
 {
     static const JacobiTuning tune = jacobi_tuning();
+    static const bool slow = getenv("PF_JSLOW") != nullptr;  // force the general (scalar) form
     const long long st = (long long)L.w * L.h;
     const int C = (L.w % 4 == 0 && L.w >= 512) ? tune.C : 2;
+    // packed form: C == 2 and the level's separable-coverage certificate (pf_jacobi.hip)
+    const bool fast = hcol && C == 2 && !slow;
     JacobiPass P{};
     P.prev = prev; P.pstride = pstride;
     P.emap = emap; P.estride = estride; P.ew = ew; P.eh = eh; P.ec = ec;
@@ -753,14 +774,15 @@ static float* run_jacobi(pf_ctx* c, const LevelDims& L, int first, const float* 
     P.sstride = st; P.dstride = st;
     P.out = out; P.ostride = ostride;
     P.w = L.w; P.h = L.h; P.h0 = L.h0; P.h1 = L.h1;
+    P.hcol = hcol;
     const int band_rows = L.h1 - L.h0 + 1;
     float* src = (first == 0) ? a : nullptr;
     float* dst = (first == 0) ? b : a;
-    const std::vector<PassPlan> plan = plan_level(c, L, C, jacobi_tcap(L), batch);
+    const std::vector<PassPlan> plan = plan_level(c, L, C, jacobi_tcap(L), batch, fast);
     static const bool show = getenv("PF_JPLAN") != nullptr;
     if (show) {
-        fprintf(stderr, "jacobi plan %dx%d band %d iters %d batch %d:", L.w, L.h, band_rows,
-                L.iters, batch);
+        fprintf(stderr, "jacobi plan %dx%d band %d iters %d batch %d %s:", L.w, L.h, band_rows,
+                L.iters, batch, fast ? "packed" : "general");
         for (const PassPlan& pp : plan) fprintf(stderr, " T%d/n%d", pp.T, pp.nchunks);
         fprintf(stderr, "\n");
     }
@@ -776,7 +798,7 @@ static float* run_jacobi(pf_ctx* c, const LevelDims& L, int first, const float* 
         P.src = src;
         P.dst = dst;
         P.out_mode = (pass + 1 == (int)plan.size() && out) ? 1 : 0;
-        launch_jstream(c->stream, P, C, T, batch);
+        launch_jstream(c->stream, P, C, T, batch, fast);
         src = dst;
         dst = (dst == a) ? b : a;
         pass++;
@@ -865,7 +887,8 @@ static int fuse_impl(pf_ctx* c, const float* emap, int ew, int eh, int ec, const
                 int passes = 0;
                 res = run_jacobi(c, L, l == 0 ? 2 : 1, emap, ew, eh, ec, estride, cols, rows,
                                  prev, pst, (const float*)c->lnorm.p, a, b, last ? out : nullptr,
-                                 plane, batch, &passes);
+                                 plane, batch, &passes,
+                                 lc.full[l] ? (const float*)lc.hcol[l].p : nullptr);
                 t.set_launches(passes);  // k_jlag launches (rocprof's count for that kernel)
             }
         }
@@ -1045,7 +1068,8 @@ int pf_fuse_finish_level(pf_ctx* c, const float* lsum, const float* cnt, int out
     float* res = nullptr;
     if (jacobi_tcap(L) >= 1)
         res = run_jacobi(c, L, 0, nullptr, 0, 0, 0, 0, nullptr, nullptr, nullptr, 0,
-                         (const float*)c->lnorm.p, buf, other, nullptr, 0, 1, nullptr);
+                         (const float*)c->lnorm.p, buf, other, nullptr, 0, 1, nullptr,
+                         lc.full[level] ? (const float*)lc.hcol[level].p : nullptr);
     else
         launch_jacobi(c->stream, buf, other, (const float*)c->lnorm.p, st, L, L.iters, 1, &res);
     if (res != buf)

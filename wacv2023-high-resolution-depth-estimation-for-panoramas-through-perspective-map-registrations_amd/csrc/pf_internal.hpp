@@ -119,6 +119,16 @@ __host__ __device__ inline float cubic_map(float X, float a, float b, float c, f
 }
 
 // EquirectangularMap::ValueAtCoord (Depth.cpp:551-556): index math promoted to double by MYPI.
+// XCD-aware block order.  The dispatcher deals workgroup b to XCD (b mod 8) (MI355X_MICROARCH.md,
+// workgroup dispatch); this maps it to a logical block so that every XCD walks one contiguous
+// range of logical blocks, and neighbouring blocks -- which re-read each other's edge lines --
+// share that XCD's L2.  A bijection on [0, n).
+__device__ __forceinline__ unsigned xcd_remap(unsigned b, unsigned n)
+{
+    const unsigned x = b & 7u, s = b >> 3, q = n >> 3, r = n & 7u;
+    return x * q + (x < r ? x : r) + s;
+}
+
 __host__ __device__ inline long long emap_index(float az, float zen, int w, int h, int c)
 {
     int x = (int)((double)az / (PF_MYPI * 2) * (double)(float)(w - 1));
@@ -139,6 +149,7 @@ struct JacobiPass {
     int out_mode;
     int w, h, h0, h1;
     int V, Tp, nstrips, nchunks, rows_per_chunk;
+    const float* hcol;  // packed form: per column 0.5 (covered) or 0 (un-windowed), w entries
 };
 
 // ------------------------------------------------------------------------------------------
@@ -150,8 +161,8 @@ void launch_targets_map(hipStream_t s, const TileGeom* geom, const TileBox* box,
                         long long tstride, const float* coeffs, LevelDims L, float* lnorm,
                         long long lstride, int batch);
 bool jstream_supported_T(int T);
-int jstream_waves_per_cu(int T);
-void launch_jstream(hipStream_t s, const JacobiPass& P, int C, int T, int batch);
+int jstream_waves_per_cu(int T, bool fast);
+void launch_jstream(hipStream_t s, const JacobiPass& P, int C, int T, int batch, bool fast);
 void launch_border(hipStream_t s, const float* prev, long long pstride, LevelDims L, float* a,
                    float* b, long long stride, uint16_t* out, long long ostride, int batch);
 void launch_seed0(hipStream_t s, const float* emap, int ew, int eh, int ec, long long estride,

@@ -4,10 +4,10 @@
 // (Depth.cpp:1680-1717).  Here one launch ("pass") advances the band by T sweeps:
 //
 //  * A wave owns a vertical strip of 64*C virtual columns (C per lane) and streams down a chunk
-//    of rows.  At step k it loads row k and, for every sweep level t = 1..T, produces row k-t of
-//    level t from rows k-t-1..k-t+1 of level t-1, which it keeps in registers (two rows of
-//    history per level).  Horizontal neighbours cross lanes with DPP wave_shr/wave_shl moves.
-//    No LDS, no barriers: every step issues T*C independent updates.
+//    of rows.  At step k it loads row k and, for every sweep level t = 1..T, produces row k-2t of
+//    level t from rows k-2t-1..k-2t+1 of level t-1, which it keeps in registers (a 3-row ring per
+//    level).  Horizontal neighbours cross lanes with DPP wave_shr/wave_shl moves.  L rows come
+//    through a per-wave LDS ring; no barriers.
 //  * Columns are "virtual": virtual column x of row Y is linear pixel Y*w + x, so x < 0 or
 //    x >= w wraps into the neighbouring row -- exactly the reference's buffer[yy*width + xx]
 //    addressing (the seam quirk of SURVEY.md Appendix A item 5 comes out for free).
@@ -33,17 +33,11 @@
 #ifndef PF_JLAG_WAVES
 #define PF_JLAG_WAVES 1  // __launch_bounds__ min waves per SIMD of the lagged kernel
 #endif
-#ifndef PF_JLAG_STAGEWISE
-#define PF_JLAG_STAGEWISE 1
-#endif
-#ifndef PF_JLAG_LDSL
-#define PF_JLAG_LDSL 1  // L rows through a per-wave LDS ring (1) or per-level registers (0)
+#ifndef PF_JPK_GROUP
+#define PF_JPK_GROUP 3  // levels per stage-wise group of the packed form (VGPR bound: 3 waves/SIMD)
 #endif
 #ifndef PF_JLAG_PF
 #define PF_JLAG_PF 2  // steps of lead for the input and L row loads (1 or 2)
-#endif
-#ifndef PF_JLAG_TOUCH
-#define PF_JLAG_TOUCH 0  // steps of lead for L2 touch loads (0 = off; measured slower)
 #endif
 
 namespace pf {
@@ -59,212 +53,74 @@ __device__ __forceinline__ float dpp_from_right(float v)
     return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0x130, 0xF, 0xF, true));
 }
 
+typedef float f2 __attribute__((ext_vector_type(2)));
+
 template <int C>
 struct Row {
     float v[C];
 };
-
-// One damped-Jacobi update of a C-column row segment.
-template <int C>
-__device__ __forceinline__ Row<C> sweep_row(const Row<C>& n, const Row<C>& c, const Row<C>& s,
-                                            const Row<C>& L)
-{
-    const float reg = (float)1e-4;
-    const float reg_ = 1 - reg;
-    float west0 = dpp_from_left(c.v[C - 1]);
-    float eastC = dpp_from_right(c.v[0]);
-    Row<C> o;
-#pragma unroll
-    for (int j = 0; j < C; j++) {
-        float W = j == 0 ? west0 : c.v[j - 1];
-        float E = j == C - 1 ? eastC : c.v[j + 1];
-        float b = c.v[j];
-        // Lcur = (((W*q + N*q) + b) + S*q) + E*q with q = -1/4.  Every product by q (and by 0.5
-        // below) is exact -- a power-of-two scaling -- so fl(W*q + N*q) = q*fl(W+N) and
-        // fl(a + x*q) = fma(x, q, a): the fused form rounds exactly where the reference rounds.
-        // (Exact unless an operand is below 2^-124, which depths in [0,1] never reach here.)
-        float cur = __builtin_fmaf(W + n.v[j], -0.25f, b);
-        cur = __builtin_fmaf(s.v[j], -0.25f, cur);
-        cur = __builtin_fmaf(E, -0.25f, cur);
-        // un-windowed pixel (L = marker): Lcur = L = 0, so the step is exactly +0.  Masked
-        // with an AND so the compiler keeps this straight-line (no exec-mask branch).
-        float d = L.v[j] - cur;
-        uint32_t m = __float_as_uint(L.v[j]) == PF_NAN_MARKER ? 0u : 0xFFFFFFFFu;
-        d = __uint_as_float(__float_as_uint(d) & m);
-        float t = __builtin_fmaf(d, 0.5f, b);  // b + (L - Lcur)*0.5, product exact
-        float v = t * reg_ + b * reg;
-        // clamp01: b is never -0 or NaN here, so med3 equals the reference's compare chain
-        v = __builtin_amdgcn_fmed3f(v, 0.0f, 1.0f);
-        o.v[j] = v;
-    }
-    return o;
-}
+// A lane's column pair as one vector value: element access .v[j] as for any C, and the packed
+// form operates on .v directly (an array member here defeats scalar replacement of the level
+// rings and sends them to scratch).
+template <>
+struct Row<2> {
+    f2 v;
+};
 
 }  // namespace
 
 // Source of a pass's input rows.
 enum { SRC_BUF = 0, SRC_UPSAMPLE = 1, SRC_SEED = 2 };
 
-template <int C, int T, int SRC, bool OUT16>
-__global__ void __launch_bounds__(256) k_jstream(JacobiPass P)
-{
-    const int lane = threadIdx.x & 63;
-    const long long job = (long long)blockIdx.x * 4 + (threadIdx.x >> 6);
-    if (job >= (long long)P.nstrips * P.nchunks) return;  // wave-uniform
-    const int b = blockIdx.y;
-    const int strip = (int)(job % P.nstrips), chunk = (int)(job / P.nstrips);
-    const int w = P.w;
-    const int xs0 = strip * P.V - P.Tp + lane * C;  // this lane's first virtual column
-    const int vlo = strip * P.V, vhi = min(vlo + P.V, w);
-    const int r0 = P.h0 + chunk * P.rows_per_chunk;
-    const int r1 = min(r0 + P.rows_per_chunk, P.h1 + 1);
-    const long long npx = (long long)w * P.h;
-
-    const float* src = P.src + b * P.sstride;
-    const float* prev = P.prev + b * P.pstride;
-    const float* emap = P.emap + b * P.estride;
-    const float* lnorm = P.lnorm + b * P.lstride;
-    float* dst = P.dst + b * P.dstride;
-    uint16_t* out = P.out + b * P.ostride;
-
-    auto load_b = [&](int k) {
-        Row<C> r;
-        if constexpr (SRC == SRC_BUF) {
-            long long base = (long long)k * w + xs0;
-            base = base < 0 ? 0 : (base > npx - C ? npx - C : base);
-            if constexpr (C == 4) {
-                float4 q = *reinterpret_cast<const float4*>(src + base);
-                r.v[0] = q.x; r.v[1] = q.y; r.v[2] = q.z; r.v[3] = q.w;
-            } else if constexpr (C == 2) {
-                float2 q = *reinterpret_cast<const float2*>(src + base);
-                r.v[0] = q.x; r.v[1] = q.y;
-            } else {
-#pragma unroll
-                for (int j = 0; j < C; j++) r.v[j] = src[base + j];
-            }
-        } else {
-#pragma unroll
-            for (int j = 0; j < C; j++) {
-                long long i = (long long)k * w + xs0 + j;
-                float v = 0.0f;
-                if (i >= 0 && i < npx) {
-                    int Y = (int)(i / w);
-                    int xr = (int)(i - (long long)Y * w);
-                    if constexpr (SRC == SRC_UPSAMPLE) {
-                        v = prev[(long long)(Y / 2) * (w / 2) + xr / 2];
-                    } else if (Y >= P.h0 && Y <= P.h1) {  // level-0 seed (Depth.cpp:1442-1465)
-                        v = emap[emap_index(P.cols[xr + 1].az, P.rows[Y + 1].zen, P.ew, P.eh, P.ec)];
-                    }
-                }
-                r.v[j] = v;
-            }
-        }
-        return r;
-    };
-    auto load_L = [&](int k) {
-        Row<C> r;
-        long long base = (long long)k * w + xs0;
-        base = base < 0 ? 0 : (base > npx - C ? npx - C : base);
-        if constexpr (C == 4) {
-            float4 q = *reinterpret_cast<const float4*>(lnorm + base);
-            r.v[0] = q.x; r.v[1] = q.y; r.v[2] = q.z; r.v[3] = q.w;
-        } else if constexpr (C == 2) {
-            float2 q = *reinterpret_cast<const float2*>(lnorm + base);
-            r.v[0] = q.x; r.v[1] = q.y;
-        } else {
-#pragma unroll
-            for (int j = 0; j < C; j++) r.v[j] = lnorm[base + j];
-        }
-        return r;
-    };
-
-    Row<C> hist[T][2];  // level t: rows (k-2-t, k-1-t) at the start of step k
-    Row<C> Lr[T + 1];   // Lr[t] = L of row k-t
-#pragma unroll
-    for (int t = 0; t < T; t++)
-#pragma unroll
-        for (int j = 0; j < C; j++) { hist[t][0].v[j] = 0.0f; hist[t][1].v[j] = 0.0f; }
-#pragma unroll
-    for (int t = 0; t <= T; t++)
-#pragma unroll
-        for (int j = 0; j < C; j++) Lr[t].v[j] = 0.0f;
-
-    const int kbeg = r0 - T, kend = r1 + T;  // input rows streamed: [kbeg, kend)
-    Row<C> nb = load_b(kbeg), nl = load_L(kbeg);
-    for (int k = kbeg; k < kend; k++) {
-        Row<C> cb = nb;
-#pragma unroll
-        for (int t = T; t >= 1; t--) Lr[t] = Lr[t - 1];
-        Lr[0] = nl;
-        if (k + 1 < kend) {  // prefetch the next input row
-            nb = load_b(k + 1);
-            nl = load_L(k + 1);
-        }
-        Row<C> newr = cb;  // level 0 row k
-#pragma unroll
-        for (int t = 1; t <= T; t++) {
-            // level t, row k-t, from level t-1 rows k-t-1, k-t, k-t+1
-            Row<C> o = sweep_row<C>(hist[t - 1][0], hist[t - 1][1], newr, Lr[t]);
-            hist[t - 1][0] = hist[t - 1][1];
-            hist[t - 1][1] = newr;
-            newr = o;
-        }
-        const int j = k - T;  // output row of the final level
-        if (j >= r0) {
-            const long long rowb = (long long)j * w;
-#pragma unroll
-            for (int q = 0; q < C; q++) {
-                int x = xs0 + q;
-                if (x >= vlo && x < vhi) {
-                    if constexpr (OUT16) {
-                        float v = newr.v[q];
-                        if (v < 0) v = 0;
-                        if (v > 1) v = 1;
-                        out[rowb + x] = (uint16_t)(v * 65535.0f);
-                    } else
-                        dst[rowb + x] = newr.v[q];
-                }
-            }
-        }
-    }
+// ---------------------------------------------------------------------------------------------
+// Lagged streaming: sweep level t produces row k-2t at step k (two rows behind level t-1), so
+// every level reads only rows finished in earlier steps and the T*C updates of a step are
+// independent (no intra-step dependency chain).  Level t keeps a 3-row ring; input rows and L rows
+// are loaded PF steps ahead.  The step loop is unrolled by 6 (lcm of the ring period 3 and the
+// load-buffer period PF+1) so every register ring index is a compile-time constant.
+//
+// L rows live in a per-wave LDS ring of R = 2T+1 rows (row r in slot r % R): each L row is loaded
+// from memory once and read T times from LDS.
+//
+// Two arithmetic forms of the same update (bit-identical results):
+//  * FAST (C == 2): the two columns of a lane are one v_pk_* operand pair, so the update costs
+//    ~9 packed ops + 2 DPP moves + 2 pair assemblies per two pixels.  A packed op moves two lanes
+//    of data at about the issue cost of a scalar op on gfx950 (tools/ubench/valu_rate.hip).  The
+//    un-windowed mask is geometric: t = fma(d, H, b) with H = 0.5 on windowed pixels and 0 on
+//    un-windowed ones (0 * finite = 0, b + 0 = b exactly).  H = Hcol(column) * Hrow(row) needs
+//    the host's separable-coverage certificate (prepare_levels in pf_api.hip): a band pixel is
+//    covered iff its row is in h0+1..h1-1 and its column in a fixed set that excludes column 0
+//    (true of the reference's layouts: column 0 and the columns past the 359.9-degree cap are
+//    uncovered).  L rows are sanitised (non-finite -> 0) as they enter the ring so that d stays
+//    finite where H = 0.
+//  * general: scalar ops, mask from the marker in L (cmp + cndmask per pixel), any coverage.
+__device__ __forceinline__ f2 pk_add_clamp01(f2 a, f2 b)
+{  // v_pk_add_f32 with the output clamp: both lanes clamped to [0, 1] (b' = clamp01(...))
+    f2 r;
+    asm("v_pk_add_f32 %0, %1, %2 clamp" : "=v"(r) : "v"(a), "v"(b));
+    return r;
 }
 
-// ---------------------------------------------------------------------------------------------
-// Lagged variant: sweep level t produces row k-2t at step k (two rows behind level t-1 instead
-// of one), so every level reads only rows finished in earlier steps and the T*C updates of a
-// step are independent (no intra-step dependency chain).  Level t keeps a 3-row ring; input
-// rows and the L rows of the next step are loaded one step ahead into double buffers.  The step
-// loop is unrolled by 6 (lcm of the ring period 3 and the double-buffer period 2) so every ring
-// index is a compile-time constant and no register moves are needed.
-template <int C, int T, int SRC, bool OUT16>
+template <int C, int T, int SRC, bool OUT16, bool FAST>
 struct JLag {
-    Row<C> H[T][3];   // H[t][r % 3] = level t row r
-    // Input rows are loaded PF steps before their first use: row r lands in In[r % NB] (issued
-    // at step r + 1 - PF, consumed at step r + 1).  NB divides the unroll factor 6.
+    static_assert(C % 2 == 0, "column pairs: vector stores and the wrap logic assume even C");
+    static_assert(!FAST || C == 2, "the packed form pairs the two columns of a lane");
     static constexpr int PF = PF_JLAG_PF, NB = PF_JLAG_PF + 1;
-    Row<C> In[NB];
-#if PF_JLAG_LDSL
-    // L rows live in a per-wave LDS ring of R = 2T+1 rows (row r in slot r % R): each L row is
-    // loaded from memory once (one step ahead, into Lin) and read T times from LDS, instead of
-    // T global loads per step held in 2*T*C registers.
-    static constexpr int R = 2 * T + 1;
-    Row<C> Lin[NB];   // L row r lands in Lin[r % NB] (issued at step r - PF), stored to LDS at step r
+    // ring of R >= 2T+1 rows, R a multiple of 6: the loop body is unrolled over the R/6 groups
+    // of 6 steps so every ring slot is a compile-time constant (LDS immediate offsets, no SALU)
+    static constexpr int R = (2 * T + 1 + 5) / 6 * 6, NG = R / 6;
+    Row<C> H[T][3];   // H[t][r % 3] = level t row r
+    Row<C> In[NB];    // input row r lands in In[r % NB] (issued at step r + 1 - PF)
+    Row<C> Lin[NB];   // L row r lands in Lin[r % NB] (issued at step r - PF), to LDS at step r
     float* lring;     // this wave's ring: R rows of 64*C floats
     int lane_c;       // lane * C (LDS column offset)
-#else
-    Row<C> Lb[2][T];  // Lb[k & 1][t-1] = L row k-2t, for step k
-#endif
-#if PF_JLAG_TOUCH
-    Row<C> Tch[2][2];      // touch-load landing registers (input row, L row)
-    uint32_t touch_acc;    // keeps the touch loads alive; never meaningful
-#endif
+    float hcol0, hcol1;  // FAST: H of the lane's columns: 0.5 (covered column) or 0
     const JacobiPass* P;
-    int w, xs0, vlo, vhi, r0, r1;
+    int w, xs0, vlo, vhi, r0, r1, h0, h1;
     int colbase;   // virtual column of lane 0 (wave-uniform)
     int lo;        // lane * C
     int rlo, rhi;  // rows loads are clamped to (wave-uniform; the host guarantees every row a
                    // valid output depends on lies inside, so clamping only touches halo rows)
-    long long npx;
     const float *src, *prev, *emap, *lnorm;
     float* dst;
     uint16_t* out;
@@ -279,12 +135,9 @@ struct JLag {
         if constexpr (C == 2) {
             float2 q = *reinterpret_cast<const float2*>(rp + lo);
             r.v[0] = q.x; r.v[1] = q.y;
-        } else if constexpr (C == 4) {
+        } else {
             float4 q = *reinterpret_cast<const float4*>(rp + lo);
             r.v[0] = q.x; r.v[1] = q.y; r.v[2] = q.z; r.v[3] = q.w;
-        } else {
-#pragma unroll
-            for (int j = 0; j < C; j++) r.v[j] = rp[lo + j];
         }
         return r;
     }
@@ -294,22 +147,28 @@ struct JLag {
         if constexpr (SRC == SRC_BUF) {
             return load_row(src, k);
         } else {
+            // Virtual column xs0 + j of row k is pixel (xr, Y) with |xs0 + j - xr| < w (the
+            // halo is narrower than a row, jacobi_tcap), so the wrap is one compare, no division.
+            // xs0 is even and C is even, so the pair (2m, 2m+1) never straddles a row end and
+            // shares one source pixel of the half-resolution level.
             Row<C> r;
 #pragma unroll
-            for (int j = 0; j < C; j++) {
-                long long i = (long long)k * w + xs0 + j;
-                float v = 0.0f;
-                if (i >= 0 && i < npx) {
-                    int Y = (int)(i / w);
-                    int xr = (int)(i - (long long)Y * w);
+            for (int j = 0; j < C; j += 2) {
+                int xr = xs0 + j, Y = k;
+                if (xr < 0) { xr += w; Y -= 1; }
+                else if (xr >= w) { xr -= w; Y += 1; }
+                float v0 = 0.0f, v1 = 0.0f;
+                if (Y >= 0 && Y < P->h) {
                     if constexpr (SRC == SRC_UPSAMPLE) {
-                        v = prev[(long long)(Y / 2) * (w / 2) + xr / 2];
+                        v0 = v1 = prev[(long long)(Y >> 1) * (w >> 1) + (xr >> 1)];
                     } else if (Y >= P->h0 && Y <= P->h1) {  // level-0 seed (Depth.cpp:1442-1465)
-                        v = emap[emap_index(P->cols[xr + 1].az, P->rows[Y + 1].zen, P->ew, P->eh,
-                                            P->ec)];
+                        const float zen = P->rows[Y + 1].zen;
+                        v0 = emap[emap_index(P->cols[xr + 1].az, zen, P->ew, P->eh, P->ec)];
+                        v1 = emap[emap_index(P->cols[xr + 2].az, zen, P->ew, P->eh, P->ec)];
                     }
                 }
-                r.v[j] = v;
+                r.v[j] = v0;
+                r.v[j + 1] = v1;
             }
             return r;
         }
@@ -317,21 +176,27 @@ struct JLag {
 
     static constexpr int slot(int ph, int a) { return ((ph - a) % 3 + 3) % 3; }
 
-#if PF_JLAG_LDSL
-    // LDS ring slot of row (group base + d); kb = group base mod R (wave-uniform, SALU).
-    __device__ __forceinline__ float* lslot(int kb, int d) const
+    // LDS ring slot of row k + d, with k = group base and GB = k mod R (compile-time)
+    template <int GB, int D>
+    __device__ __forceinline__ float* lslot() const
     {
-        const int s = (kb + d + 2 * R) % R;  // d >= -2T > -2R
+        constexpr int s = ((GB + D) % R + R) % R;
         return lring + s * (64 * C) + lane_c;
     }
-    __device__ __forceinline__ void lds_put(float* p, const Row<C>& r) const
+    template <int GB, int PH>
+    __device__ __forceinline__ float* lslot_t(int t) const
+    {  // t is a constant after unrolling; the modulo folds
+        const int s = ((GB + PH - 2 * t) % R + R) % R;
+        return lring + s * (64 * C) + lane_c;
+    }
+    __device__ __forceinline__ void lds_put(float* p, Row<C> r) const
     {
-        if constexpr (C == 2) *reinterpret_cast<float2*>(p) = make_float2(r.v[0], r.v[1]);
-        else if constexpr (C == 4) *reinterpret_cast<float4*>(p) = make_float4(r.v[0], r.v[1], r.v[2], r.v[3]);
-        else {
+        if constexpr (FAST) {
 #pragma unroll
-            for (int j = 0; j < C; j++) p[j] = r.v[j];
+            for (int j = 0; j < C; j++) r.v[j] = __builtin_isfinite(r.v[j]) ? r.v[j] : 0.0f;
         }
+        if constexpr (C == 2) *reinterpret_cast<float2*>(p) = make_float2(r.v[0], r.v[1]);
+        else *reinterpret_cast<float4*>(p) = make_float4(r.v[0], r.v[1], r.v[2], r.v[3]);
     }
     __device__ __forceinline__ Row<C> lds_get(const float* p) const
     {
@@ -339,56 +204,18 @@ struct JLag {
         if constexpr (C == 2) {
             float2 q = *reinterpret_cast<const float2*>(p);
             r.v[0] = q.x; r.v[1] = q.y;
-        } else if constexpr (C == 4) {
+        } else {
             float4 q = *reinterpret_cast<const float4*>(p);
             r.v[0] = q.x; r.v[1] = q.y; r.v[2] = q.z; r.v[3] = q.w;
-        } else {
-#pragma unroll
-            for (int j = 0; j < C; j++) r.v[j] = p[j];
         }
         return r;
     }
-#endif
 
-    // Step k = (group base) + PH; kb = group base mod R (used by the LDS L ring only).
+    // general form: T*C scalar updates, stage-wise so consecutive VALU instructions belong to
+    // different updates (hides the dependent-issue latency)
     template <int PH>
-    __device__ __forceinline__ void step(int k, int kb)
+    __device__ __forceinline__ void sweep_general(const Row<C>* Lv, Row<C>* nw) const
     {
-        // level-0 row k-1 (loaded last step) joins the ring
-        H[0][slot(PH, 1)] = In[(PH + NB - 1) % NB];
-#if PF_JLAG_LDSL
-        // L row k (landed in Lin last step) goes to its ring slot; fetch L row k+1.  The slot
-        // is reused by row k+R > k, after every level has read row k (last read at k + 2T).
-        lds_put(lslot(kb, PH), Lin[PH % NB]);
-        Lin[(PH + PF) % NB] = load_row(lnorm, k + PF);
-        Row<C> Lv[T];
-#pragma unroll
-        for (int t = 1; t <= T; t++) Lv[t - 1] = lds_get(lslot(kb, PH - 2 * t));
-#endif
-#if PF_JLAG_TOUCH
-        // Touch loads: bring the input and L rows PF_JLAG_TOUCH steps ahead into L2 (their
-        // first use would otherwise wait on HBM with only one step of lead).  The values are
-        // folded into a dummy one step later so the waits never land in this step.
-        if constexpr (SRC == SRC_BUF) {
-            touch_acc ^= __float_as_uint(Tch[(PH + 1) & 1][0].v[0]) ^
-                         __float_as_uint(Tch[(PH + 1) & 1][1].v[0]);
-            Tch[PH & 1][0] = load_row(src, k + PF_JLAG_TOUCH);
-        } else {
-            touch_acc ^= __float_as_uint(Tch[(PH + 1) & 1][1].v[0]);
-        }
-        Tch[PH & 1][1] = load_row(lnorm, k + PF_JLAG_TOUCH);
-#endif
-        // loads for the next step: input row k, L rows (k+1) - 2t
-        In[(PH + PF - 1) % NB] = load_input(k + PF - 1);
-#if !PF_JLAG_LDSL
-#pragma unroll
-        for (int t = 1; t <= T; t++) Lb[(PH + 1) & 1][t - 1] = load_row(lnorm, k + 1 - 2 * t);
-        const Row<C>* Lv = Lb[PH & 1];
-#endif
-        Row<C> nw[T];
-#if PF_JLAG_STAGEWISE
-        // Stage-wise over the T*C independent updates of this step, so consecutive VALU
-        // instructions belong to different updates (hides the dependent-issue latency).
         float Wl[T], Er[T];
 #pragma unroll
         for (int t = 1; t <= T; t++) {
@@ -404,6 +231,10 @@ struct JLag {
                 float W = j == 0 ? Wl[t - 1] : c.v[j - 1];
                 cur[t - 1][j] = W + H[t - 1][slot(PH, 2 * t + 1)].v[j];
             }
+        // Lcur = (((W*q + N*q) + b) + S*q) + E*q with q = -1/4.  Every product by q (and by 0.5
+        // below) is exact -- a power-of-two scaling -- so fl(W*q + N*q) = q*fl(W+N) and
+        // fl(a + x*q) = fma(x, q, a): the fused form rounds exactly where the reference rounds.
+        // (Exact unless an operand is below 2^-124, which depths in [0,1] never reach here.)
 #pragma unroll
         for (int t = 1; t <= T; t++)
 #pragma unroll
@@ -422,6 +253,8 @@ struct JLag {
                 float E = j == C - 1 ? Er[t - 1] : c.v[j + 1];
                 cur[t - 1][j] = __builtin_fmaf(E, -0.25f, cur[t - 1][j]);
             }
+        // un-windowed pixel (L = marker): Lcur = L = 0, so the step is exactly +0.  Masked with
+        // an AND so the compiler keeps this straight-line (no exec-mask branch).
 #pragma unroll
         for (int t = 1; t <= T; t++)
 #pragma unroll
@@ -436,51 +269,184 @@ struct JLag {
 #pragma unroll
             for (int j = 0; j < C; j++) {
                 const float b = H[t - 1][slot(PH, 2 * t)].v[j];
-                float tt = __builtin_fmaf(cur[t - 1][j], 0.5f, b);
+                float tt = __builtin_fmaf(cur[t - 1][j], 0.5f, b);  // b + (L - Lcur)*0.5
                 float v = tt * (1 - (float)1e-4) + b * (float)1e-4;
+                // clamp01: b is never -0 or NaN here, so med3 equals the reference's compares
                 nw[t - 1].v[j] = __builtin_amdgcn_fmed3f(v, 0.0f, 1.0f);
             }
-#else
+    }
+
+    // FAST form (C == 2): the same update on the lane's column pair with packed ops, stage-wise
+    // over groups of PF_JPK_GROUP levels (bounds the live temporaries, i.e. the VGPR count).
+    template <int PH, int T0, int T1, bool ROWS>
+    __device__ __forceinline__ void sweep_packed_group(const Row<C>* Lv, Row<C>* nw, int k) const
+    {
+        constexpr int G = T1 - T0;
+        const f2 q = {-0.25f, -0.25f};
+        const f2 reg = {(float)1e-4, (float)1e-4};
+        const f2 reg_ = {1 - (float)1e-4, 1 - (float)1e-4};
+        float Wl[G], Er[G];
 #pragma unroll
-        for (int t = 1; t <= T; t++)
-            nw[t - 1] = sweep_row<C>(H[t - 1][slot(PH, 2 * t + 1)], H[t - 1][slot(PH, 2 * t)],
-                                     H[t - 1][slot(PH, 2 * t - 1)], Lv[t - 1]);
+        for (int g = 0; g < G; g++) {
+            constexpr int t0 = T0 + 1;
+            Wl[g] = dpp_from_left(H[t0 + g - 1][slot(PH, 2 * (t0 + g))].v[1]);
+            Er[g] = dpp_from_right(H[t0 + g - 1][slot(PH, 2 * (t0 + g))].v[0]);
+        }
+        f2 cur[G];
+        // Lcur = (((W*q + N*q) + b) + S*q) + E*q, q = -1/4, as in sweep_general
+#pragma unroll
+        for (int g = 0; g < G; g++) {
+            const int t = T0 + 1 + g;
+            cur[g] = f2{Wl[g], H[t - 1][slot(PH, 2 * t)].v[0]} + H[t - 1][slot(PH, 2 * t + 1)].v;
+        }
+#pragma unroll
+        for (int g = 0; g < G; g++) {
+            const int t = T0 + 1 + g;
+            cur[g] = __builtin_elementwise_fma(cur[g], q, H[t - 1][slot(PH, 2 * t)].v);
+        }
+#pragma unroll
+        for (int g = 0; g < G; g++) {
+            const int t = T0 + 1 + g;
+            cur[g] = __builtin_elementwise_fma(H[t - 1][slot(PH, 2 * t - 1)].v, q, cur[g]);
+        }
+#pragma unroll
+        for (int g = 0; g < G; g++) {
+            const int t = T0 + 1 + g;
+            cur[g] = __builtin_elementwise_fma(f2{H[t - 1][slot(PH, 2 * t)].v[1], Er[g]}, q, cur[g]);
+        }
+#pragma unroll
+        for (int g = 0; g < G; g++) {
+            const int t = T0 + 1 + g;
+            // rows h0 and h1 are un-windowed (the host certified the rest of the band); only
+            // passes whose row window reaches them (ROWS) pay for the test
+            f2 hh = f2{hcol0, hcol1};
+            if constexpr (ROWS) {
+                const int row = k - 2 * t;
+                const float hr = (row == h0 || row == h1) ? 0.0f : 1.0f;
+                hh = hh * hr;
+            }
+            cur[g] = __builtin_elementwise_fma(Lv[t - 1].v - cur[g], hh, H[t - 1][slot(PH, 2 * t)].v);
+        }
+#pragma unroll
+        for (int g = 0; g < G; g++) {
+            const int t = T0 + 1 + g;
+            nw[t - 1].v = pk_add_clamp01(cur[g] * reg_, H[t - 1][slot(PH, 2 * t)].v * reg);
+        }
+    }
+    template <int PH, int T0, bool ROWS>
+    __device__ __forceinline__ void sweep_packed(const Row<C>* Lv, Row<C>* nw, int k) const
+    {
+        constexpr int T1 = T0 + PF_JPK_GROUP < T ? T0 + PF_JPK_GROUP : T;
+        sweep_packed_group<PH, T0, T1, ROWS>(Lv, nw, k);
+        if constexpr (T1 < T) sweep_packed<PH, T1, ROWS>(Lv, nw, k);
+    }
+
+    // Step k = (group base) + PH; GB = group base mod R.
+    template <int PH, bool ROWS, int GB>
+    __device__ __forceinline__ void step(int k)
+    {
+        // level-0 row k-1 (loaded last step) joins the ring
+        H[0][slot(PH, 1)] = In[(PH + NB - 1) % NB];
+        // L row k (landed in Lin last step) goes to its ring slot; fetch L row k+PF.  The slot
+        // is reused by row k+R > k, after every level has read row k (last read at k + 2T).
+        Row<C> Lv[T];
+#if PF_JDBG_NOLDS  // profiling only (wrong results): no LDS ring
+#pragma unroll
+        for (int t = 1; t <= T; t++) Lv[t - 1] = Lin[(PH + t) % NB];
+#else
+        lds_put(lslot<GB, PH>(), Lin[PH % NB]);
+#pragma unroll
+        for (int t = 1; t <= T; t++) Lv[t - 1] = lds_get(lslot_t<GB, PH>(t));
 #endif
+#if PF_JDBG_NOGLOBAL  // profiling only (wrong results): no global loads in the loop
+        Lin[(PH + PF) % NB] = H[T - 1][slot(PH, 1)];
+        In[(PH + PF - 1) % NB] = H[T - 2][slot(PH, 2)];
+#else
+        Lin[(PH + PF) % NB] = load_row(lnorm, k + PF);
+        // input row k + PF - 1 for a later step
+        In[(PH + PF - 1) % NB] = load_input(k + PF - 1);
+#endif
+        Row<C> nw[T];
+        if constexpr (FAST) sweep_packed<PH, 0, ROWS>(Lv, nw, k);
+        else sweep_general<PH>(Lv, nw);
 #pragma unroll
         for (int t = 1; t < T; t++) H[t][slot(PH, 2 * t)] = nw[t - 1];
         const int j = k - 2 * T;  // final-level row finished this step
-        if (j >= r0 && j < r1) {
+        // xs0, vlo, vhi and C are even, so a lane's columns are all inside [vlo, vhi) or all
+        // outside: one vector store per lane.
+        if (j >= r0 && j < r1 && xs0 >= vlo && xs0 < vhi) {
             const long long rowb = (long long)j * w + colbase;
+            if constexpr (OUT16) {
+                // quantise (Depth.cpp:1721-1736); v is already in [0,1], truncating cast
+                uint32_t qv[C];
 #pragma unroll
-            for (int q = 0; q < C; q++) {
-                int x = xs0 + q;
-                if (x >= vlo && x < vhi) {
-                    if constexpr (OUT16) {
-                        float v = nw[T - 1].v[q];
-                        if (v < 0) v = 0;
-                        if (v > 1) v = 1;
-                        (out + rowb)[lo + q] = (uint16_t)(v * 65535.0f);
-                    } else {
-                        (dst + rowb)[lo + q] = nw[T - 1].v[q];
-                    }
+                for (int p = 0; p < C; p++) qv[p] = (uint32_t)(nw[T - 1].v[p] * 65535.0f);
+                if constexpr (C == 2) {
+                    *reinterpret_cast<uint32_t*>(out + rowb + lo) = qv[0] | (qv[1] << 16);
+                } else {
+                    *reinterpret_cast<uint2*>(out + rowb + lo) =
+                        make_uint2(qv[0] | (qv[1] << 16), qv[2] | (qv[3] << 16));
                 }
+            } else {
+                if constexpr (C == 2)
+                    *reinterpret_cast<float2*>(dst + rowb + lo) = make_float2(nw[T - 1].v[0], nw[T - 1].v[1]);
+                else
+                    *reinterpret_cast<float4*>(dst + rowb + lo) =
+                        make_float4(nw[T - 1].v[0], nw[T - 1].v[1], nw[T - 1].v[2], nw[T - 1].v[3]);
             }
         }
     }
+
+    // one group of 6 steps starting at k, k mod R == 6G
+    template <bool ROWS, int G>
+    __device__ __forceinline__ void group(int k)
+    {
+        step<0, ROWS, 6 * G>(k);
+        step<1, ROWS, 6 * G>(k + 1);
+        step<2, ROWS, 6 * G>(k + 2);
+        step<3, ROWS, 6 * G>(k + 3);
+        step<4, ROWS, 6 * G>(k + 4);
+        step<5, ROWS, 6 * G>(k + 5);
+    }
+    // groups G..NG-1 of the unrolled ring period; returns false once k reaches kend
+    template <bool ROWS, int G>
+    __device__ __forceinline__ bool groups_from(int& k, int kend)
+    {
+        group<ROWS, G>(k);
+        k += 6;
+        if (k >= kend) return false;
+        if constexpr (G + 1 < NG) return groups_from<ROWS, G + 1>(k, kend);
+        else return true;
+    }
+    // the step loop: enter the unrolled ring period at group g0 = (k0 mod R) / 6
+    template <bool ROWS>
+    __device__ __forceinline__ void run(int k0, int kend, int g0)
+    {
+        int k = k0;
+        bool more = true;
+        if constexpr (NG > 3) { if (g0 == 3) more = groups_from<ROWS, (NG > 3 ? 3 : 0)>(k, kend); }
+        if constexpr (NG > 2) { if (more && g0 == 2) more = groups_from<ROWS, (NG > 2 ? 2 : 0)>(k, kend); }
+        if constexpr (NG > 1) { if (more && g0 == 1) more = groups_from<ROWS, (NG > 1 ? 1 : 0)>(k, kend); }
+        static_assert(NG <= 4, "entry switch covers up to 4 groups");
+        while (more) more = groups_from<ROWS, 0>(k, kend);
+    }
 };
 
-template <int C, int T, int SRC, bool OUT16>
+template <int C, int T, int SRC, bool OUT16, bool FAST>
 __global__ void __launch_bounds__(256, PF_JLAG_WAVES) k_jlag(JacobiPass P)
 {
+    using S_t = JLag<C, T, SRC, OUT16, FAST>;
     const int lane = threadIdx.x & 63;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int job = blockIdx.x * 4 + wave;
     if (job >= P.nstrips * P.nchunks) return;  // wave-uniform
     const int b = blockIdx.y;
     const int strip = job % P.nstrips, chunk = job / P.nstrips;
-    JLag<C, T, SRC, OUT16> S;
+    S_t S;
     S.P = &P;
     S.w = P.w;
+    S.h0 = P.h0;
+    S.h1 = P.h1;
     S.colbase = strip * P.V - P.Tp;
     S.lo = lane * C;
     S.rlo = 1;
@@ -490,87 +456,55 @@ __global__ void __launch_bounds__(256, PF_JLAG_WAVES) k_jlag(JacobiPass P)
     S.vhi = min(S.vlo + P.V, P.w);
     S.r0 = P.h0 + chunk * P.rows_per_chunk;
     S.r1 = min(S.r0 + P.rows_per_chunk, P.h1 + 1);
-    S.npx = (long long)P.w * P.h;
     S.src = P.src + b * P.sstride;
     S.prev = P.prev + b * P.pstride;
     S.emap = P.emap + b * P.estride;
     S.lnorm = P.lnorm + b * P.lstride;
     S.dst = P.dst + b * P.dstride;
     S.out = P.out + b * P.ostride;
+    // H of the lane's two columns.  Column 0 is un-windowed (certified), so the only halo cell
+    // that can reach a stored pixel is virtual column w (pixel (0, Y+1), the east tap of column
+    // w-1 -- the seam quirk), whose H is 0; other halo cells get 0 too (never read).
+    S.hcol0 = S.hcol1 = 0.0f;
+    if constexpr (FAST) {
+        if (S.xs0 >= 0 && S.xs0 < P.w) {
+            S.hcol0 = P.hcol[S.xs0];
+            S.hcol1 = P.hcol[S.xs0 + 1];
+        }
+    }
 #pragma unroll
     for (int t = 0; t < T; t++)
 #pragma unroll
         for (int q = 0; q < 3; q++)
 #pragma unroll
             for (int j = 0; j < C; j++) S.H[t][q].v[j] = 0.0f;
-    constexpr int NB = JLag<C, T, SRC, OUT16>::NB;
 #pragma unroll
-    for (int q = 0; q < NB; q++) {
+    for (int q = 0; q < S_t::NB; q++)
 #pragma unroll
-        for (int j = 0; j < C; j++) S.In[q].v[j] = 0.0f;
-#if PF_JLAG_LDSL
-#pragma unroll
-        for (int j = 0; j < C; j++) S.Lin[q].v[j] = 0.0f;
-#endif
-    }
-#if !PF_JLAG_LDSL
-#pragma unroll
-    for (int q = 0; q < 2; q++)
-#pragma unroll
-        for (int t = 0; t < T; t++)
-#pragma unroll
-            for (int j = 0; j < C; j++) S.Lb[q][t].v[j] = 0.0f;
-#endif
-#if PF_JLAG_LDSL
-    constexpr int R = JLag<C, T, SRC, OUT16>::R;
+        for (int j = 0; j < C; j++) { S.In[q].v[j] = 0.0f; S.Lin[q].v[j] = 0.0f; }
+    constexpr int R = S_t::R;
     __shared__ float lds_l[4 * R * 64 * C];  // per-wave private rings, no barriers needed
     S.lring = lds_l + wave * (R * 64 * C);
     S.lane_c = lane * C;
-#endif
-#if PF_JLAG_TOUCH
-    S.touch_acc = 0;
-#pragma unroll
-    for (int q = 0; q < 2; q++)
-#pragma unroll
-        for (int r = 0; r < 2; r++)
-#pragma unroll
-            for (int j = 0; j < C; j++) S.Tch[q][r].v[j] = 0.0f;
-#endif
     // steps k0 .. kend: level 0 needs rows from r0 - T, the last output row r1-1 finishes at
     // step r1 - 1 + 2T; k0 is rounded down to a multiple of 6 so ring slots are static.
     int kfirst = S.r0 - T - 1;
     int k0 = kfirst - (((kfirst % 6) + 6) % 6);
     int kend = S.r1 + 2 * T;
     // prime the rows the first steps consume before their in-loop loads land (the rest are
-    // loaded PF steps ahead inside step()).  With the LDS ring the slots of rows before k0 stay
-    // unwritten: they only feed halo/stale cells, exactly like the zero-initialised level rows.
-    // k0 is a multiple of 6, so row k0 + r sits in buffer r.
+    // loaded PF steps ahead inside step()).  The ring slots of rows before k0 stay unwritten:
+    // they only feed halo/stale cells, like the zero-initialised level rows.  k0 is a multiple
+    // of 6, so row k0 + r sits in buffer r.
 #pragma unroll
-    for (int r = 0; r + 1 < JLag<C, T, SRC, OUT16>::PF; r++) S.In[r] = S.load_input(k0 + r);
-#if PF_JLAG_LDSL
+    for (int r = 0; r + 1 < S_t::PF; r++) S.In[r] = S.load_input(k0 + r);
 #pragma unroll
-    for (int r = 0; r < JLag<C, T, SRC, OUT16>::PF; r++) S.Lin[r] = S.load_row(S.lnorm, k0 + r);
-    int kb = ((k0 % R) + R) % R;
-#else
-#pragma unroll
-    for (int t = 1; t <= T; t++) S.Lb[0][t - 1] = S.load_row(S.lnorm, k0 - 2 * t);
-    const int kb = 0;
-#endif
-    for (int k = k0; k < kend; k += 6) {
-        S.template step<0>(k, kb);
-        S.template step<1>(k + 1, kb);
-        S.template step<2>(k + 2, kb);
-        S.template step<3>(k + 3, kb);
-        S.template step<4>(k + 4, kb);
-        S.template step<5>(k + 5, kb);
-#if PF_JLAG_LDSL
-        kb = (kb + 6) % R;
-#endif
-    }
-#if PF_JLAG_TOUCH
-    // never true for real data (P.w > 0); keeps the touch loads from being optimised away
-    if (S.touch_acc == 0x7FBADBAEu && P.w < 0) S.dst[0] = 0.0f;
-#endif
+    for (int r = 0; r < S_t::PF; r++) S.Lin[r] = S.load_row(S.lnorm, k0 + r);
+    const int g0 = (((k0 % R) + R) % R) / 6;  // k0 is a multiple of 6, so is R
+    // rows computed by some level of this pass: k - 2t for k in [k0, kend + 5], t in [1, T]
+    const int wlo = k0 - 2 * T, whi = kend + 3;
+    const bool rows = (S.h0 >= wlo && S.h0 <= whi) || (S.h1 >= wlo && S.h1 <= whi);
+    if (!FAST || rows) S.template run<true>(k0, kend, g0);
+    else S.template run<false>(k0, kend, g0);
 }
 
 // Out-of-band rows of a level: 0 (level 0, Depth.cpp:1449-1452) or the nearest upsample of the
@@ -602,80 +536,80 @@ __global__ void __launch_bounds__(256) k_border(const float* __restrict__ prev, 
 }
 
 // ---------------------------------------------------------------------------------------------
-template <int C, int T, int SRC, bool OUT16>
+template <int C, int T, int SRC, bool OUT16, bool FAST>
 static void launch_pass_cts(hipStream_t s, const JacobiPass& P, int batch)
 {
-    static const bool lag = !(getenv("PF_JKERNEL") && strcmp(getenv("PF_JKERNEL"), "stream") == 0);
     long long jobs = (long long)P.nstrips * P.nchunks;
     dim3 grid((unsigned)((jobs + 3) / 4), batch);
-    if (lag) hipLaunchKernelGGL((k_jlag<C, T, SRC, OUT16>), grid, dim3(256), 0, s, P);
-    else hipLaunchKernelGGL((k_jstream<C, T, SRC, OUT16>), grid, dim3(256), 0, s, P);
+    hipLaunchKernelGGL((k_jlag<C, T, SRC, OUT16, FAST>), grid, dim3(256), 0, s, P);
 }
 
-template <int C, int T>
+template <int C, int T, bool FAST>
 static void launch_pass_ct(hipStream_t s, const JacobiPass& P, int batch)
 {
     if (P.out_mode) {
-        if (P.src_mode == SRC_BUF) launch_pass_cts<C, T, SRC_BUF, true>(s, P, batch);
-        else if (P.src_mode == SRC_UPSAMPLE) launch_pass_cts<C, T, SRC_UPSAMPLE, true>(s, P, batch);
-        else launch_pass_cts<C, T, SRC_SEED, true>(s, P, batch);
+        if (P.src_mode == SRC_BUF) launch_pass_cts<C, T, SRC_BUF, true, FAST>(s, P, batch);
+        else if (P.src_mode == SRC_UPSAMPLE) launch_pass_cts<C, T, SRC_UPSAMPLE, true, FAST>(s, P, batch);
+        else launch_pass_cts<C, T, SRC_SEED, true, FAST>(s, P, batch);
     } else {
-        if (P.src_mode == SRC_BUF) launch_pass_cts<C, T, SRC_BUF, false>(s, P, batch);
-        else if (P.src_mode == SRC_UPSAMPLE) launch_pass_cts<C, T, SRC_UPSAMPLE, false>(s, P, batch);
-        else launch_pass_cts<C, T, SRC_SEED, false>(s, P, batch);
+        if (P.src_mode == SRC_BUF) launch_pass_cts<C, T, SRC_BUF, false, FAST>(s, P, batch);
+        else if (P.src_mode == SRC_UPSAMPLE) launch_pass_cts<C, T, SRC_UPSAMPLE, false, FAST>(s, P, batch);
+        else launch_pass_cts<C, T, SRC_SEED, false, FAST>(s, P, batch);
     }
 }
 
-template <int C>
+template <int C, bool FAST>
 static void launch_pass_c(hipStream_t s, const JacobiPass& P, int T, int batch)
 {
     switch (T) {
-        case 1: launch_pass_ct<C, 1>(s, P, batch); break;
-        case 2: launch_pass_ct<C, 2>(s, P, batch); break;
-        case 4: launch_pass_ct<C, 4>(s, P, batch); break;
-        case 5: launch_pass_ct<C, 5>(s, P, batch); break;
-        case 8: launch_pass_ct<C, 8>(s, P, batch); break;
-        default: launch_pass_ct<C, 10>(s, P, batch); break;
+        case 1: launch_pass_ct<C, 1, FAST>(s, P, batch); break;
+        case 2: launch_pass_ct<C, 2, FAST>(s, P, batch); break;
+        case 4: launch_pass_ct<C, 4, FAST>(s, P, batch); break;
+        case 5: launch_pass_ct<C, 5, FAST>(s, P, batch); break;
+        case 8: launch_pass_ct<C, 8, FAST>(s, P, batch); break;
+        default: launch_pass_ct<C, 10, FAST>(s, P, batch); break;
     }
 }
 
 bool jstream_supported_T(int T) { return T == 1 || T == 2 || T == 4 || T == 5 || T == 8 || T == 10; }
 
-template <int T>
+template <int T, bool FAST>
 static int waves_per_cu_t()
 {
     int nb = 0;
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(
-            &nb, reinterpret_cast<const void*>(k_jlag<2, T, SRC_BUF, false>), 256, 0) != hipSuccess)
+            &nb, reinterpret_cast<const void*>(k_jlag<2, T, SRC_BUF, false, FAST>), 256, 0) != hipSuccess)
         nb = 1;
     return nb * 4;
 }
 
 // Resident waves per CU of the pass kernel at depth T (used to size the grid to whole rounds).
-int jstream_waves_per_cu(int T)
+int jstream_waves_per_cu(int T, bool fast)
 {
-    static int cache[11] = {0};
+    static int cache[2][11] = {{0}};
     if (T < 1 || T > 10) return 4;
-    if (!cache[T]) {
+    int& c = cache[fast ? 1 : 0][T];
+    if (!c) {
         switch (T) {
-            case 1: cache[T] = waves_per_cu_t<1>(); break;
-            case 2: cache[T] = waves_per_cu_t<2>(); break;
-            case 4: cache[T] = waves_per_cu_t<4>(); break;
-            case 5: cache[T] = waves_per_cu_t<5>(); break;
-            case 8: cache[T] = waves_per_cu_t<8>(); break;
-            default: cache[T] = waves_per_cu_t<10>(); break;
+            case 1: c = fast ? waves_per_cu_t<1, true>() : waves_per_cu_t<1, false>(); break;
+            case 2: c = fast ? waves_per_cu_t<2, true>() : waves_per_cu_t<2, false>(); break;
+            case 4: c = fast ? waves_per_cu_t<4, true>() : waves_per_cu_t<4, false>(); break;
+            case 5: c = fast ? waves_per_cu_t<5, true>() : waves_per_cu_t<5, false>(); break;
+            case 8: c = fast ? waves_per_cu_t<8, true>() : waves_per_cu_t<8, false>(); break;
+            default: c = fast ? waves_per_cu_t<10, true>() : waves_per_cu_t<10, false>(); break;
         }
     }
-    return cache[T];
+    return c;
 }
 
-void launch_jstream(hipStream_t s, const JacobiPass& P, int C, int T, int batch)
+void launch_jstream(hipStream_t s, const JacobiPass& P, int C, int T, int batch, bool fast)
 {
 #if PF_JACOBI_C4
-    if (C == 4) { launch_pass_c<4>(s, P, T, batch); return; }
+    if (C == 4) { launch_pass_c<4, false>(s, P, T, batch); return; }
 #endif
     (void)C;
-    launch_pass_c<2>(s, P, T, batch);
+    if (fast) launch_pass_c<2, true>(s, P, T, batch);
+    else launch_pass_c<2, false>(s, P, T, batch);
 }
 
 void launch_border(hipStream_t s, const float* prev, long long pstride, LevelDims L, float* a,

@@ -60,12 +60,16 @@ __global__ void __launch_bounds__(256) k_targets_map(const TileGeom* __restrict_
                                                      LevelDims L, float* __restrict__ lnorm,
                                                      long long lstride, int batch)
 {
-    const long long i = (long long)blockIdx.x * 256 + threadIdx.x;
+    // XCD-contiguous runs of band rows: the N/C/S taps of neighbouring rows read the same tile
+    // lines, and so do horizontally adjacent blocks.
+    const unsigned lb = xcd_remap(blockIdx.x + gridDim.x * blockIdx.y, gridDim.x * gridDim.y);
+    const unsigned bx = lb % gridDim.x, by = lb / gridDim.x;
+    const long long i = (long long)bx * 256 + threadIdx.x;
     const long long nband = (long long)L.w * (L.h1 - L.h0 + 1);
     if (i >= nband) return;
     const int Y = (int)(i / L.w) + L.h0, X = (int)(i - (long long)(Y - L.h0) * L.w);
     const long long o = (long long)Y * L.w + X;
-    const int bbeg = blockIdx.y * kTgtBatch;
+    const int bbeg = by * kTgtBatch;
     float acc[kTgtBatch];
 #pragma unroll
     for (int q = 0; q < kTgtBatch; q++) acc[q] = 0.0f;

@@ -318,8 +318,10 @@ __global__ void __launch_bounds__(kWB) k_warp_depth(const TileGeom* __restrict__
                                                     long long tstride, int batch)
 {
     __shared__ float box[2][kCap];
-    const int pid = (int)(blockIdx.x % (unsigned)npatch);
-    const int chunk = (int)(blockIdx.x / (unsigned)npatch);
+    // XCD-contiguous runs of patches: neighbouring patches' footprint boxes share edge lines
+    const unsigned lb = xcd_remap(blockIdx.x, gridDim.x);
+    const int pid = (int)(lb % (unsigned)npatch);
+    const int chunk = (int)(lb / (unsigned)npatch);
     const WarpPatch P = patches[pid];
     const TileGeom& g = geom[P.tile];
     const int t = threadIdx.x;
