@@ -840,12 +840,19 @@ static int fuse_impl(pf_ctx* c, const float* emap, int ew, int eh, int ec, const
         const GridRow* rows = (const GridRow*)lc.rows[l].p;
         {
             StageTimer t(c, PF_STAGE_TARGETS, B * (4.0 * band + 4.0 * (double)c->tile_elems), 1);
-            static const bool direct =
-                getenv("PF_TARGETS") && strcmp(getenv("PF_TARGETS"), "direct") == 0;
+            // PF_TARGETS=direct|map selects the older per-pixel gathers (A/B tuning runs)
+            static const char* tsel = getenv("PF_TARGETS");
+            static const bool direct = tsel && strcmp(tsel, "direct") == 0;
+            static const bool permap = tsel && strcmp(tsel, "map") == 0;
             if (direct)
                 launch_targets(c->stream, (const TileGeom*)c->geom.p, (const TileBox*)lc.box[l].p,
                                0, c->ntiles, cols, rows, tiles, c->tile_elems, coeffs, c->ntiles,
                                L, (float*)c->lnorm.p, st, batch);
+            else if (!permap)
+                launch_targets_patch(c->stream, (const TileGeom*)c->geom.p,
+                                     (const TileBox*)lc.box[l].p, (const TapBox*)lc.tapbox[l].p,
+                                     c->ntiles, (const int32_t*)lc.tapmap[l].p, tiles,
+                                     c->tile_elems, coeffs, L, (float*)c->lnorm.p, st, batch);
             else
                 launch_targets_map(c->stream, (const TileGeom*)c->geom.p,
                                    (const TileBox*)lc.box[l].p, (const TapBox*)lc.tapbox[l].p,

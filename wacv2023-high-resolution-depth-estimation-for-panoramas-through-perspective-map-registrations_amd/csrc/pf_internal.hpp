@@ -118,7 +118,6 @@ __host__ __device__ inline float cubic_map(float X, float a, float b, float c, f
     return Y;
 }
 
-// EquirectangularMap::ValueAtCoord (Depth.cpp:551-556): index math promoted to double by MYPI.
 // XCD-aware block order.  The dispatcher deals workgroup b to XCD (b mod 8) (MI355X_MICROARCH.md,
 // workgroup dispatch); this maps it to a logical block so that every XCD walks one contiguous
 // range of logical blocks, and neighbouring blocks -- which re-read each other's edge lines --
@@ -129,6 +128,7 @@ __device__ __forceinline__ unsigned xcd_remap(unsigned b, unsigned n)
     return x * q + (x < r ? x : r) + s;
 }
 
+// EquirectangularMap::ValueAtCoord (Depth.cpp:551-556): index math promoted to double by MYPI.
 __host__ __device__ inline long long emap_index(float az, float zen, int w, int h, int c)
 {
     int x = (int)((double)az / (PF_MYPI * 2) * (double)(float)(w - 1));
@@ -160,6 +160,10 @@ void launch_targets_map(hipStream_t s, const TileGeom* geom, const TileBox* box,
                         const TapBox* tb, int ntiles, const int32_t* map, const float* tiles,
                         long long tstride, const float* coeffs, LevelDims L, float* lnorm,
                         long long lstride, int batch);
+void launch_targets_patch(hipStream_t s, const TileGeom* geom, const TileBox* box,
+                          const TapBox* tb, int ntiles, const int32_t* map, const float* tiles,
+                          long long tstride, const float* coeffs, LevelDims L, float* lnorm,
+                          long long lstride, int batch);
 bool jstream_supported_T(int T);
 int jstream_waves_per_cu(int T, bool fast);
 void launch_jstream(hipStream_t s, const JacobiPass& P, int C, int T, int batch, bool fast);

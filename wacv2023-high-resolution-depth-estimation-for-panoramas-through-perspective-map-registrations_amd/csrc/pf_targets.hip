@@ -127,6 +127,139 @@ __global__ void __launch_bounds__(256) k_targets_map(const TileGeom* __restrict_
     }
 }
 
+// ---------------------------------------------------------------------------------------------
+// Patch-staged form (the default).  Every fusion-grid point is a tap of up to five stencils, so
+// gathering per pixel reads each tile value five times.  Here a block owns a kTPW x kTPH patch of
+// band pixels and kTNB panoramas; for every tile whose box meets the patch (index order), the tap
+// values of the patch plus a one-pixel ring are gathered once per grid point, transformed once
+// (Depth2DepthTransform), staged in LDS, and the five-point stencils read LDS.  The per-pixel
+// arithmetic and the tile-order accumulation are exactly those of k_targets_map.
+static constexpr int kTPW = 64, kTPH = 4;                        // patch: one pixel per thread
+static constexpr int kTGW = kTPW + 2, kTGH = kTPH + 2, kTG = kTGW * kTGH;  // 396 grid points
+static constexpr int kTNB = 8;                                   // panoramas per block
+
+__device__ __forceinline__ bool box_meets(const TileBox& bx, int X0, int X1, int Y0, int Y1)
+{  // does the box (X from x0 stepping xs, stopping before x1; rows y0..y1) meet [X0,X1]x[Y0,Y1]
+    if (bx.y0 > bx.y1 || bx.y1 < Y0 || bx.y0 > Y1) return false;
+    const int lo = bx.xs > 0 ? bx.x0 : bx.x1 + 1, hi = bx.xs > 0 ? bx.x1 - 1 : bx.x0;
+    return lo <= hi && hi >= X0 && lo <= X1;
+}
+
+template <bool XFORM>
+__global__ void __launch_bounds__(256) k_targets_patch(const TileGeom* __restrict__ geom,
+                                                       const TileBox* __restrict__ box,
+                                                       const TapBox* __restrict__ tb, int ntiles,
+                                                       const int32_t* __restrict__ map,
+                                                       const float* __restrict__ tiles,
+                                                       long long tstride,
+                                                       const float* __restrict__ coeffs,
+                                                       LevelDims L, int npx, int npatch,
+                                                       float* __restrict__ lnorm,
+                                                       long long lstride, int batch)
+{
+    __shared__ float sv[kTNB][kTG];
+    // XCD-contiguous runs of patches (neighbouring patches read the same tile lines)
+    const unsigned lb = xcd_remap(blockIdx.x, gridDim.x);
+    const int pid = (int)(lb % (unsigned)npatch), bgrp = (int)(lb / (unsigned)npatch);
+    const int X0 = (pid % npx) * kTPW, Y0 = L.h0 + (pid / npx) * kTPH;
+    const int t = threadIdx.x;
+    const int X = X0 + (t & (kTPW - 1)), Y = Y0 + t / kTPW;
+    const bool valid = X < L.w && Y <= L.h1;
+    const bool inner = Y > L.h0 && Y < L.h1;
+    const int bbeg = bgrp * kTNB;
+    float acc[kTNB];
+#pragma unroll
+    for (int q = 0; q < kTNB; q++) acc[q] = 0.0f;
+    int n = 0;
+    const int X1 = min(X0 + kTPW - 1, L.w - 1), Y1 = min(Y0 + kTPH - 1, L.h1);
+    for (int p = 0; p < ntiles; p++) {  // tile index order (the reference's accumulation order)
+        const TileBox bx = box[p];
+        if (!box_meets(bx, X0, X1, Y0, Y1)) continue;  // block-uniform
+        const TapBox B = tb[p];
+        const long long toff = geom[p].off;
+        float4 k[kTNB];
+        if constexpr (XFORM) {
+#pragma unroll
+            for (int q = 0; q < kTNB; q++) {
+                const int b = bbeg + q < batch ? bbeg + q : batch - 1;
+                k[q] = *reinterpret_cast<const float4*>(coeffs + ((long long)b * ntiles + p) * 4);
+            }
+        }
+        // stage the tap values of the patch + ring that lie in this tile's tap-index map
+        for (int g = t; g < kTG; g += 256) {
+            const int gx = X0 - 1 + g % kTGW - B.xmin, gy = Y0 - 1 + g / kTGW - B.ymin;
+            if (gx < 0 || gx >= B.nx || gy < 0 || gy >= B.ny) continue;
+            const int32_t m = map[B.off + (long long)gy * B.nx + gx];
+            float v[kTNB];
+#pragma unroll
+            for (int q = 0; q < kTNB; q++) {
+                const int b = bbeg + q < batch ? bbeg + q : batch - 1;
+                v[q] = tiles[b * tstride + toff + m];
+            }
+#pragma unroll
+            for (int q = 0; q < kTNB; q++) {
+                float x = v[q];
+                if constexpr (XFORM) x = cubic_map(x, k[q].x, k[q].y, k[q].z, k[q].w);
+                sv[q][g] = x;
+            }
+        }
+        __syncthreads();
+        if (valid && inner && in_box2(bx, X, Y)) {
+            const int c = (t / kTPW + 1) * kTGW + (t & (kTPW - 1)) + 1;  // (X, Y) in the grid
+#pragma unroll
+            for (int q = 0; q < kTNB; q++) {
+                // taps in std::map key order: (X-1,Y), (X,Y-1), (X,Y), (X,Y+1), (X+1,Y)
+                float Lp = 0;
+                Lp += sv[q][c - 1] * -0.25f;
+                Lp += sv[q][c - kTGW] * -0.25f;
+                Lp += sv[q][c] * 1.0f;
+                Lp += sv[q][c + kTGW] * -0.25f;
+                Lp += sv[q][c + 1] * -0.25f;
+                acc[q] += Lp;
+            }
+            n++;
+        }
+        __syncthreads();
+    }
+    if (!valid) return;
+    float scale = 1.0f;
+    if (n > 1) {
+        float center = 0.0f;
+        for (int i = 0; i < n; i++) center += 1.0f;
+        scale = 1.0f / center;
+    }
+    const long long o = (long long)Y * L.w + X;
+#pragma unroll
+    for (int q = 0; q < kTNB; q++) {
+        const int b = bbeg + q;
+        if (b >= batch) break;
+        float out;
+        if (n == 0) out = __uint_as_float(PF_NAN_MARKER);
+        else if (n == 1) out = acc[q];
+        else out = acc[q] * scale;
+        lnorm[b * lstride + o] = out;
+    }
+}
+
+void launch_targets_patch(hipStream_t s, const TileGeom* geom, const TileBox* box,
+                          const TapBox* tb, int ntiles, const int32_t* map, const float* tiles,
+                          long long tstride, const float* coeffs, LevelDims L, float* lnorm,
+                          long long lstride, int batch)
+{
+    const int npx = (L.w + kTPW - 1) / kTPW;
+    const int npy = (L.h1 - L.h0 + 1 + kTPH - 1) / kTPH;
+    const int npatch = npx * npy;
+    const long long nblk = (long long)npatch * ((batch + kTNB - 1) / kTNB);
+    if (coeffs)
+        hipLaunchKernelGGL(k_targets_patch<true>, dim3((unsigned)nblk), dim3(256), 0, s, geom, box,
+                           tb, ntiles, map, tiles, tstride, coeffs, L, npx, npatch, lnorm, lstride,
+                           batch);
+    else
+        hipLaunchKernelGGL(k_targets_patch<false>, dim3((unsigned)nblk), dim3(256), 0, s, geom,
+                           box, tb, ntiles, map, tiles, tstride, coeffs, L, npx, npatch, lnorm,
+                           lstride, batch);
+}
+
 void launch_tapmap(hipStream_t s, const TileGeom* geom, const TapBox* tb, int ntiles,
                    long long max_points, const GridCol* cols, const GridRow* rows, int32_t* map)
 {
