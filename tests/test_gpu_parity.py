@@ -304,3 +304,55 @@ def test_fuse_bit_exact_coverage_holes(fuser):
     fuser.fuse(_dev(emap)[None], _dev(data)[None].contiguous(), out, ZR)
     ref, _ = O.solve_depth_all(emap, tiles, data, 2048, ZR)
     assert int((out.cpu().numpy().view(np.uint16)[0] != ref).sum()) == 0
+
+
+def test_merge_batch16_staggered_halves(fuser):
+    """A batch of 16: every panorama equals the oracle, and the run with the stage timers on
+    (events between stages) equals the run without."""
+    out_w, ew = CFGS["C1"]
+    lay = PL.config_layout("C1")
+    fuser.set_tiles(lay)
+    tiles, total = O.make_tiles(lay)
+    B = 16
+    seeds = pf_synth.seeds_for(B, 4242)
+    emaps = pf_synth.baseline_emap(seeds, ew, ew // 2).numpy()
+    gts = pf_synth.scene_depth(seeds, out_w, out_w // 2).numpy()
+    resp = pf_synth.responses(seeds, lay.ntiles)
+    datas = np.stack([O.warp_depth(gts[b], tiles, total,
+                                   O.responses(resp[b * lay.ntiles:(b + 1) * lay.ntiles]))
+                      for b in range(B)])
+    out = torch.zeros((B, out_w // 2, out_w), dtype=torch.int16, device=DEV)
+    fuser.merge(_dev(emaps), _dev(datas), out, ZR)
+    got = out.cpu().numpy().view(np.uint16)
+    for b in range(B):
+        ref, _ = O.merge(emaps[b], tiles, datas[b].copy(), out_w, ZR)
+        assert int((got[b] != ref).sum()) == 0, f"pano {b}"
+    fuser.profile(True)
+    out2 = torch.zeros_like(out)
+    fuser.merge(_dev(emaps), _dev(datas), out2, ZR)
+    fuser.profile_read()
+    fuser.profile(False)
+    assert torch.equal(out, out2)
+
+
+def test_merge_c2_batch16_profiled_equals_plain(fuser):
+    out_w, ew = CFGS["C2"]
+    lay = PL.config_layout("C2")
+    fuser.set_tiles(lay)
+    B = 16
+    seeds = pf_synth.seeds_for(B, 99)
+    dev = torch.device(DEV)
+    gt = pf_synth.scene_depth(seeds, out_w, out_w // 2, dev).contiguous()
+    emap = pf_synth.baseline_emap(seeds, ew, ew // 2, dev).contiguous()
+    tiles = torch.empty((B, fuser.tile_elems), dtype=torch.float32, device=dev)
+    fuser.warp_depth(gt, tiles, panofuse.make_responses(pf_synth.responses(seeds, lay.ntiles), dev))
+    outs = []
+    for prof in (False, True):
+        fuser.profile(prof)
+        o = torch.zeros((B, out_w // 2, out_w), dtype=torch.int16, device=dev)
+        fuser.merge(emap, tiles, o, ZR)
+        if prof:
+            fuser.profile_read()
+        outs.append(o)
+    fuser.profile(False)
+    assert torch.equal(outs[0], outs[1])

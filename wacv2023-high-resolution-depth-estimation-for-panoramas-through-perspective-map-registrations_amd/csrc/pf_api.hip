@@ -330,7 +330,9 @@ void pf_destroy(pf_ctx* c)
         release(c->lc.rows[l]);
         release(c->lc.tapbox[l]);
         release(c->lc.tapmap[l]);
+        release(c->lc.hcol[l]);
     }
+
     for (auto& s : c->spans) {
         (void)hipEventDestroy(s.a);
         (void)hipEventDestroy(s.b);
@@ -807,18 +809,15 @@ static float* run_jacobi(pf_ctx* c, const LevelDims& L, int first, const float* 
     return src;
 }
 
-static int fuse_impl(pf_ctx* c, const float* emap, int ew, int eh, int ec, const float* tiles,
-                     const float* coeffs, int batch, int out_w, int out_h, float zr0,
-                     float zr1, uint16_t* out)
+// The fusion levels of panoramas [0, batch) of the given pointers, on c->stream.  ws/lnorm_ws
+// are the workspace bases (pano b of a level with stride st at base + b*st).
+static int fuse_range(pf_ctx* c, const float* emap, int ew, int eh, int ec, const float* tiles,
+                      const float* coeffs, int batch, int out_w, int out_h, uint16_t* out,
+                      float* const ws[3], float* lnorm_ws)
 {
-    int rc;
-    if ((rc = prepare_levels(c, out_w, out_h, zr0, zr1))) return rc;
     const long long plane = (long long)out_w * out_h;
-    for (int k = 0; k < 3; k++)
-        if ((rc = ensure(c, c->buf[k], sizeof(float) * plane * batch))) return rc;
-    if ((rc = ensure(c, c->lnorm, sizeof(float) * plane * batch))) return rc;
     const long long estride = (long long)ew * eh * ec;
-    float* bufs[3] = {(float*)c->buf[0].p, (float*)c->buf[1].p, (float*)c->buf[2].p};
+    float* bufs[3] = {ws[0], ws[1], ws[2]};
     float* prev = nullptr;
     LevelCache& lc = c->lc;
     static const bool naive = getenv("PF_JACOBI") && strcmp(getenv("PF_JACOBI"), "naive") == 0;
@@ -847,17 +846,17 @@ static int fuse_impl(pf_ctx* c, const float* emap, int ew, int eh, int ec, const
             if (direct)
                 launch_targets(c->stream, (const TileGeom*)c->geom.p, (const TileBox*)lc.box[l].p,
                                0, c->ntiles, cols, rows, tiles, c->tile_elems, coeffs, c->ntiles,
-                               L, (float*)c->lnorm.p, st, batch);
+                               L, lnorm_ws, st, batch);
             else if (!permap)
                 launch_targets_patch(c->stream, (const TileGeom*)c->geom.p,
                                      (const TileBox*)lc.box[l].p, (const TapBox*)lc.tapbox[l].p,
                                      c->ntiles, (const int32_t*)lc.tapmap[l].p, tiles,
-                                     c->tile_elems, coeffs, L, (float*)c->lnorm.p, st, batch);
+                                     c->tile_elems, coeffs, L, lnorm_ws, st, batch);
             else
                 launch_targets_map(c->stream, (const TileGeom*)c->geom.p,
                                    (const TileBox*)lc.box[l].p, (const TapBox*)lc.tapbox[l].p,
                                    c->ntiles, (const int32_t*)lc.tapmap[l].p, tiles,
-                                   c->tile_elems, coeffs, L, (float*)c->lnorm.p, st, batch);
+                                   c->tile_elems, coeffs, L, lnorm_ws, st, batch);
         }
         float* res = nullptr;
         if (naive || jacobi_tcap(L) < 1) {
@@ -873,7 +872,7 @@ static int fuse_impl(pf_ctx* c, const float* emap, int ew, int eh, int ec, const
                                      c->stream));
             {
                 StageTimer t(c, PF_STAGE_JACOBI, B * 12.0 * band * L.iters, L.iters);
-                launch_jacobi(c->stream, a, b, (const float*)c->lnorm.p, st, L, L.iters, batch,
+                launch_jacobi(c->stream, a, b, (const float*)lnorm_ws, st, L, L.iters, batch,
                               &res);
             }
             if (last) {
@@ -893,7 +892,7 @@ static int fuse_impl(pf_ctx* c, const float* emap, int ew, int eh, int ec, const
                 StageTimer t(c, PF_STAGE_JACOBI, B * 12.0 * band * L.iters, L.iters);
                 int passes = 0;
                 res = run_jacobi(c, L, l == 0 ? 2 : 1, emap, ew, eh, ec, estride, cols, rows,
-                                 prev, pst, (const float*)c->lnorm.p, a, b, last ? out : nullptr,
+                                 prev, pst, (const float*)lnorm_ws, a, b, last ? out : nullptr,
                                  plane, batch, &passes,
                                  lc.full[l] ? (const float*)lc.hcol[l].p : nullptr);
                 t.set_launches(passes);  // k_jlag launches (rocprof's count for that kernel)
@@ -903,6 +902,25 @@ static int fuse_impl(pf_ctx* c, const float* emap, int ew, int eh, int ec, const
     }
     HIPCHK(c, hipGetLastError());
     return PF_OK;
+}
+
+// SolveDepthAll for a batch, on c->stream.  (Running the batch as two staggered halves on two
+// streams, so that one half's coarse levels overlap the other's fine levels, was measured slower:
+// 10.4-10.6k vs 11.6k panoramas/s at batch 64 -- the half-size passes lose more than the
+// overlap wins.)
+static int fuse_impl(pf_ctx* c, const float* emap, int ew, int eh, int ec, const float* tiles,
+                     const float* coeffs, int batch, int out_w, int out_h, float zr0,
+                     float zr1, uint16_t* out)
+{
+    int rc;
+    if ((rc = prepare_levels(c, out_w, out_h, zr0, zr1))) return rc;
+    const long long plane = (long long)out_w * out_h;
+    for (int k = 0; k < 3; k++)
+        if ((rc = ensure(c, c->buf[k], sizeof(float) * plane * batch))) return rc;
+    if ((rc = ensure(c, c->lnorm, sizeof(float) * plane * batch))) return rc;
+    float* ws[3] = {(float*)c->buf[0].p, (float*)c->buf[1].p, (float*)c->buf[2].p};
+    return fuse_range(c, emap, ew, eh, ec, tiles, coeffs, batch, out_w, out_h, out, ws,
+                      (float*)c->lnorm.p);
 }
 
 extern "C" {
