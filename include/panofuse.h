@@ -42,7 +42,8 @@ typedef struct pf_window {
 
 /* Synthetic stand-in for the external depth net (not part of the reference): per tile,
  * d' = clamp01(alpha*d + (kappa*d)*d + beta + sigma*u), u uniform in [-1,1) hashed from
- * (seed, tile, pixel).  Used only to manufacture benchmark tiles from a ground-truth pano. */
+ * (seed, pixel) -- seed unique per (panorama, layout-wide tile) -- as the oracle's pfo_hash32.
+ * Used only to manufacture benchmark tiles from a ground-truth pano. */
 typedef struct pf_response {
     float alpha, kappa, beta, sigma;
     uint32_t seed, pad;

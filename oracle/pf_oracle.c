@@ -611,16 +611,19 @@ static inline uint32_t mix32(uint32_t x)
     return x;
 }
 
-uint32_t pfo_hash32(uint32_t seed, uint32_t tile, uint32_t idx)
-{ /* counter-based noise keyed by (seed, tile, pixel): the (seed, tile) key is mixed once, the
-   * pixel counter once more (the GPU evaluates the key on its scalar unit) */
-    uint32_t key = mix32(seed ^ mix32(tile + 0x9E3779B9u));
-    return mix32(idx ^ key);
+uint32_t pfo_hash32(uint32_t seed, uint32_t idx)
+{ /* counter-based noise keyed by (seed, pixel).  seed is unique per (panorama, tile) -- the host
+   * folds the layout-wide tile index into it (pf_synth.responses), so a shard's sub-layout warps
+   * the same noise as the whole layout.  The pixel hash mix32(idx) does not depend on the
+   * panorama and the key mix32(seed) does not depend on the pixel; per (panorama, pixel) they
+   * meet in one 24x24-bit multiply, the top 24 bits of its low word are the draw. */
+    uint32_t x = mix32(idx) ^ mix32(seed);
+    return (x & 0xFFFFFFu) * 0x9E3779u;
 }
 
-static inline float response(const pfo_response* r, uint32_t tile, uint32_t idx, float d)
+static inline float response(const pfo_response* r, uint32_t idx, float d)
 {
-    float u = (float)(pfo_hash32(r->seed, tile, idx) >> 8) * (1.0f / 16777216.0f);
+    float u = (float)(pfo_hash32(r->seed, idx) >> 8) * (1.0f / 16777216.0f);
     float nz = u * 2.0f - 1.0f;
     float v = r->alpha * d;
     v = v + (r->kappa * d) * d;
@@ -660,7 +663,7 @@ void pfo_warp_depth(const float* pano, int pw, int ph, const pfo_tile* tiles, in
                 float bot = g10 * (1.0f - fx) + g11 * fx;
                 float v = top * (1.0f - fy) + bot * fy;
                 uint32_t idx = (uint32_t)(Y * t->width + X);
-                if (resp) v = response(&resp[p], (uint32_t)p, idx, v);
+                if (resp) v = response(&resp[p], idx, v);
                 tile_data[t->offset + (long long)idx * t->channels] = v;
             }
     }

@@ -39,7 +39,8 @@ typedef struct pfo_tile {
 } pfo_tile;
 
 /* Synthetic stand-in for the external depth net's response (per tile):
- * d' = clamp01(alpha*d + (kappa*d)*d + beta + sigma*u), u uniform in [-1,1) from a hash. */
+ * d' = clamp01(alpha*d + (kappa*d)*d + beta + sigma*u), u uniform in [-1,1) from
+ * pfo_hash32(seed, pixel) >> 8; seed is unique per (panorama, layout-wide tile). */
 typedef struct pfo_response {
     float alpha, kappa, beta, sigma;
     uint32_t seed;
@@ -109,7 +110,7 @@ int  pfo_merge(const float* emap, int ew, int eh, int ec, const pfo_tile* tiles,
 /* ---------------- E->P depth warp (a5 mapping, Depth.cpp:157-166 + 2960-2971) ------------ */
 void pfo_warp_depth(const float* pano, int pw, int ph, const pfo_tile* tiles, int ntiles,
                     const pfo_response* resp, float* tile_data);
-uint32_t pfo_hash32(uint32_t seed, uint32_t tile, uint32_t idx);
+uint32_t pfo_hash32(uint32_t seed, uint32_t idx);
 
 /* ---------------- E->P RGB warp (a18: Main.cpp:242-326, fs_perspective.txt:67-73) --------- */
 void pfo_warp_rgb(const uint8_t* pano, int pw, int ph, const pfo_tile* tiles, int ntiles,

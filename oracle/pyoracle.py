@@ -84,7 +84,7 @@ def lib():
         L.pfo_warp_depth.argtypes = [fp, C.c_int, C.c_int, TP, C.c_int, C.POINTER(Response), fp]
         L.pfo_warp_rgb.argtypes = [C.POINTER(C.c_uint8), C.c_int, C.c_int, TP, C.c_int,
                                    C.POINTER(C.c_uint8)]
-        L.pfo_hash32.argtypes = [C.c_uint32, C.c_uint32, C.c_uint32]
+        L.pfo_hash32.argtypes = [C.c_uint32, C.c_uint32]
         L.pfo_hash32.restype = C.c_uint32
         L.pfo_set_threads.argtypes = [C.c_int]
         L.pfo_nan_marker.restype = C.c_uint32

@@ -356,3 +356,57 @@ def test_merge_c2_batch16_profiled_equals_plain(fuser):
         outs.append(o)
     fuser.profile(False)
     assert torch.equal(outs[0], outs[1])
+
+
+def test_tile_sharded_pipeline_equals_fuse(fuser):
+    """C5 decomposition on one GPU: sub-layout warps into slices of the full tile block, then
+    pf_dist.fuse_tile_sharded over two simulated ranks (per-rank partials summed, as the RCCL
+    reduce would) == the whole-layout warp + fuse, bit for bit."""
+    import pf_dist
+    out_w, ew = CFGS["C2"]
+    lay = PL.config_layout("C2")
+    seeds = pf_synth.seeds_for(1, 20261015 + 7)
+    gt = pf_synth.scene_depth(seeds, out_w, out_w // 2, DEV).contiguous()
+    emap = pf_synth.baseline_emap(seeds, ew, ew // 2, DEV).contiguous()
+    resp_all = pf_synth.responses(seeds, lay.ntiles)
+    fuser.set_tiles(lay)
+    full = torch.zeros((1, fuser.tile_elems), dtype=torch.float32, device=DEV)
+    fuser.warp_depth(gt, full, panofuse.make_responses(resp_all, DEV))
+    ref = torch.zeros((1, out_w // 2, out_w), dtype=torch.int16, device=DEV)
+    fuser.fuse(emap, full, ref, ZR)
+
+    world = 2
+    tiles = torch.zeros_like(full)
+    off = 0
+    for rank in range(world):
+        t0, t1 = pf_dist.shard_range(lay.ntiles, rank, world)
+        sub = PL.Layout("sub", lay.fovs[t0:t1], lay.ranges[t0:t1], lay.tile_w[t0:t1],
+                        lay.tile_h[t0:t1])
+        fs = panofuse.Fuser(0)
+        fs.set_tiles(sub)
+        fs.warp_depth(gt, tiles[:, off:off + fs.tile_elems],
+                      panofuse.make_responses(resp_all[t0:t1], DEV))
+        off += fs.tile_elems
+        fs.close()
+    assert torch.equal(tiles.view(torch.int32), full.view(torch.int32))
+
+    out = torch.zeros_like(ref)
+    fz = panofuse.Fuser(0)
+    fz.set_tiles(lay)
+    be = pf_dist.HipTileShardBackend(fz, emap, tiles, None, out_w, ZR, out)
+
+    class SumBackend:
+        """Rank 0's view: partial() returns the sum over every simulated rank's shard."""
+        def partial(self, level, t0, t1):
+            acc = None
+            for r in range(world):
+                l, n = be.partial(level, *pf_dist.shard_range(lay.ntiles, r, world))
+                acc = (l, n) if acc is None else (acc[0] + l, acc[1] + n)
+            return acc
+
+        seed, finish = be.seed, be.finish
+
+    nlev = panofuse.level_info(out_w, out_w // 2, ZR, 0)[5]
+    pf_dist.fuse_tile_sharded(SumBackend(), nlev, lay.ntiles, 0, 1)
+    torch.cuda.synchronize()
+    assert int((out != ref).sum().item()) == 0

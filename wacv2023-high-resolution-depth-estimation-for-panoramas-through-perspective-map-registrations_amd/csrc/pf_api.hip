@@ -8,6 +8,7 @@
 #include "../../include/panofuse.h"
 #include "pf_internal.hpp"
 
+#include <algorithm>
 #include <cfloat>
 #include <cmath>
 #include <cstdarg>
@@ -923,6 +924,28 @@ static int fuse_impl(pf_ctx* c, const float* emap, int ew, int eh, int ec, const
                       (float*)c->lnorm.p);
 }
 
+// Once per (layout, panorama size): order the warp patches by panorama footprint -- 32-row bands
+// of the box centre, then its azimuth -- instead of tile by tile.  The blocks resident on one XCD
+// then stage overlapping boxes (neighbouring patches of a tile and the overlapping patches of the
+// neighbouring tiles) at about the same time, so a panorama line is fetched from HBM once and
+// re-read from that XCD's L2 instead of once per box that holds it (the boxes hold each panorama
+// pixel ~3 times at the C2 layout).  Patches are self-describing, so the permutation is free.
+static int sort_warp_patches(pf_ctx* c, int pw)
+{
+    std::vector<WarpPatch> p(c->npatch);
+    HIPCHK(c, hipMemcpyAsync(p.data(), c->wpatch.p, sizeof(WarpPatch) * p.size(),
+                             hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    auto key = [pw](const WarpPatch& w) {
+        const long long band = (w.gy0 + w.bh / 2) / 32;
+        const long long col = (w.gx0 + w.bw / 2) % pw;
+        return band * 65536 + col;
+    };
+    std::stable_sort(p.begin(), p.end(),
+                     [&](const WarpPatch& a, const WarpPatch& b) { return key(a) < key(b); });
+    return upload(c, c->wpatch, p);
+}
+
 extern "C" {
 
 int pf_register(pf_ctx* c, const float* emap, int ew, int eh, int ec, float* tiles, int batch,
@@ -996,6 +1019,9 @@ int pf_warp_depth(pf_ctx* c, const float* pano, int pw, int ph, int batch,
     static_assert(sizeof(pf_response) == sizeof(Resp), "pf_response layout");
     if ((long long)pw * ph >= (1ll << 30) || pw >= 65536 || ph >= 65536)
         return fail(c, PF_EINVAL, "pano %dx%d: too large (< 2^30 pixels, sides < 65536)", pw, ph);
+    if (c->tile_elems >= (1ll << 29))  // the warp addresses a panorama's tile block with 32-bit
+        return fail(c, PF_EINVAL, "tile block of %lld floats: too large for the depth warp "
+                    "(< 2^29)", c->tile_elems);      // byte offsets (buffer stores)
     const long long npix = c->tile_elems / c->tile_c;
     if (c->wmap_pw != pw || c->wmap_ph != ph) {
         if ((rc = ensure(c, c->wmap, sizeof(uint32_t) * npix))) return rc;
@@ -1004,6 +1030,7 @@ int pf_warp_depth(pf_ctx* c, const float* pano, int pw, int ph, int batch,
                             (WarpPatch*)c->wpatch.p, c->npatch, pw, ph, (uint32_t*)c->wmap.p,
                             (float*)c->wfxy.p);
         HIPCHK(c, hipGetLastError());
+        if ((rc = sort_warp_patches(c, pw))) return rc;
         c->wmap_pw = pw;
         c->wmap_ph = ph;
     }

@@ -192,11 +192,13 @@ __global__ void __launch_bounds__(kWB) k_warp_local(const TileGeom* __restrict__
     }
 }
 
-// Per-panorama response of one tile with its noise key, staged in LDS at block start (a scalar
-// load per panorama inside the loop would expose its latency on lgkmcnt with the LDS reads).
+// Per-panorama response of one tile with its noise key mix32(seed), staged in LDS at block start
+// (a scalar load per panorama inside the loop would expose its latency on lgkmcnt with the LDS
+// reads).  The seed is unique per (panorama, layout-wide tile): pf_synth.responses folds the tile
+// index in, so a shard's sub-layout draws the same noise as the whole layout.
 struct RespK {
     float alpha, kappa, beta, sigma;
-    uint32_t key, on, pad[2];
+    uint32_t key, pad[3];
 };
 
 __device__ __forceinline__ RespK resp_key(const Resp* __restrict__ resp, int b, int ntiles,
@@ -206,104 +208,163 @@ __device__ __forceinline__ RespK resp_key(const Resp* __restrict__ resp, int b, 
     if (resp) {
         const Resp r = resp[(long long)b * ntiles + tile];
         k.alpha = r.alpha; k.kappa = r.kappa; k.beta = r.beta; k.sigma = r.sigma;
-        k.key = mix32(r.seed ^ mix32((uint32_t)tile + 0x9E3779B9u));
-        k.on = 1;
+        k.key = mix32(r.seed);
     }
     return k;
 }
 
-// Bilinear sample (Depth.cpp-convention weights, no contraction) + the synthetic depth-net
-// response d' = clamp01(alpha*d + (kappa*d)*d + beta + sigma*u), u uniform in [-1, 1).
-__device__ __forceinline__ float warp_value(float t00, float t01, float t10, float t11, float fx,
-                                            float fy, const RespK& rk, uint32_t i)
-{
-    float top = t00 * (1.0f - fx) + t01 * fx;
-    float bot = t10 * (1.0f - fx) + t11 * fx;
-    float v = top * (1.0f - fy) + bot * fy;
-    if (rk.on) {
-        const RespK* r = &rk;
-        const uint32_t key = rk.key;
-        uint32_t h = mix32(i ^ key);
-        float u = (float)(h >> 8) * (1.0f / 16777216.0f);
-        float nz = u * 2.0f - 1.0f;
-        float t = r->alpha * v;
-        t = t + (r->kappa * v) * v;
-        t = t + r->beta;
-        t = t + r->sigma * nz;
-        if (t < 0) t = 0;
-        else if (t > 1) t = 1;
-        v = t;
-    }
-    return v;
+typedef float f2 __attribute__((ext_vector_type(2)));
+
+__device__ __forceinline__ f2 pk_add_clamp01(f2 a, f2 b)
+{  // v_pk_add_f32 with the output clamp: both lanes to [0, 1] as the reference-style
+   // `if (t < 0) t = 0; else if (t > 1) t = 1` (t is finite and never -0: beta != 0)
+    f2 r;
+    asm("v_pk_add_f32 %0, %1, %2 clamp" : "=v"(r) : "v"(a), "v"(b));
+    return r;
 }
 
-struct WarpLanes {  // one thread's kPx pixels
-    const uint32_t* li;
-    const float *fx, *fy;
-    const uint32_t* pix;
-    const bool* ok;
+// The noise draw of pfo_hash32: hp = mix32(pixel) is per pixel (hoisted out of the panorama
+// loop), key = mix32(seed) per panorama, and one full-rate 24x24-bit multiply mixes them.  Returns
+// h >> 8 as a float; the caller forms nz = u*2 - 1 (u = (h >> 8) * 2^-24) as fma(., 2^-23, -1),
+// exact because the product is a power-of-two scaling of an integer < 2^24.
+__device__ __forceinline__ float noise_top24(uint32_t hp, uint32_t key)
+{
+    const uint32_t h = ((hp ^ key) & 0xFFFFFFu) * 0x9E3779u;
+    return (float)(h >> 8);
+}
+
+__device__ __forceinline__ float add_f32(float a, float b)
+{  // a scalar v_add_f32: keeps the SLP vectoriser from re-pairing lane sums into packed adds
+   // (which costs a v_mov per operand to rebuild the register pairs)
+    float r;
+    asm("v_add_f32 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+    return r;
+}
+
+// Bilinear sample in the reference's operand order, no contraction: P = (c00, c01) * (1-fx, fx)
+// and Q = (c10, c11) * (1-fx, fx) are one packed multiply each, top/bot their lane sums,
+// v = top*(1-fy) + bot*fy with the two products as one more packed multiply.
+__device__ __forceinline__ float bilinear(f2 c0, f2 c1, f2 wx, f2 wy)
+{
+    const f2 p = c0 * wx, q = c1 * wx;
+    const f2 tb = f2{add_f32(p.x, p.y), add_f32(q.x, q.y)} * wy;
+    return add_f32(tb.x, tb.y);
+}
+
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc(const void* base, uint32_t bytes)
+{  // raw buffer descriptor (wave-uniform inputs): 32-bit byte offsets, range-checked
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), 0, (int)bytes, 0x00020000);
+}
+
+struct WarpLanes {  // one thread's kPx pixels, all panorama-invariant
+    uint32_t la[kPx];   // LDS float index of corner (x0, y0) in the parity-interleaved box (x2)
+    uint32_t oo[kPx];   // byte offset of the pixel inside one panorama's tile block; past the
+                        // block (a dropped buffer store) for lanes outside the tile
+    uint32_t hp[kPx];   // mix32(pixel index): the per-pixel half of the noise hash
+    f2 wx[kPx], wy[kPx];  // (1-fx, fx), (1-fy, fy)
+    bool ok[kPx];
 };
 
-// LDS-staged interpolation of kNB panoramas for a box of at most NS*256 floats.  Every staging
-// load is issued unconditionally (slots past the box reload a valid element, panoramas past the
-// chunk reload the last one), so the loads for panorama q+2 go out before panorama q is
-// interpolated and the wait for panorama q+1's loads -- an in-order vmcnt -- never covers them.
-template <int NS>
-__device__ __forceinline__ void warp_staged(float (*box)[kCap], const RespK* rk,
-                                            const WarpPatch& P, const TileGeom& g, int t,
-                                            const WarpLanes& W, const float* __restrict__ pano,
-                                            int pw, int ph, long long pstride,
-                                            float* __restrict__ tiles, long long tstride,
-                                            int bbeg, int nb)
+// LDS-staged interpolation of kNB panoramas for a box of at most NS*256 floats.  The box is
+// double-buffered with the two parities interleaved (element e of parity PA at box[2e + PA]), so
+// a pixel's c00/c01 (and c10/c11) are one ds_read2_b32 with immediate offsets in both parities.
+// Every staging load is issued unconditionally (slots past the box reload a valid element,
+// panoramas past the chunk reload the last one), so the loads for panorama q+2 go out before
+// panorama q is interpolated and the wait for panorama q+1's loads -- an in-order vmcnt -- never
+// covers them.
+template <int NS, bool RESP>
+__device__ __forceinline__ void warp_staged(float* box, const RespK* rk, const WarpPatch& P,
+                                            int t, const WarpLanes& W,
+                                            const float* __restrict__ pano, int pw, int ph,
+                                            long long pstride, float* __restrict__ tiles,
+                                            long long tstride, int bbeg, int nb)
 {
-    const int bw = P.bw, area = P.bw * P.bh;
+    const int bw2 = 2 * P.bw, area = P.bw * P.bh;
     uint32_t goff[NS];  // element e = t + 256*s of the bw x bh box -> panorama offset
 #pragma unroll
     for (int s = 0; s < NS; s++) {
         int e = t + s * kWB;
         e = e < area ? e : area - 1;
-        const int r = e / bw, c = e - r * bw;
+        const int r = e / P.bw, c = e - r * P.bw;
         int row = P.gy0 + r;
         row = row < ph ? row : ph - 1;
         int col = P.gx0 + c;
         col = col < pw ? col : col - pw;
-        goff[s] = (uint32_t)(row * pw + col);
+        goff[s] = (uint32_t)(row * pw + col) * 4u;
     }
     float stg[2][NS];
+    const uint32_t pbytes = (uint32_t)(pstride * 4);
     auto fetch = [&](float* dst, int q) {
-        const float* pp = pano + (long long)(bbeg + (q < nb ? q : nb - 1)) * pstride;
+        const auto pr = rsrc(pano + (long long)(bbeg + (q < nb ? q : nb - 1)) * pstride, pbytes);
 #pragma unroll
-        for (int s = 0; s < NS; s++) dst[s] = pp[goff[s]];
+        for (int s = 0; s < NS; s++)
+            dst[s] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(pr, (int)goff[s], 0, 0));
     };
-    auto put = [&](float* dst, const float* src) {
+    auto put = [&](int pa, const float* src) {
 #pragma unroll
-        for (int s = 0; s < NS; s++) dst[t + s * kWB] = src[s];
+        for (int s = 0; s < NS; s++) box[2 * (t + s * kWB) + pa] = src[s];
     };
     auto iter = [&](auto parity, int q) {
         constexpr int PA = decltype(parity)::value;
-        fetch(stg[PA], q + 2);  // panorama q was put into box[PA] last iteration: reuse stg[PA]
-        const float* L = box[PA];
+        fetch(stg[PA], q + 2);  // panorama q was put into parity PA last iteration: reuse stg[PA]
+        const float* L = box + PA;
         const int b = bbeg + q;
-        const RespK r = rk[q];
-        float* out = tiles + b * tstride + g.off;
-#pragma unroll
-        for (int k = 0; k < kPx; k++) {
-            const float* c = L + W.li[k];
-            const float v = warp_value(c[0], c[1], c[bw], c[bw + 1], W.fx[k], W.fy[k], r,
-                                       W.pix[k]);
-            if (W.ok[k]) out[(long long)W.pix[k] * g.c] = v;
+        const auto orr = rsrc(tiles + b * tstride, (uint32_t)(tstride * 4));
+        f2 al{}, ka{}, be{}, si{};
+        uint32_t key = 0;
+        if (RESP) {
+            const RespK r = rk[q];
+            al = f2{r.alpha, r.alpha}; ka = f2{r.kappa, r.kappa};
+            be = f2{r.beta, r.beta}; si = f2{r.sigma, r.sigma};
+            key = r.key;
         }
-        put(box[1 - PA], stg[1 - PA]);  // panorama q+1 (a duplicate past the chunk: unread)
+#pragma unroll
+        for (int k = 0; k < kPx; k += 2) {
+            f2 v;
+#pragma unroll
+            for (int j = 0; j < 2; j++) {
+                const float* c = L + W.la[k + j];
+                v[j] = bilinear(f2{c[0], c[2]}, f2{c[bw2], c[bw2 + 2]}, W.wx[k + j],
+                                W.wy[k + j]);
+            }
+            if (RESP) {
+                const f2 u = f2{noise_top24(W.hp[k], key), noise_top24(W.hp[k + 1], key)};
+                const f2 nz = __builtin_elementwise_fma(u, f2{0x1p-23f, 0x1p-23f},
+                                                        f2{-1.0f, -1.0f});
+                f2 tt = al * v;
+                tt = tt + (ka * v) * v;
+                tt = tt + be;
+                v = pk_add_clamp01(tt, si * nz);
+            }
+#pragma unroll
+            for (int j = 0; j < 2; j++)
+                __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v[j]), orr, (int)W.oo[k + j],
+                                                      0, 0);
+        }
+        put(1 - PA, stg[1 - PA]);  // panorama q+1 (a duplicate past the chunk: unread)
         __syncthreads();
     };
     fetch(stg[0], 0);
     fetch(stg[1], 1);
-    put(box[0], stg[0]);
+    put(0, stg[0]);
     __syncthreads();
     for (int q = 0; q < nb; q += 2) {
         iter(std::integral_constant<int, 0>{}, q);
         if (q + 1 < nb) iter(std::integral_constant<int, 1>{}, q + 1);
     }
+}
+
+template <int NS>
+__device__ __forceinline__ void warp_staged_sel(bool resp, float* box, const RespK* rk,
+                                                const WarpPatch& P, int t, const WarpLanes& W,
+                                                const float* pano, int pw, int ph,
+                                                long long pstride, float* tiles,
+                                                long long tstride, int bbeg, int nb)
+{
+    if (resp) warp_staged<NS, true>(box, rk, P, t, W, pano, pw, ph, pstride, tiles, tstride,
+                                    bbeg, nb);
+    else warp_staged<NS, false>(box, rk, P, t, W, pano, pw, ph, pstride, tiles, tstride, bbeg,
+                                nb);
 }
 
 __global__ void __launch_bounds__(kWB) k_warp_depth(const TileGeom* __restrict__ geom,
@@ -317,8 +378,9 @@ __global__ void __launch_bounds__(kWB) k_warp_depth(const TileGeom* __restrict__
                                                     float* __restrict__ tiles,
                                                     long long tstride, int batch)
 {
-    __shared__ float box[2][kCap];
-    // XCD-contiguous runs of patches: neighbouring patches' footprint boxes share edge lines
+    __shared__ float box[2 * kCap];
+    // XCD-contiguous runs of patches; the host sorts the patches by panorama footprint, so the
+    // blocks resident on one XCD stage overlapping boxes and re-read each other's lines from L2
     const unsigned lb = xcd_remap(blockIdx.x, gridDim.x);
     const int pid = (int)(lb % (unsigned)npatch);
     const int chunk = (int)(lb / (unsigned)npatch);
@@ -328,19 +390,19 @@ __global__ void __launch_bounds__(kWB) k_warp_depth(const TileGeom* __restrict__
     const int bbeg = chunk * kNB;
     const int nb = min(kNB, batch - bbeg);
 
-    uint32_t li[kPx], pix[kPx];
-    float fx[kPx], fy[kPx];
-    bool ok[kPx];
+    WarpLanes W;
 #pragma unroll
     for (int k = 0; k < kPx; k++) {
         int i;
-        ok[k] = patch_pixel(P, g, t, k, i);
-        pix[k] = (uint32_t)i;
-        li[k] = 0; fx[k] = 0; fy[k] = 0;
-        if (ok[k]) {
-            li[k] = wloc[g.pix_off + i];
+        W.ok[k] = patch_pixel(P, g, t, k, i);
+        W.la[k] = 0; W.wx[k] = f2{1.0f, 0.0f}; W.wy[k] = f2{1.0f, 0.0f};
+        W.hp[k] = mix32((uint32_t)i);
+        W.oo[k] = W.ok[k] ? (uint32_t)(g.off + (long long)i * g.c) * 4u : 0xFFFFFFF0u;
+        if (W.ok[k]) {
+            W.la[k] = wloc[g.pix_off + i];
             const float2 f = wfxy[g.pix_off + i];
-            fx[k] = f.x; fy[k] = f.y;
+            W.wx[k] = f2{1.0f - f.x, f.x};
+            W.wy[k] = f2{1.0f - f.y, f.y};
         }
     }
 
@@ -349,28 +411,39 @@ __global__ void __launch_bounds__(kWB) k_warp_depth(const TileGeom* __restrict__
             const int b = bbeg + q;
             const float* pp = pano + b * pstride;
             const RespK r = resp_key(resp, b, ntiles, P.tile);
-            float* out = tiles + b * tstride + g.off;
+            float* out = tiles + b * tstride;
 #pragma unroll
             for (int k = 0; k < kPx; k++) {
-                if (!ok[k]) continue;
-                const uint32_t o00 = li[k] & 0x3FFFFFFFu, dx = li[k] >> 31;
-                const uint32_t o10 = o00 + (((li[k] >> 30) & 1u) ? (uint32_t)pw : 0u);
-                const float v = warp_value(pp[o00], pp[o00 + dx], pp[o10], pp[o10 + dx], fx[k],
-                                           fy[k], r, pix[k]);
-                out[(long long)pix[k] * g.c] = v;
+                if (!W.ok[k]) continue;
+                const uint32_t o00 = W.la[k] & 0x3FFFFFFFu, dx = W.la[k] >> 31;
+                const uint32_t o10 = o00 + (((W.la[k] >> 30) & 1u) ? (uint32_t)pw : 0u);
+                float v = bilinear(f2{pp[o00], pp[o00 + dx]}, f2{pp[o10], pp[o10 + dx]},
+                                   W.wx[k], W.wy[k]);
+                if (resp) {
+                    const float nz = __builtin_fmaf(noise_top24(W.hp[k], r.key), 0x1p-23f, -1.0f);
+                    float tt = r.alpha * v;
+                    tt = tt + (r.kappa * v) * v;
+                    tt = tt + r.beta;
+                    tt = tt + r.sigma * nz;
+                    v = tt < 0.0f ? 0.0f : (tt > 1.0f ? 1.0f : tt);
+                }
+                out[W.oo[k] >> 2] = v;
             }
         }
         return;
     }
 
+#pragma unroll
+    for (int k = 0; k < kPx; k++) W.la[k] *= 2;  // parity-interleaved box
     __shared__ RespK rk[kNB];  // published by the first barrier inside warp_staged
     if (t < nb) rk[t] = resp_key(resp, bbeg + t, ntiles, P.tile);
     const int ns = (P.bw * P.bh + kWB - 1) / kWB;  // uniform: staging loads per thread
-    WarpLanes W{li, fx, fy, pix, ok};
-    if (ns <= 4) warp_staged<4>(box, rk, P, g, t, W, pano, pw, ph, pstride, tiles, tstride, bbeg, nb);
-    else if (ns <= 8) warp_staged<8>(box, rk, P, g, t, W, pano, pw, ph, pstride, tiles, tstride,
-                                     bbeg, nb);
-    else warp_staged<kSlots>(box, rk, P, g, t, W, pano, pw, ph, pstride, tiles, tstride, bbeg, nb);
+    if (ns <= 4) warp_staged_sel<4>(resp != nullptr, box, rk, P, t, W, pano, pw, ph, pstride,
+                                    tiles, tstride, bbeg, nb);
+    else if (ns <= 8) warp_staged_sel<8>(resp != nullptr, box, rk, P, t, W, pano, pw, ph,
+                                         pstride, tiles, tstride, bbeg, nb);
+    else warp_staged_sel<kSlots>(resp != nullptr, box, rk, P, t, W, pano, pw, ph, pstride,
+                                 tiles, tstride, bbeg, nb);
 }
 
 // ---------------------------------------------------------------------------------------------

@@ -26,6 +26,42 @@ def panorama_block(batch_per_rank, rank, base_seed=20261015):
     return [base_seed + rank * batch_per_rank + i for i in range(batch_per_rank)]
 
 
+class HipTileShardBackend:
+    """GPU backend of `fuse_tile_sharded` for one rank (pf_fuse_partial / pf_fuse_seed /
+    pf_fuse_finish_level on a panofuse.Fuser bound to this rank's GPU).  tiles: [1, tile_elems]
+    of the full layout (only [t0, t1) is read); coeffs: [ntiles, 4] or None; out: the int16
+    [out_h, out_w] result written by the last level on rank 0."""
+
+    def __init__(self, fuser, emap, tiles, coeffs, out_w, zr, out=None):
+        import panofuse
+        self.fz, self.emap, self.tiles, self.coeffs = fuser, emap, tiles, coeffs
+        self.out_w, self.zr, self.out = out_w, zr, out
+        n = panofuse.level_info(out_w, out_w // 2, zr, 0)[5]
+        self.levels = [panofuse.level_info(out_w, out_w // 2, zr, lv) for lv in range(n)]
+
+    def _plane(self, level):
+        import torch
+        w, h = self.levels[level][:2]
+        return torch.empty(h * w, dtype=torch.float32, device=self.tiles.device)
+
+    def partial(self, level, t0, t1):
+        lsum, cnt = self._plane(level), self._plane(level)
+        self.fz.fuse_partial(self.tiles, self.coeffs, t0, t1, self.out_w, self.zr, level,
+                             lsum, cnt)
+        return lsum, cnt
+
+    def seed(self, level, prev):
+        buf = self._plane(level)
+        self.fz.fuse_seed(self.emap if level == 0 else None, prev, self.out_w, self.zr, level,
+                          buf)
+        return buf
+
+    def finish(self, level, lsum, cnt, buf, last):
+        self.fz.fuse_finish_level(lsum, cnt, self.out_w, self.zr, level, buf,
+                                  self.out if last else None)
+        return buf
+
+
 def fuse_tile_sharded(backend, nlevels, ntiles, rank, world, dist=None, group=None):
     """Tile-sharded fusion of one panorama.
 
