@@ -74,6 +74,9 @@ struct pf_ctx {
     bool prof_on = false;
     std::vector<Span> spans;
     std::vector<hipEvent_t> event_pool;
+    // side stream for the finer levels' target planes (fuse_range), created on first use
+    hipStream_t aux = nullptr;
+    hipEvent_t ev_fork = nullptr, ev_tgt[4] = {};
 };
 
 namespace {
@@ -339,6 +342,12 @@ void pf_destroy(pf_ctx* c)
         (void)hipEventDestroy(s.b);
     }
     for (hipEvent_t e : c->event_pool) (void)hipEventDestroy(e);
+    if (c->aux) {
+        (void)hipStreamSynchronize(c->aux);
+        (void)hipStreamDestroy(c->aux);
+        (void)hipEventDestroy(c->ev_fork);
+        for (hipEvent_t e : c->ev_tgt) (void)hipEventDestroy(e);
+    }
     delete c;
 }
 
@@ -810,8 +819,37 @@ static float* run_jacobi(pf_ctx* c, const LevelDims& L, int first, const float* 
     return src;
 }
 
-// The fusion levels of panoramas [0, batch) of the given pointers, on c->stream.  ws/lnorm_ws
-// are the workspace bases (pano b of a level with stride st at base + b*st).
+// Side stream (lowest priority) and its fork/join events, created once per context.
+static int ensure_aux(pf_ctx* c)
+{
+    if (c->aux) return PF_OK;
+    int least = 0, greatest = 0;
+    HIPCHK(c, hipDeviceGetStreamPriorityRange(&least, &greatest));
+    const char* pr = getenv("PF_AUXPRIO");  // A/B runs: "high" | "default" (else lowest)
+    const int prio = pr && !strcmp(pr, "high") ? greatest : (pr && !strcmp(pr, "default") ? 0 : least);
+    HIPCHK(c, hipStreamCreateWithPriority(&c->aux, hipStreamNonBlocking, prio));
+    HIPCHK(c, hipEventCreateWithFlags(&c->ev_fork, hipEventDisableTiming));
+    for (hipEvent_t& e : c->ev_tgt) HIPCHK(c, hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    return PF_OK;
+}
+
+// Floats of the per-level target planes of one panorama (fuse_range's lnorm workspace).
+static long long target_planes(const LevelCache& lc)
+{
+    long long n = 0;
+    for (int l = 0; l < lc.nlevels; l++) n += (long long)lc.dims[l].w * lc.dims[l].h;
+    return n;
+}
+
+// The fusion levels of panoramas [0, batch) of the given pointers, on c->stream.  ws are the
+// level-buffer bases (pano b of a level with stride st at base + b*st); lnorm_ws holds one target
+// plane per level (level l at lnorm_ws + batch * sum_{k<l} st_k), target_planes() * batch floats.
+//
+// The target planes depend only on the tiles and the coefficients, not on any Jacobi result, so
+// the finer levels' planes are gathered on a low-priority side stream while the coarse levels
+// sweep: the level-0 and level-1 passes fill ~2 waves per SIMD (a 512- or 1024-wide band per
+// panorama), leaving room for the gathers.  With the stage timers on, everything stays on
+// c->stream so that every stage's time is its own.
 static int fuse_range(pf_ctx* c, const float* emap, int ew, int eh, int ec, const float* tiles,
                       const float* coeffs, int batch, int out_w, int out_h, uint16_t* out,
                       float* const ws[3], float* lnorm_ws)
@@ -822,6 +860,52 @@ static int fuse_range(pf_ctx* c, const float* emap, int ew, int eh, int ec, cons
     float* prev = nullptr;
     LevelCache& lc = c->lc;
     static const bool naive = getenv("PF_JACOBI") && strcmp(getenv("PF_JACOBI"), "naive") == 0;
+    static const bool noside = getenv("PF_NOSIDE") != nullptr;  // A/B runs
+    float* lnl[4] = {};
+    {
+        long long off = 0;
+        for (int l = 0; l < lc.nlevels; l++) {
+            lnl[l] = lnorm_ws + off;
+            off += (long long)lc.dims[l].w * lc.dims[l].h * batch;
+        }
+    }
+    auto targets = [&](int l, hipStream_t s) {
+        const LevelDims& L = lc.dims[l];
+        const long long st = (long long)L.w * L.h;
+        const GridCol* cols = (const GridCol*)lc.cols[l].p;
+        const GridRow* rows = (const GridRow*)lc.rows[l].p;
+        // PF_TARGETS=direct|map selects the older per-pixel gathers (A/B tuning runs)
+        static const char* tsel = getenv("PF_TARGETS");
+        static const bool direct = tsel && strcmp(tsel, "direct") == 0;
+        static const bool permap = tsel && strcmp(tsel, "map") == 0;
+        if (direct)
+            launch_targets(s, (const TileGeom*)c->geom.p, (const TileBox*)lc.box[l].p, 0,
+                           c->ntiles, cols, rows, tiles, c->tile_elems, coeffs, c->ntiles, L,
+                           lnl[l], st, batch);
+        else if (!permap)
+            launch_targets_patch(s, (const TileGeom*)c->geom.p, (const TileBox*)lc.box[l].p,
+                                 (const TapBox*)lc.tapbox[l].p, c->ntiles,
+                                 (const int32_t*)lc.tapmap[l].p, tiles, c->tile_elems, coeffs, L,
+                                 lnl[l], st, batch);
+        else
+            launch_targets_map(s, (const TileGeom*)c->geom.p, (const TileBox*)lc.box[l].p,
+                               (const TapBox*)lc.tapbox[l].p, c->ntiles,
+                               (const int32_t*)lc.tapmap[l].p, tiles, c->tile_elems, coeffs, L,
+                               lnl[l], st, batch);
+    };
+    const bool side = !c->prof_on && !noside && lc.nlevels > 1;
+    if (side) {
+        int rc;
+        if ((rc = ensure_aux(c))) return rc;
+        // the side stream starts after everything queued so far on c->stream (tiles, coeffs,
+        // and the previous call's reads of these planes)
+        HIPCHK(c, hipEventRecord(c->ev_fork, c->stream));
+        HIPCHK(c, hipStreamWaitEvent(c->aux, c->ev_fork, 0));
+        for (int l = 1; l < lc.nlevels; l++) {
+            targets(l, c->aux);
+            HIPCHK(c, hipEventRecord(c->ev_tgt[l], c->aux));
+        }
+    }
     for (int l = 0; l < lc.nlevels; l++) {
         const LevelDims& L = lc.dims[l];
         const long long st = (long long)L.w * L.h;
@@ -838,26 +922,12 @@ static int fuse_range(pf_ctx* c, const float* emap, int ew, int eh, int ec, cons
         const double band = (double)L.w * (L.h1 - L.h0 + 1);
         const GridCol* cols = (const GridCol*)lc.cols[l].p;
         const GridRow* rows = (const GridRow*)lc.rows[l].p;
-        {
+        float* const lnorm_l = lnl[l];
+        if (side && l > 0) {
+            HIPCHK(c, hipStreamWaitEvent(c->stream, c->ev_tgt[l], 0));
+        } else {
             StageTimer t(c, PF_STAGE_TARGETS, B * (4.0 * band + 4.0 * (double)c->tile_elems), 1);
-            // PF_TARGETS=direct|map selects the older per-pixel gathers (A/B tuning runs)
-            static const char* tsel = getenv("PF_TARGETS");
-            static const bool direct = tsel && strcmp(tsel, "direct") == 0;
-            static const bool permap = tsel && strcmp(tsel, "map") == 0;
-            if (direct)
-                launch_targets(c->stream, (const TileGeom*)c->geom.p, (const TileBox*)lc.box[l].p,
-                               0, c->ntiles, cols, rows, tiles, c->tile_elems, coeffs, c->ntiles,
-                               L, lnorm_ws, st, batch);
-            else if (!permap)
-                launch_targets_patch(c->stream, (const TileGeom*)c->geom.p,
-                                     (const TileBox*)lc.box[l].p, (const TapBox*)lc.tapbox[l].p,
-                                     c->ntiles, (const int32_t*)lc.tapmap[l].p, tiles,
-                                     c->tile_elems, coeffs, L, lnorm_ws, st, batch);
-            else
-                launch_targets_map(c->stream, (const TileGeom*)c->geom.p,
-                                   (const TileBox*)lc.box[l].p, (const TapBox*)lc.tapbox[l].p,
-                                   c->ntiles, (const int32_t*)lc.tapmap[l].p, tiles,
-                                   c->tile_elems, coeffs, L, lnorm_ws, st, batch);
+            targets(l, c->stream);
         }
         float* res = nullptr;
         if (naive || jacobi_tcap(L) < 1) {
@@ -873,7 +943,7 @@ static int fuse_range(pf_ctx* c, const float* emap, int ew, int eh, int ec, cons
                                      c->stream));
             {
                 StageTimer t(c, PF_STAGE_JACOBI, B * 12.0 * band * L.iters, L.iters);
-                launch_jacobi(c->stream, a, b, (const float*)lnorm_ws, st, L, L.iters, batch,
+                launch_jacobi(c->stream, a, b, (const float*)lnorm_l, st, L, L.iters, batch,
                               &res);
             }
             if (last) {
@@ -893,7 +963,7 @@ static int fuse_range(pf_ctx* c, const float* emap, int ew, int eh, int ec, cons
                 StageTimer t(c, PF_STAGE_JACOBI, B * 12.0 * band * L.iters, L.iters);
                 int passes = 0;
                 res = run_jacobi(c, L, l == 0 ? 2 : 1, emap, ew, eh, ec, estride, cols, rows,
-                                 prev, pst, (const float*)lnorm_ws, a, b, last ? out : nullptr,
+                                 prev, pst, (const float*)lnorm_l, a, b, last ? out : nullptr,
                                  plane, batch, &passes,
                                  lc.full[l] ? (const float*)lc.hcol[l].p : nullptr);
                 t.set_launches(passes);  // k_jlag launches (rocprof's count for that kernel)
@@ -918,7 +988,7 @@ static int fuse_impl(pf_ctx* c, const float* emap, int ew, int eh, int ec, const
     const long long plane = (long long)out_w * out_h;
     for (int k = 0; k < 3; k++)
         if ((rc = ensure(c, c->buf[k], sizeof(float) * plane * batch))) return rc;
-    if ((rc = ensure(c, c->lnorm, sizeof(float) * plane * batch))) return rc;
+    if ((rc = ensure(c, c->lnorm, sizeof(float) * target_planes(c->lc) * batch))) return rc;
     float* ws[3] = {(float*)c->buf[0].p, (float*)c->buf[1].p, (float*)c->buf[2].p};
     return fuse_range(c, emap, ew, eh, ec, tiles, coeffs, batch, out_w, out_h, out, ws,
                       (float*)c->lnorm.p);
