@@ -29,6 +29,7 @@ sys.path.insert(0, PKG)
 
 METRIC = "panoramas/sec (whole node), 2048×1024 × 20 tiles, at 1/2/4/8 MI355X"
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+VALU_PEAK_TF = 157.3   # MI355X_MICROARCH.md: peak FP32 vector (packed FMA), spec
 
 
 def parse():
@@ -241,6 +242,7 @@ def main():
     value = total_panos / elapsed
     jms, jbytes, jlaunch = prof["jacobi"]
     achieved = jbytes / (jms * 1e-3) / 1e9 if jms > 0 else 0.0
+    jtf = jbytes / 12.0 * 14.0 / (jms * 1e-3) / 1e12 if jms > 0 else 0.0
     wms, wbytes, wlaunch = prof["warp"]  # read 4 B/pano pixel + write 4 B/tile pixel (8d)
     wach = wbytes / (wms * 1e-3) / 1e9 if wms > 0 else 0.0
     stages = {k: {"ms_per_step": v[0] / nprof,
@@ -283,6 +285,15 @@ def main():
                               "kernel": "k_warp_depth",
                               "avg_launch_us": (wms / wlaunch * 1e3) if wlaunch else None,
                               "bytes_per_launch": (wbytes / wlaunch) if wlaunch else None},
+            # the Jacobi sweep's real bound is VALU issue (temporal blocking moves it off the
+            # HBM roof): algorithmic FLOP = 14 fp32 operations per pixel-update as the
+            # reference writes them (Depth.cpp:1680-1717: 4 mul + 4 add for Lcur, sub, mul,
+            # add, 2 mul, add for b'), against the vector FP32 peak (MI355X_MICROARCH.md)
+            "roofline_valu": {"bound": "valu", "achieved": jtf, "peak": VALU_PEAK_TF,
+                              "unit": "TFLOP/s", "frac": jtf / VALU_PEAK_TF,
+                              "kernel": "k_jlag (all Jacobi passes of the 3 levels, aggregated)",
+                              "flop_per_update": 14,
+                              "updates_per_step": jbytes / 12.0 / nprof},
             "stages": stages,
             "nonzero_px_pano0": nz,
         }

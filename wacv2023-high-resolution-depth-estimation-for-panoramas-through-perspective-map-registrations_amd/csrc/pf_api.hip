@@ -659,16 +659,16 @@ static int check_emap(pf_ctx* c, const float* emap, int ew, int eh, int ec)
 // cost model of plan_level().  Env overrides for tuning runs: PF_JT (largest T), PF_JOVH (per-step
 // overhead in update units), PF_JC=4 (4 columns per lane, builds with PF_JACOBI_C4 only).
 struct JacobiTuning {
-    int C = 2, Tmax = 10;
+    int C = 2, Tmax = 10;  // PF_JC=0: per level, the cheaper of 2 and 4 by the cost model
     double step_overhead = 3.0, lone_cycles = 4.0;  // swept on MI355X (tools/jsweep.sh)
+    double c4_eff = 23.0 / 26.0;  // packed C=4 issue per pixel-update relative to C=2
 };
 
 static JacobiTuning jacobi_tuning()
 {
     JacobiTuning t;
-#if PF_JACOBI_C4
-    if (const char* e = getenv("PF_JC")) t.C = atoi(e) == 4 ? 4 : 2;
-#endif
+    if (const char* e = getenv("PF_JC")) t.C = atoi(e) == 4 ? 4 : (atoi(e) == 0 ? 0 : 2);
+    if (const char* e = getenv("PF_JC4EFF")) t.c4_eff = atof(e);
     if (const char* e = getenv("PF_JT")) t.Tmax = atoi(e);
     if (const char* e = getenv("PF_JOVH")) t.step_overhead = atof(e);
     if (const char* e = getenv("PF_JC1")) t.lone_cycles = atof(e);
@@ -687,8 +687,10 @@ struct PassPlan {
 };
 
 static PassPlan best_chunks(int T, int C, int band_rows, int w, int batch, int per_simd,
-                            int nsimd, double ovh, double c1)
+                            int nsimd, double ovh, double c1, double c4_eff)
 {
+    // VALU work of one step in update units: T*C updates, per-update issue of the C form
+    const double work = C == 4 ? T * 2.0 * c4_eff : (double)T;
     PassPlan best;
     best.T = T;
     best.cost = 1e300;
@@ -707,7 +709,7 @@ static PassPlan best_chunks(int T, int C, int band_rows, int w, int batch, int p
             const double W = (double)((in_round + nsimd - 1) / nsimd);
             cyc += (2.0 * W > c1 ? 2.0 * W : c1);
         }
-        const double cost = cyc * (rows + 3.0 * T + 4.0) * (T + ovh);
+        const double cost = cyc * (rows + 3.0 * T + 4.0) * (work + ovh);
         if (cost < best.cost) {
             best.cost = cost;
             best.nchunks = n;
@@ -727,8 +729,9 @@ static std::vector<PassPlan> plan_level(pf_ctx* c, const LevelDims& L, int C, in
     PassPlan opt[11];
     for (int T : menu)
         if (T <= tcap && jstream_supported_T(T))
-            opt[T] = best_chunks(T, C, band_rows, L.w, batch, jstream_waves_per_cu(T, fast) / 4,
-                                 4 * c->num_cu, tune.step_overhead, tune.lone_cycles);
+            opt[T] = best_chunks(T, C, band_rows, L.w, batch,
+                                 jstream_waves_per_cu(C, T, fast) / 4, 4 * c->num_cu,
+                                 tune.step_overhead, tune.lone_cycles, tune.c4_eff);
     std::vector<double> dp(L.iters + 1, 1e300);
     std::vector<int> choice(L.iters + 1, 1);
     dp[0] = 0;
@@ -775,9 +778,23 @@ static float* run_jacobi(pf_ctx* c, const LevelDims& L, int first, const float* 
     static const JacobiTuning tune = jacobi_tuning();
     static const bool slow = getenv("PF_JSLOW") != nullptr;  // force the general (scalar) form
     const long long st = (long long)L.w * L.h;
-    const int C = (L.w % 4 == 0 && L.w >= 512) ? tune.C : 2;
-    // packed form: C == 2 and the level's separable-coverage certificate (pf_jacobi.hip)
-    const bool fast = hcol && C == 2 && !slow;
+    // packed form: the level's separable-coverage certificate (pf_jacobi.hip)
+    const bool fast = hcol && !slow;
+    // 4 columns per lane (packed form only): fewer DPP moves and pair assemblies per pixel and a
+    // wider strip per halo; 2 keeps more waves resident.  The cost model picks per level.
+    const bool c4ok = jstream_supported_C(4, fast) && L.w % 4 == 0 && L.w >= 512;
+    int C = 2;
+    std::vector<PassPlan> plan = plan_level(c, L, 2, jacobi_tcap(L), batch, fast);
+    if (c4ok && tune.C != 2) {
+        std::vector<PassPlan> p4 = plan_level(c, L, 4, jacobi_tcap(L), batch, fast);
+        double c2 = 0, c4 = 0;
+        for (const PassPlan& pp : plan) c2 += pp.cost;
+        for (const PassPlan& pp : p4) c4 += pp.cost;
+        if (tune.C == 4 || c4 < c2) {
+            C = 4;
+            plan.swap(p4);
+        }
+    }
     JacobiPass P{};
     P.prev = prev; P.pstride = pstride;
     P.emap = emap; P.estride = estride; P.ew = ew; P.eh = eh; P.ec = ec;
@@ -790,11 +807,10 @@ static float* run_jacobi(pf_ctx* c, const LevelDims& L, int first, const float* 
     const int band_rows = L.h1 - L.h0 + 1;
     float* src = (first == 0) ? a : nullptr;
     float* dst = (first == 0) ? b : a;
-    const std::vector<PassPlan> plan = plan_level(c, L, C, jacobi_tcap(L), batch, fast);
     static const bool show = getenv("PF_JPLAN") != nullptr;
     if (show) {
-        fprintf(stderr, "jacobi plan %dx%d band %d iters %d batch %d %s:", L.w, L.h, band_rows,
-                L.iters, batch, fast ? "packed" : "general");
+        fprintf(stderr, "jacobi plan %dx%d band %d iters %d batch %d %s C%d:", L.w, L.h,
+                band_rows, L.iters, batch, fast ? "packed" : "general", C);
         for (const PassPlan& pp : plan) fprintf(stderr, " T%d/n%d", pp.T, pp.nchunks);
         fprintf(stderr, "\n");
     }

@@ -165,7 +165,8 @@ void launch_targets_patch(hipStream_t s, const TileGeom* geom, const TileBox* bo
                           long long tstride, const float* coeffs, LevelDims L, float* lnorm,
                           long long lstride, int batch);
 bool jstream_supported_T(int T);
-int jstream_waves_per_cu(int T, bool fast);
+int jstream_waves_per_cu(int C, int T, bool fast);
+bool jstream_supported_C(int C, bool fast);
 void launch_jstream(hipStream_t s, const JacobiPass& P, int C, int T, int batch, bool fast);
 void launch_border(hipStream_t s, const float* prev, long long pstride, LevelDims L, float* a,
                    float* b, long long stride, uint16_t* out, long long ostride, int batch);

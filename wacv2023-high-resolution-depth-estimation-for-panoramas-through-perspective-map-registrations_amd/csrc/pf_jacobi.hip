@@ -30,6 +30,12 @@
 #include <cstdlib>
 #include <cstring>
 
+#ifndef PF_JACOBI_C4
+#define PF_JACOBI_C4 0   // general (scalar) form at 4 columns per lane
+#endif
+#ifndef PF_JACOBI_C4P
+#define PF_JACOBI_C4P 0  // packed form at 4 columns per lane
+#endif
 #ifndef PF_JLAG_WAVES
 #define PF_JLAG_WAVES 1  // __launch_bounds__ min waves per SIMD of the lagged kernel
 #endif
@@ -65,6 +71,11 @@ struct Row {
 template <>
 struct Row<2> {
     f2 v;
+};
+typedef float f4 __attribute__((ext_vector_type(4)));
+template <>
+struct Row<4> {  // the packed form works on the pairs .lo = columns 0,1 and .hi = columns 2,3
+    f4 v;
 };
 
 }  // namespace
@@ -104,7 +115,7 @@ __device__ __forceinline__ f2 pk_add_clamp01(f2 a, f2 b)
 template <int C, int T, int SRC, bool OUT16, bool FAST>
 struct JLag {
     static_assert(C % 2 == 0, "column pairs: vector stores and the wrap logic assume even C");
-    static_assert(!FAST || C == 2, "the packed form pairs the two columns of a lane");
+    static_assert(!FAST || C == 2 || C == 4, "the packed form works on column pairs");
     static constexpr int PF = PF_JLAG_PF, NB = PF_JLAG_PF + 1;
     // ring of R >= 2T+1 rows, R a multiple of 6: the loop body is unrolled over the R/6 groups
     // of 6 steps so every ring slot is a compile-time constant (LDS immediate offsets, no SALU)
@@ -114,7 +125,7 @@ struct JLag {
     Row<C> Lin[NB];   // L row r lands in Lin[r % NB] (issued at step r - PF), to LDS at step r
     float* lring;     // this wave's ring: R rows of 64*C floats
     int lane_c;       // lane * C (LDS column offset)
-    float hcol0, hcol1;  // FAST: H of the lane's columns: 0.5 (covered column) or 0
+    float hcol[C];  // FAST: H of the lane's columns: 0.5 (covered column) or 0
     const JacobiPass* P;
     int w, xs0, vlo, vhi, r0, r1, h0, h1;
     int colbase;   // virtual column of lane 0 (wave-uniform)
@@ -276,6 +287,77 @@ struct JLag {
             }
     }
 
+    // FAST form, C == 4: the lane's columns 0..3 are the pairs lo = (0, 1) and hi = (2, 3).  The
+    // west pair of hi and the east pair of lo are the same (c1, c2), so per four pixels the
+    // update costs 18 packed ops + 2 DPP moves + 3 pair assemblies (C == 2: 9 + 2 + 2 per two).
+    template <int PH, int T0, int T1, bool ROWS>
+    __device__ __forceinline__ void sweep_packed_group4(const Row<C>* Lv, Row<C>* nw, int k) const
+    {
+        constexpr int G = T1 - T0;
+        const f2 q = {-0.25f, -0.25f};
+        const f2 reg = {(float)1e-4, (float)1e-4};
+        const f2 reg_ = {1 - (float)1e-4, 1 - (float)1e-4};
+        float Wl[G], Er[G];
+#pragma unroll
+        for (int g = 0; g < G; g++) {
+            constexpr int t0 = T0 + 1;
+            Wl[g] = dpp_from_left(H[t0 + g - 1][slot(PH, 2 * (t0 + g))].v[3]);
+            Er[g] = dpp_from_right(H[t0 + g - 1][slot(PH, 2 * (t0 + g))].v[0]);
+        }
+        f2 lo[G], hi[G];
+        // Lcur = (((W*q + N*q) + b) + S*q) + E*q, q = -1/4, as in sweep_general
+#pragma unroll
+        for (int g = 0; g < G; g++) {
+            const int t = T0 + 1 + g;
+            const f4 c = H[t - 1][slot(PH, 2 * t)].v, n = H[t - 1][slot(PH, 2 * t + 1)].v;
+            lo[g] = f2{Wl[g], c[0]} + n.lo;
+            hi[g] = f2{c[1], c[2]} + n.hi;
+        }
+#pragma unroll
+        for (int g = 0; g < G; g++) {
+            const int t = T0 + 1 + g;
+            const f4 c = H[t - 1][slot(PH, 2 * t)].v;
+            lo[g] = __builtin_elementwise_fma(lo[g], q, c.lo);
+            hi[g] = __builtin_elementwise_fma(hi[g], q, c.hi);
+        }
+#pragma unroll
+        for (int g = 0; g < G; g++) {
+            const int t = T0 + 1 + g;
+            const f4 sv = H[t - 1][slot(PH, 2 * t - 1)].v;
+            lo[g] = __builtin_elementwise_fma(sv.lo, q, lo[g]);
+            hi[g] = __builtin_elementwise_fma(sv.hi, q, hi[g]);
+        }
+#pragma unroll
+        for (int g = 0; g < G; g++) {
+            const int t = T0 + 1 + g;
+            const f4 c = H[t - 1][slot(PH, 2 * t)].v;
+            lo[g] = __builtin_elementwise_fma(f2{c[1], c[2]}, q, lo[g]);
+            hi[g] = __builtin_elementwise_fma(f2{c[3], Er[g]}, q, hi[g]);
+        }
+#pragma unroll
+        for (int g = 0; g < G; g++) {
+            const int t = T0 + 1 + g;
+            const f4 c = H[t - 1][slot(PH, 2 * t)].v;
+            f2 hm0 = f2{hcol[0], hcol[1]}, hm1 = f2{hcol[2], hcol[3]};
+            if constexpr (ROWS) {
+                const int row = k - 2 * t;
+                const float hr = (row == h0 || row == h1) ? 0.0f : 1.0f;
+                hm0 = hm0 * hr;
+                hm1 = hm1 * hr;
+            }
+            lo[g] = __builtin_elementwise_fma(Lv[t - 1].v.lo - lo[g], hm0, c.lo);
+            hi[g] = __builtin_elementwise_fma(Lv[t - 1].v.hi - hi[g], hm1, c.hi);
+        }
+#pragma unroll
+        for (int g = 0; g < G; g++) {
+            const int t = T0 + 1 + g;
+            const f4 c = H[t - 1][slot(PH, 2 * t)].v;
+            const f2 a = pk_add_clamp01(lo[g] * reg_, c.lo * reg);
+            const f2 b = pk_add_clamp01(hi[g] * reg_, c.hi * reg);
+            nw[t - 1].v = f4{a[0], a[1], b[0], b[1]};
+        }
+    }
+
     // FAST form (C == 2): the same update on the lane's column pair with packed ops, stage-wise
     // over groups of PF_JPK_GROUP levels (bounds the live temporaries, i.e. the VGPR count).
     template <int PH, int T0, int T1, bool ROWS>
@@ -319,7 +401,7 @@ struct JLag {
             const int t = T0 + 1 + g;
             // rows h0 and h1 are un-windowed (the host certified the rest of the band); only
             // passes whose row window reaches them (ROWS) pay for the test
-            f2 hh = f2{hcol0, hcol1};
+            f2 hh = f2{hcol[0], hcol[1]};
             if constexpr (ROWS) {
                 const int row = k - 2 * t;
                 const float hr = (row == h0 || row == h1) ? 0.0f : 1.0f;
@@ -337,7 +419,8 @@ struct JLag {
     __device__ __forceinline__ void sweep_packed(const Row<C>* Lv, Row<C>* nw, int k) const
     {
         constexpr int T1 = T0 + PF_JPK_GROUP < T ? T0 + PF_JPK_GROUP : T;
-        sweep_packed_group<PH, T0, T1, ROWS>(Lv, nw, k);
+        if constexpr (C == 4) sweep_packed_group4<PH, T0, T1, ROWS>(Lv, nw, k);
+        else sweep_packed_group<PH, T0, T1, ROWS>(Lv, nw, k);
         if constexpr (T1 < T) sweep_packed<PH, T1, ROWS>(Lv, nw, k);
     }
 
@@ -465,12 +548,13 @@ __global__ void __launch_bounds__(256, PF_JLAG_WAVES) k_jlag(JacobiPass P)
     // H of the lane's two columns.  Column 0 is un-windowed (certified), so the only halo cell
     // that can reach a stored pixel is virtual column w (pixel (0, Y+1), the east tap of column
     // w-1 -- the seam quirk), whose H is 0; other halo cells get 0 too (never read).
-    S.hcol0 = S.hcol1 = 0.0f;
+#pragma unroll
+    for (int j = 0; j < C; j++) S.hcol[j] = 0.0f;
     if constexpr (FAST) {
-        if (S.xs0 >= 0 && S.xs0 < P.w) {
-            S.hcol0 = P.hcol[S.xs0];
-            S.hcol1 = P.hcol[S.xs0 + 1];
-        }
+        // xs0 and w are multiples of C, so the lane's C columns are all inside or all outside
+        if (S.xs0 >= 0 && S.xs0 < P.w)
+#pragma unroll
+            for (int j = 0; j < C; j++) S.hcol[j] = P.hcol[S.xs0 + j];
     }
 #pragma unroll
     for (int t = 0; t < T; t++)
@@ -573,41 +657,71 @@ static void launch_pass_c(hipStream_t s, const JacobiPass& P, int T, int batch)
 
 bool jstream_supported_T(int T) { return T == 1 || T == 2 || T == 4 || T == 5 || T == 8 || T == 10; }
 
-template <int T, bool FAST>
+template <int C, int T, bool FAST>
 static int waves_per_cu_t()
 {
     int nb = 0;
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(
-            &nb, reinterpret_cast<const void*>(k_jlag<2, T, SRC_BUF, false, FAST>), 256, 0) != hipSuccess)
+            &nb, reinterpret_cast<const void*>(k_jlag<C, T, SRC_BUF, false, FAST>), 256, 0) != hipSuccess)
         nb = 1;
     return nb * 4;
 }
 
-// Resident waves per CU of the pass kernel at depth T (used to size the grid to whole rounds).
-int jstream_waves_per_cu(int T, bool fast)
+template <int C, bool FAST>
+static int waves_per_cu_c(int T)
 {
-    static int cache[2][11] = {{0}};
+    switch (T) {
+        case 1: return waves_per_cu_t<C, 1, FAST>();
+        case 2: return waves_per_cu_t<C, 2, FAST>();
+        case 4: return waves_per_cu_t<C, 4, FAST>();
+        case 5: return waves_per_cu_t<C, 5, FAST>();
+        case 8: return waves_per_cu_t<C, 8, FAST>();
+        default: return waves_per_cu_t<C, 10, FAST>();
+    }
+}
+
+// Resident waves per CU of the pass kernel at depth T (used to size the grid to whole rounds).
+int jstream_waves_per_cu(int C, int T, bool fast)
+{
+    static int cache[2][2][11] = {{{0}}};
     if (T < 1 || T > 10) return 4;
-    int& c = cache[fast ? 1 : 0][T];
+    int& c = cache[C == 4 ? 1 : 0][fast ? 1 : 0][T];
     if (!c) {
-        switch (T) {
-            case 1: c = fast ? waves_per_cu_t<1, true>() : waves_per_cu_t<1, false>(); break;
-            case 2: c = fast ? waves_per_cu_t<2, true>() : waves_per_cu_t<2, false>(); break;
-            case 4: c = fast ? waves_per_cu_t<4, true>() : waves_per_cu_t<4, false>(); break;
-            case 5: c = fast ? waves_per_cu_t<5, true>() : waves_per_cu_t<5, false>(); break;
-            case 8: c = fast ? waves_per_cu_t<8, true>() : waves_per_cu_t<8, false>(); break;
-            default: c = fast ? waves_per_cu_t<10, true>() : waves_per_cu_t<10, false>(); break;
+        if (C == 4) {
+#if PF_JACOBI_C4
+            if (!fast) c = waves_per_cu_c<4, false>(T);
+#endif
+#if PF_JACOBI_C4P
+            if (fast) c = waves_per_cu_c<4, true>(T);
+#endif
+            if (!c) c = 4;
+        } else {
+            c = fast ? waves_per_cu_c<2, true>(T) : waves_per_cu_c<2, false>(T);
         }
     }
     return c;
 }
 
+// C == 4: packed form in PF_JACOBI_C4P builds, general form in PF_JACOBI_C4 builds (both off by
+// default: measured slower than C == 2 on MI355X; they double the build time).
+bool jstream_supported_C(int C, bool fast)
+{
+    if (C == 2) return true;
+    if (C != 4) return false;
+    return fast ? PF_JACOBI_C4P != 0 : PF_JACOBI_C4 != 0;
+}
+
 void launch_jstream(hipStream_t s, const JacobiPass& P, int C, int T, int batch, bool fast)
 {
+    if (C == 4) {
 #if PF_JACOBI_C4
-    if (C == 4) { launch_pass_c<4, false>(s, P, T, batch); return; }
+        if (!fast) { launch_pass_c<4, false>(s, P, T, batch); return; }
 #endif
-    (void)C;
+#if PF_JACOBI_C4P
+        if (fast) { launch_pass_c<4, true>(s, P, T, batch); return; }
+#endif
+        return;  // unreachable: the host checks jstream_supported_C first
+    }
     if (fast) launch_pass_c<2, true>(s, P, T, batch);
     else launch_pass_c<2, false>(s, P, T, batch);
 }
