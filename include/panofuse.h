@@ -135,6 +135,31 @@ int pf_profile_read(pf_ctx* ctx, double* ms, double* bytes, long long* launches)
 int pf_probe_taps(pf_ctx* ctx, int out_w, int out_h, float zr0, float zr1, int level,
                   int32_t* tap_index);
 
+/* ---- accuracy metrics ----
+ * ErrorData (Depth.cpp:1980-2213) when given16 != NULL: the u16 result [batch][h][w];
+ * ErrorEmap (Depth.cpp:2215-2458) when given != NULL: a float map [batch][h][w][given_c]
+ * (channel 0).  gt: [batch][gh][gw][gc] float in 0..1 (channel 0).  Rows
+ * [(int)(zr0/MYPI*h), (int)(zr1/MYPI*h)] are compared, gt < 1e-4 is skipped, cap_depth caps
+ * both at 10 m; align_way 0 = none, 1 = median shift (exact medians), 2 = least squares.
+ * out: DEVICE array of batch pf_metrics.  Replaces the reference's float outputs
+ * (mse, mae, mre, mselog, delta1..3) and the optional median_shift_factor / least_square_shift. */
+typedef struct pf_metrics {
+    float mse, mae, mre, mselog, delta1, delta2, delta3;
+    float median_shift;          /* gt_median / given_median (align_way 1), else 1 */
+    float ls_s, ls_o;            /* least_square {s, o} (align_way 2), else 0 */
+    float gt_median, given_median;
+    int32_t n, nlog;             /* num_compares, num_log_compares */
+    int32_t reserved[2];
+} pf_metrics;
+int pf_error_metrics(pf_ctx* ctx, const float* gt, int gw, int gh, int gc, const float* given,
+                     const uint16_t* given16, int w, int h, int given_c, int batch, float zr0,
+                     float zr1, int align_way, int cap_depth, pf_metrics* out);
+
+/* Depth2DepthTransform of one map (Depth.cpp:245-274): channel 0 of npix pixels of a DEVICE
+ * buffer with `channels` interleaved channels, X = clamp(v, 1e-4, 1-1e-4),
+ * v' = clamp01(a X^3 + b X^2 + c X + d) in the reference's fp32 order; abcd is a HOST float[4]. */
+int pf_depth_transform(pf_ctx* ctx, float* data, long long npix, int channels, const float* abcd);
+
 #ifdef __cplusplus
 }
 #endif

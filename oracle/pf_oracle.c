@@ -756,3 +756,130 @@ int pfo_probe_taps(const pfo_tile* tiles, int ntiles, const pfo_level* L, int32_
     free(first);
     return 0;
 }
+
+
+/* ---- accuracy metrics: ErrorData (Depth.cpp:1980-2213) / ErrorEmap (Depth.cpp:2215-2458) ---- */
+static int cmp_f32(const void* a, const void* b)
+{
+    float x = *(const float*)a, y = *(const float*)b;
+    return (x > y) - (x < y);
+}
+
+/* One pixel of the compare loops (Depth.cpp:2033-2053 / :2248-2268). */
+static int metrics_px(const float* gt, int gw, int gh, int gc, const float* given,
+                      const uint16_t* given16, int w, int given_c, float rx, float ry, int x,
+                      int y, int abs_skip, int cap, float depth_max, float* v0, float* v1)
+{
+    int X = (int)((float)x * rx), Y = (int)((float)y * ry);
+    if (X > gw - 1) X = gw - 1;
+    if (Y > gh - 1) Y = gh - 1;
+    float a = gt[((long long)Y * gw + X) * gc];
+    float b = given16 ? (float)given16[(long long)y * w + x] / 65535.0f
+                      : given[((long long)y * w + x) * given_c];
+    if ((abs_skip ? fabsf(a) : a) < 1e-4) return 0;
+    if (cap) {
+        a = a < depth_max ? a : depth_max;
+        b = b < depth_max ? b : depth_max;
+    }
+    *v0 = a;
+    *v1 = b;
+    return 1;
+}
+
+void pfo_error_metrics(const float* gt, int gw, int gh, int gc, const float* given,
+                       const uint16_t* given16, int w, int h, int given_c, float zr0, float zr1,
+                       int align_way, int cap_depth, float* out, int* cnt)
+{
+    int height0 = (int)(zr0 / PFO_MYPI * h), height1 = (int)(zr1 / PFO_MYPI * h);
+    float rx = (float)gw / (float)w, ry = (float)gh / (float)h;
+    const float to_matterport = 65535.0f / 4000.0f;
+    float depth_max = 10.0f / to_matterport;
+    float shift = 1.0f, ls_s = 0.0f, ls_o = 0.0f, gt_med = 0.0f, gv_med = 0.0f;
+    int abs_skip = given16 ? 0 : 1;
+    if (height0 < 0) height0 = 0;
+    if (height1 > h - 1) height1 = h - 1;
+    if (align_way == 1) {
+        long long cap = (long long)(height1 - height0 + 1) * w, n = 0;
+        float* g = (float*)malloc(sizeof(float) * (cap > 0 ? cap : 1));
+        float* v = (float*)malloc(sizeof(float) * (cap > 0 ? cap : 1));
+        for (int y = height0; y <= height1; y++)
+            for (int x = 0; x < w; x++) {
+                float a, b;
+                if (!metrics_px(gt, gw, gh, gc, given, given16, w, given_c, rx, ry, x, y, abs_skip,
+                                cap_depth, depth_max, &a, &b))
+                    continue;
+                g[n] = a;
+                v[n] = b;
+                n++;
+            }
+        qsort(g, n, sizeof(float), cmp_f32);
+        qsort(v, n, sizeof(float), cmp_f32);
+        if (n > 0) {
+            gt_med = g[n / 2];
+            gv_med = v[n / 2];
+        }
+        shift = gt_med / gv_med;
+        free(g);
+        free(v);
+    } else if (align_way == 2) {
+        float a00 = 0, a01 = 0, a11 = 0, b0 = 0, b1 = 0;
+        for (int y = height0; y <= height1; y++)
+            for (int x = 0; x < w; x++) {
+                float a, b;
+                if (!metrics_px(gt, gw, gh, gc, given, given16, w, given_c, rx, ry, x, y, 0,
+                                cap_depth, depth_max, &a, &b))
+                    continue;
+                a00 += b * b;
+                a01 += b;
+                a11 += 1;
+                b0 += a * b;
+                b1 += a;
+            }
+        float det = a00 * a11 - a01 * a01;
+        ls_s = (a11 * b0 - a01 * b1) / det;
+        ls_o = (-a01 * b0 + a00 * b1) / det;
+    }
+    float mse = 0, mae = 0, mre = 0, mselog = 0;
+    int n = 0, nlog = 0, f1 = 0, f2 = 0, f3 = 0;
+    for (int y = height0; y <= height1; y++)
+        for (int x = 0; x < w; x++) {
+            float a, b;
+            if (!metrics_px(gt, gw, gh, gc, given, given16, w, given_c, rx, ry, x, y, 0, cap_depth,
+                            depth_max, &a, &b))
+                continue;
+            if (align_way == 1)
+                b *= shift;
+            else if (align_way == 2)
+                b = b * ls_s + ls_o;
+            mse = (float)((double)mse + pow(a - b, 2));
+            mae += fabsf(a - b);
+            mre += fabsf(a - b) / a;
+            if (a > 1e-4 && b > 1e-4) {
+                float lg = log10f(a) - log10f(b);
+                mselog = (float)((double)mselog + pow(lg, 2));
+                nlog++;
+            }
+            if (a > 0 && b > 0) {
+                float r01 = a / b, r10 = b / a;
+                float rm = r01 > r10 ? r01 : r10;
+                if (rm >= 1.25) f1++;
+                if (rm >= pow(1.25, 2)) f2++;
+                if (rm >= pow(1.25, 3)) f3++;
+            }
+            n++;
+        }
+    out[0] = mse / (float)n;
+    out[1] = mae / (float)n;
+    out[2] = mre / (float)n;
+    out[3] = mselog / (float)nlog;
+    out[4] = (float)(n - f1) / (float)n;
+    out[5] = (float)(n - f2) / (float)n;
+    out[6] = (float)(n - f3) / (float)n;
+    out[7] = shift;
+    out[8] = ls_s;
+    out[9] = ls_o;
+    out[10] = gt_med;
+    out[11] = gv_med;
+    cnt[0] = n;
+    cnt[1] = nlog;
+}

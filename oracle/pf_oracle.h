@@ -120,6 +120,14 @@ int  pfo_probe_taps(const pfo_tile* tiles, int ntiles, const pfo_level* L, int32
 void pfo_set_threads(int n);
 uint32_t pfo_nan_marker(void);
 
+/* ErrorData (Depth.cpp:1980-2213; given16 != NULL) / ErrorEmap (Depth.cpp:2215-2458; given
+ * != NULL): sequential fp32 accumulation exactly as written, medians by sorting (the element at
+ * index size/2).  out[0..6] = mse, mae, mre, mselog, delta1, delta2, delta3; out[7] = median
+ * shift; out[8..9] = least-squares {s, o}; out[10..11] = gt / given medians; cnt[0..1] = n, nlog. */
+void pfo_error_metrics(const float* gt, int gw, int gh, int gc, const float* given,
+                       const uint16_t* given16, int w, int h, int given_c, float zr0, float zr1,
+                       int align_way, int cap_depth, float* out, int* cnt);
+
 #ifdef __cplusplus
 }
 #endif

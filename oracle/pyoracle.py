@@ -88,6 +88,9 @@ def lib():
         L.pfo_hash32.restype = C.c_uint32
         L.pfo_set_threads.argtypes = [C.c_int]
         L.pfo_nan_marker.restype = C.c_uint32
+        L.pfo_error_metrics.argtypes = [fp, C.c_int, C.c_int, C.c_int, fp, C.POINTER(C.c_uint16),
+                                        C.c_int, C.c_int, C.c_int, C.c_float, C.c_float,
+                                        C.c_int, C.c_int, fp, C.POINTER(C.c_int)]
         _lib = L
     return _lib
 
@@ -283,3 +286,31 @@ def targets_subset(tiles, t0, t1, tile_data, lv):
     if rc != 0:
         raise ValueError(f"pfo_targets rc={rc}")
     return Lsum.reshape(lv.h, lv.w), cnt.reshape(lv.h, lv.w)
+
+
+METRIC_KEYS = ("mse", "mae", "mre", "mselog", "delta1", "delta2", "delta3", "median_shift",
+               "ls_s", "ls_o", "gt_median", "given_median")
+
+
+def error_metrics(gt, given, zr, align_way=1, cap_depth=True):
+    """ErrorData (given: uint16 [h][w]) / ErrorEmap (given: float [h][w] or [h][w][c]);
+    gt: float [gh][gw] or [gh][gw][gc].  Returns a dict of METRIC_KEYS + n, nlog."""
+    gt = np.ascontiguousarray(gt, np.float32)
+    gh, gw = gt.shape[:2]
+    gc = gt.shape[2] if gt.ndim == 3 else 1
+    h, w = given.shape[:2]
+    out = np.zeros(12, np.float32)
+    cnt = np.zeros(2, np.int32)
+    if given.dtype == np.uint16:
+        g16 = np.ascontiguousarray(given)
+        lib().pfo_error_metrics(_p(gt), gw, gh, gc, None, _p(g16, C.c_uint16), w, h, 1,
+                                zr[0], zr[1], align_way, int(cap_depth), _p(out),
+                                _p(cnt, C.c_int))
+    else:
+        gf = np.ascontiguousarray(given, np.float32)
+        c = gf.shape[2] if gf.ndim == 3 else 1
+        lib().pfo_error_metrics(_p(gt), gw, gh, gc, _p(gf), None, w, h, c, zr[0], zr[1],
+                                align_way, int(cap_depth), _p(out), _p(cnt, C.c_int))
+    d = {k: float(out[i]) for i, k in enumerate(METRIC_KEYS)}
+    d["n"], d["nlog"] = int(cnt[0]), int(cnt[1])
+    return d

@@ -1,0 +1,123 @@
+"""GPU end-to-end of the mode-0 command line (Main.cpp:331-687):
+bin/panofuse_main reads the baseline, the 15 LeReS-layout tiles and the ground truth from
+folders with the reference's naming conventions, fuses on the GPU through the DepthNamespace
+facade, and writes <raw>.png (u16), <raw>.aligned.txt, .res.png and .giv.png.
+
+Bars: the fused u16 PNG is bit-exact against the CPU oracle's MergeDepthMaps on the same
+(u16-quantised) inputs; the metrics file agrees with the oracle's ErrorData/ErrorEmap within
+the tolerances of tests/test_gpu_metrics.py (plus the file's 6-decimal printing).  The
+reference's tiles are JPEG (not decodable by this build): the tiles here are 16-bit PNGs, the
+MiDaS naming of Main.cpp:570-573."""
+import math
+import os
+import struct
+import subprocess
+import zlib
+
+import numpy as np
+import pytest
+
+torch = pytest.importorskip("torch")
+
+pytestmark = pytest.mark.gpu
+
+import panofuse  # noqa: E402
+import pf_layouts as PL  # noqa: E402
+import pf_synth  # noqa: E402
+import pyoracle as O  # noqa: E402
+
+ROOT = os.path.dirname(os.path.dirname(panofuse.LIB_PATH))
+BIN = os.path.join(ROOT, "bin", "panofuse_main")
+MYPI = 3.14159265359
+ZR = PL.ZENITH_RANGE
+
+
+def _png16_write(path, a):
+    h, w = a.shape
+    raw = b"".join(b"\0" + a[y].astype(">u2").tobytes() for y in range(h))
+
+    def chunk(t, d):
+        return struct.pack(">I", len(d)) + t + d + struct.pack(">I", zlib.crc32(t + d))
+    open(path, "wb").write(b"\x89PNG\r\n\x1a\n" +
+                           chunk(b"IHDR", struct.pack(">IIBBBBB", w, h, 16, 0, 0, 0, 0)) +
+                           chunk(b"IDAT", zlib.compress(raw, 1)) + chunk(b"IEND", b""))
+
+
+def _png16_read(path):
+    d = open(path, "rb").read()
+    pos, idat = 8, b""
+    while pos < len(d):
+        n = struct.unpack(">I", d[pos:pos + 4])[0]
+        t, body = d[pos + 4:pos + 8], d[pos + 8:pos + 8 + n]
+        if t == b"IHDR":
+            w, h = struct.unpack(">II", body[:8])
+        elif t == b"IDAT":
+            idat += body
+        pos += 12 + n
+    raw = zlib.decompress(idat)
+    return np.frombuffer(b"".join(raw[y * (2 * w + 1) + 1:(y + 1) * (2 * w + 1)]
+                                  for y in range(h)), ">u2").reshape(h, w).astype(np.uint16)
+
+
+def _cround(x):  # C round(): half away from zero
+    return int(math.copysign(math.floor(abs(x) + 0.5), x))
+
+
+def _q16(a):
+    return (np.clip(a, 0, 1) * 65535.0 + 0.5).astype(np.uint16)
+
+
+def test_mode0_cli_end_to_end(tmp_path):
+    if not torch.cuda.is_available():
+        pytest.fail("GPU test collected on a host without a GPU")
+    d = {k: tmp_path / k for k in ("rgb", "gt", "base", "result_hohonet", "tiles")}
+    for p in d.values():
+        p.mkdir()
+    lay = PL.leres_layout(512, 494)
+    tiles_o, total = O.make_tiles(lay)
+    expected = {}
+    for i, raw in enumerate(["scene01_rgb", "scene02_rgb"]):
+        (d["rgb"] / (raw + ".jpg")).write_bytes(b"\xff\xd8")  # only the name is used
+        seeds = pf_synth.seeds_for(1, 20261015 + 31 * i)
+        gt = _q16(pf_synth.scene_depth(seeds, 2048, 1024)[0].numpy())
+        base = _q16(pf_synth.baseline_emap(seeds, 512, 256)[0].numpy())
+        _png16_write(d["gt"] / (raw.replace("_rgb", "_depth") + ".png"), gt)
+        _png16_write(d["base"] / (raw + ".depth.png"), base)  # hohonet naming (Main.cpp:512-516)
+        gt_f = gt.astype(np.float32) / np.float32(65535.0)
+        resp = pf_synth.responses(seeds, lay.ntiles)
+        tdata = O.warp_depth(gt_f, tiles_o, total, O.responses(resp))
+        tq = _q16(tdata)
+        off = 0
+        for t in range(lay.ntiles):
+            f = [_cround(float(v) / MYPI * 180.0) for v in lay.fovs[t]]
+            name = f"{raw}.{f[0]}_{f[1]}_{f[2]}_{f[3]}.png"
+            n = 512 * 494
+            _png16_write(d["tiles"] / name, tq[off:off + n].reshape(494, 512))
+            off += n
+        base_f = base.astype(np.float32) / np.float32(65535.0)
+        out, _ = O.merge(base_f, tiles_o, tq.astype(np.float32) / np.float32(65535.0), 2048, ZR)
+        expected[raw] = (out, gt_f, base_f)
+
+    cmd = [BIN, "0", str(d["rgb"]), str(d["gt"]), str(d["base"]), str(d["result_hohonet"]),
+           "--tiles", str(d["tiles"])]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stdout + r.stderr
+    for raw, (out, gt_f, base_f) in expected.items():
+        got = _png16_read(d["result_hohonet"] / (raw + ".png"))
+        assert got.shape == (1024, 2048)
+        bad = int((got != out).sum())
+        assert bad == 0, f"{raw}: {bad} pixels differ from the oracle"
+        for suffix in (".png.res.png", ".png.giv.png"):
+            assert (d["result_hohonet"] / (raw + suffix)).exists()
+        txt = (d["result_hohonet"] / (raw + ".aligned.txt")).read_text()
+        vals = dict(line.split(": ") for line in txt.strip().splitlines())
+        ref_r = O.error_metrics(gt_f, out, ZR, 1, True)
+        ref_g = O.error_metrics(gt_f, base_f, ZR, 1, True)
+        for key, ref in (("result", ref_r), ("given", ref_g)):
+            for m in ("mse", "mae", "mre", "mselog"):
+                assert float(vals[f"{m}_{key}"]) == pytest.approx(ref[m], rel=1e-2, abs=1e-6)
+            for m in ("delta1", "delta2", "delta3"):
+                assert float(vals[f"{m}_{key}"]) == pytest.approx(ref[m], abs=1e-6)
+    # second run: every output exists -> skipped (Main.cpp:552-561)
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0 and r.stdout.count("skip!") == 2

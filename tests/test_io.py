@@ -1,0 +1,192 @@
+"""CPU checks of the file formats either side of the path:
+the PNG / PGM / PFM readers behind EquirectangularMap::Load / PerspectiveMap::Load
+(Depth.cpp:45-109, 277-355, 376-549; stb_image semantics: native channel count, 16-bit samples
+/ 65535, 8-bit / 255), the Save16BitPNG writer (Depth.cpp:27-32), and the mode-0 LeReS layout
+table of the C++ driver against pf_layouts (Main.cpp:788-843).  The PNGs are encoded here with
+zlib + struct (all five filter types, palette, sub-byte gray) and decoded by the library; the
+library's writer is decoded here.  No device calls."""
+import ctypes as C
+import os
+import struct
+import zlib
+
+import numpy as np
+import pytest
+
+import panofuse
+import pf_layouts as PL
+
+LIB = os.path.join(os.path.dirname(panofuse.LIB_PATH), "libpanofuse_depth.so")
+BIN = os.path.join(os.path.dirname(os.path.dirname(panofuse.LIB_PATH)), "bin", "panofuse_main")
+
+
+@pytest.fixture(scope="module")
+def lib():
+    L = C.CDLL(LIB)
+    fp = C.POINTER(C.c_float)
+    ip = C.POINTER(C.c_int)
+    L.pfd_load_map.argtypes = [C.c_char_p, C.c_int, fp, C.c_longlong, ip, ip, ip]
+    L.pfd_save_png16.argtypes = [C.c_char_p, C.POINTER(C.c_uint16), C.c_int, C.c_int]
+    L.pfd_leres_layout.argtypes = [fp, fp]
+    return L
+
+
+def _load(lib, fn, is_emap=1):
+    w, h, c = C.c_int(), C.c_int(), C.c_int()
+    buf = np.zeros(1 << 22, np.float32)
+    rc = lib.pfd_load_map(str(fn).encode(), is_emap, buf.ctypes.data_as(C.POINTER(C.c_float)),
+                          buf.size, C.byref(w), C.byref(h), C.byref(c))
+    if rc != 0:
+        return None
+    n = w.value * h.value * c.value
+    return buf[:n].reshape(h.value, w.value, c.value)
+
+
+def _chunk(t, d):
+    return struct.pack(">I", len(d)) + t + d + struct.pack(">I", zlib.crc32(t + d) & 0xFFFFFFFF)
+
+
+def _paeth(a, b, c):
+    p = a + b - c
+    pa, pb, pc = abs(p - a), abs(p - b), abs(p - c)
+    return a if pa <= pb and pa <= pc else (b if pb <= pc else c)
+
+
+def _filter_row(ft, row, prev, bpp):
+    out = bytearray(len(row))
+    for i in range(len(row)):
+        a = row[i - bpp] if i >= bpp else 0
+        b = prev[i] if prev is not None else 0
+        c = prev[i - bpp] if (prev is not None and i >= bpp) else 0
+        pred = [0, a, b, (a + b) >> 1, _paeth(a, b, c)][ft]
+        out[i] = (row[i] - pred) & 0xFF
+    return bytes(out)
+
+
+def _png(path, rows, w, h, depth, ctype, plte=None, trns=None):
+    """rows: list of raw (unfiltered) scanline bytes."""
+    nc = {0: 1, 2: 3, 3: 1, 4: 2, 6: 4}[ctype]
+    bpp = max(1, nc * depth // 8)
+    raw = b""
+    prev = None
+    for y, r in enumerate(rows):
+        ft = y % 5
+        raw += bytes([ft]) + _filter_row(ft, r, prev, bpp)
+        prev = r
+    data = b"\x89PNG\r\n\x1a\n" + _chunk(b"IHDR", struct.pack(">IIBBBBB", w, h, depth, ctype,
+                                                               0, 0, 0))
+    if plte is not None:
+        data += _chunk(b"PLTE", plte)
+    if trns is not None:
+        data += _chunk(b"tRNS", trns)
+    data += _chunk(b"IDAT", zlib.compress(raw)) + _chunk(b"IEND", b"")
+    open(path, "wb").write(data)
+
+
+def test_png_gray16_and_rgb8_all_filters(lib, tmp_path):
+    rng = np.random.default_rng(1)
+    g16 = rng.integers(0, 65536, (13, 17), dtype=np.uint16)
+    _png(tmp_path / "g16.png", [g16[y].astype(">u2").tobytes() for y in range(13)], 17, 13, 16, 0)
+    got = _load(lib, tmp_path / "g16.png")
+    assert got.shape == (13, 17, 1)
+    np.testing.assert_array_equal(got[..., 0], g16.astype(np.float32) / np.float32(65535.0))
+    rgb = rng.integers(0, 256, (9, 11, 3), dtype=np.uint8)
+    _png(tmp_path / "rgb.png", [rgb[y].tobytes() for y in range(9)], 11, 9, 8, 2)
+    got = _load(lib, tmp_path / "rgb.png", 0)
+    assert got.shape == (9, 11, 3)
+    np.testing.assert_array_equal(got, rgb.astype(np.float32) / np.float32(255.0))
+    rgba16 = rng.integers(0, 65536, (5, 7, 4), dtype=np.uint16)
+    _png(tmp_path / "rgba16.png", [rgba16[y].astype(">u2").tobytes() for y in range(5)], 7, 5,
+         16, 6)
+    got = _load(lib, tmp_path / "rgba16.png")
+    np.testing.assert_array_equal(got, rgba16.astype(np.float32) / np.float32(65535.0))
+
+
+def test_png_palette_and_subbyte_gray(lib, tmp_path):
+    plte = bytes(range(30))  # 10 entries
+    idx = np.arange(24).reshape(4, 6) % 10
+    rows = []
+    for y in range(4):  # 4-bit indices, two per byte
+        r = idx[y]
+        rows.append(bytes((int(r[i]) << 4) | int(r[i + 1]) for i in range(0, 6, 2)))
+    _png(tmp_path / "pal.png", rows, 6, 4, 4, 3, plte=plte)
+    got = _load(lib, tmp_path / "pal.png")
+    assert got.shape == (4, 6, 3)
+    pal = np.frombuffer(plte, np.uint8).reshape(10, 3)
+    np.testing.assert_array_equal(got, pal[idx].astype(np.float32) / np.float32(255.0))
+    bits = np.random.default_rng(2).integers(0, 2, (3, 10))
+    rows = [np.packbits(bits[y]).tobytes() for y in range(3)]
+    _png(tmp_path / "g1.png", rows, 10, 3, 1, 0)
+    got = _load(lib, tmp_path / "g1.png")
+    np.testing.assert_array_equal(got[..., 0], bits.astype(np.float32) * 255 / np.float32(255.0))
+
+
+def _read_png16(path):
+    d = open(path, "rb").read()
+    assert d[:8] == b"\x89PNG\r\n\x1a\n"
+    pos, idat = 8, b""
+    while pos < len(d):
+        n = struct.unpack(">I", d[pos:pos + 4])[0]
+        t = d[pos + 4:pos + 8]
+        body = d[pos + 8:pos + 8 + n]
+        assert struct.unpack(">I", d[pos + 8 + n:pos + 12 + n])[0] == zlib.crc32(t + body)
+        if t == b"IHDR":
+            w, h, depth, ct = struct.unpack(">IIBB", body[:10])
+            assert depth == 16 and ct == 0
+        elif t == b"IDAT":
+            idat += body
+        pos += 12 + n
+    raw = zlib.decompress(idat)
+    rows = [raw[y * (2 * w + 1) + 1:(y + 1) * (2 * w + 1)] for y in range(h)]
+    assert all(raw[y * (2 * w + 1)] == 0 for y in range(h))
+    return np.frombuffer(b"".join(rows), ">u2").reshape(h, w).astype(np.uint16)
+
+
+def test_save16bitpng_roundtrip(lib, tmp_path):
+    a = np.random.default_rng(3).integers(0, 65536, (31, 64), dtype=np.uint16)
+    fn = str(tmp_path / "o.png").encode()
+    assert lib.pfd_save_png16(fn, a.ctypes.data_as(C.POINTER(C.c_uint16)), 64, 31) == 0
+    np.testing.assert_array_equal(_read_png16(tmp_path / "o.png"), a)
+    got = _load(lib, tmp_path / "o.png")  # and back through the loader
+    np.testing.assert_array_equal(got[..., 0], a.astype(np.float32) / np.float32(65535.0))
+
+
+@pytest.mark.parametrize("little", [True, False])
+def test_pfm_endianness_and_cap(lib, tmp_path, little):
+    """Depth.cpp:455-525: no flip, no normalisation: v<0 -> 0, then min(v/10, 10)."""
+    v = np.random.default_rng(4).normal(3, 8, (6, 9)).astype(np.float32)
+    hdr = b"Pf\n9 6\n" + (b"-1.0\n" if little else b"1.0\n")
+    open(tmp_path / "d.pfm", "wb").write(hdr + v.astype("<f4" if little else ">f4").tobytes())
+    got = _load(lib, tmp_path / "d.pfm")
+    ref = np.minimum(np.maximum(v, 0) / np.float32(10.0), np.float32(10.0))
+    np.testing.assert_array_equal(got[..., 0], ref)
+
+
+def test_pgm_and_rejections(lib, tmp_path):
+    a = np.random.default_rng(5).integers(0, 4096, (4, 5), dtype=np.uint16)
+    open(tmp_path / "a.pgm", "wb").write(b"P5\n# c\n5 4\n4095\n" + a.astype(">u2").tobytes())
+    got = _load(lib, tmp_path / "a.pgm")
+    np.testing.assert_array_equal(got[..., 0], a.astype(np.float32) / np.float32(65535.0))
+    open(tmp_path / "x.jpg", "wb").write(b"\xff\xd8\xff\xe0" + b"\0" * 64)
+    assert _load(lib, tmp_path / "x.jpg") is None
+    assert _load(lib, tmp_path / "missing.png") is None
+    open(tmp_path / "t.png", "wb").write(open(tmp_path / "a.pgm", "rb").read()[:5])
+    assert _load(lib, tmp_path / "t.png") is None
+
+
+def test_cli_leres_layout_matches_python(lib):
+    f = np.zeros(60, np.float32)
+    r = np.zeros(60, np.float32)
+    lib.pfd_leres_layout(f.ctypes.data_as(C.POINTER(C.c_float)),
+                         r.ctypes.data_as(C.POINTER(C.c_float)))
+    lay = PL.leres_layout()
+    np.testing.assert_array_equal(f.reshape(15, 4), lay.fovs)
+    np.testing.assert_array_equal(r.reshape(15, 4), lay.ranges)
+
+
+def test_cli_binary_usage():
+    import subprocess
+    out = subprocess.run([BIN], capture_output=True, text=True, timeout=60)
+    assert out.returncode == 0 and "usage" in out.stdout
+    out = subprocess.run([BIN, "0", "a"], capture_output=True, text=True, timeout=60)
+    assert out.returncode == 1 and "argc>=6" in out.stdout

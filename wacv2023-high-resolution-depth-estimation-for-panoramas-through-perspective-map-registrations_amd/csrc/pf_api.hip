@@ -63,7 +63,7 @@ struct pf_ctx {
     int wmap_pw = 0, wmap_ph = 0, npatch = 0;
     DevBuf wmap, wfxy, wpatch;
     // workspace
-    DevBuf buf[3], lnorm, coeffs, lsum_ws;
+    DevBuf buf[3], lnorm, coeffs, lsum_ws, metrics_ws;
     // stage profiling
     struct Span {
         int stage;
@@ -326,7 +326,7 @@ void pf_destroy(pf_ctx* c)
     (void)hipStreamSynchronize(c->stream);
     DevBuf* all[] = {&c->geom, &c->reg, &c->rcols, &c->rrows, &c->cams, &c->rgb_off,
                      &c->buf[0], &c->buf[1], &c->buf[2], &c->lnorm, &c->coeffs, &c->lsum_ws,
-                     &c->wmap, &c->wfxy, &c->wpatch};
+                     &c->wmap, &c->wfxy, &c->wpatch, &c->metrics_ws};
     for (DevBuf* b : all) release(*b);
     for (int l = 0; l < 4; l++) {
         release(c->lc.box[l]);
@@ -1229,6 +1229,57 @@ int pf_probe_taps(pf_ctx* c, int out_w, int out_h, float zr0, float zr1, int lev
     launch_probe_taps(c->stream, (const TileGeom*)c->geom.p, (const TileBox*)lc.box[level].p,
                       c->ntiles, (const GridCol*)lc.cols[level].p, (const GridRow*)lc.rows[level].p,
                       lc.dims[level], tap_index);
+    HIPCHK(c, hipGetLastError());
+    return PF_OK;
+}
+
+int pf_error_metrics(pf_ctx* c, const float* gt, int gw, int gh, int gc, const float* given,
+                     const uint16_t* given16, int w, int h, int given_c, int batch, float zr0,
+                     float zr1, int align_way, int cap_depth, pf_metrics* out)
+{
+    if (!c) return PF_EINVAL;
+    if (hipSetDevice(c->device) != hipSuccess) return fail(c, PF_EHIP, "hipSetDevice failed");
+    if (!gt || !out || (!given == !given16))
+        return fail(c, PF_EINVAL, "pf_error_metrics: need gt, out and exactly one of given/given16");
+    if (gw < 1 || gh < 1 || gc < 1 || w < 1 || h < 1 || (given && given_c < 1))
+        return fail(c, PF_EINVAL, "pf_error_metrics: bad shape gt %dx%dx%d given %dx%dx%d", gw,
+                    gh, gc, w, h, given_c);
+    if (batch <= 0 || batch > 65535) return fail(c, PF_EINVAL, "batch %d out of range", batch);
+    if (align_way < 0 || align_way > 2) return fail(c, PF_EINVAL, "align_way %d", align_way);
+    if ((long long)w * h >= (1ll << 31) || (long long)gw * gh * gc >= (1ll << 31))
+        return fail(c, PF_EINVAL, "pf_error_metrics: map too large");
+    // Depth.cpp:1984-1985 (int)(g_zenith_range[k] / MYPI * data_height), fp64
+    MetricsJob j;
+    j.gt = gt;
+    j.gw = gw;
+    j.gh = gh;
+    j.gc = gc;
+    j.given = given;
+    j.given16 = given16;
+    j.w = w;
+    j.h = h;
+    j.gc_given = given16 ? 1 : given_c;
+    j.batch = batch;
+    j.h0 = std::max(0, (int)((double)zr0 / PF_MYPI * h));
+    j.h1 = std::min(h - 1, (int)((double)zr1 / PF_MYPI * h));
+    if (j.h1 < j.h0) return fail(c, PF_EINVAL, "pf_error_metrics: empty zenith band");
+    j.align_way = align_way;
+    j.cap_depth = cap_depth ? 1 : 0;
+    int rc;
+    if ((rc = ensure(c, c->metrics_ws, metrics_workspace_bytes(batch)))) return rc;
+    launch_metrics(c->stream, j, c->metrics_ws.p, out);
+    HIPCHK(c, hipGetLastError());
+    return PF_OK;
+}
+
+int pf_depth_transform(pf_ctx* c, float* data, long long npix, int channels, const float* abcd)
+{
+    if (!c) return PF_EINVAL;
+    if (hipSetDevice(c->device) != hipSuccess) return fail(c, PF_EHIP, "hipSetDevice failed");
+    if (!data || !abcd || npix < 0 || channels < 1)
+        return fail(c, PF_EINVAL, "pf_depth_transform: bad arguments");
+    if (npix == 0) return PF_OK;
+    launch_d2d_map(c->stream, data, npix, channels, abcd);
     HIPCHK(c, hipGetLastError());
     return PF_OK;
 }

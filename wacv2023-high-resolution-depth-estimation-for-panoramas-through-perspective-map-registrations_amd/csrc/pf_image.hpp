@@ -1,0 +1,37 @@
+// pf_image.hpp -- file formats either side of the fusion path.
+//
+// Replaces the reference's third-party image I/O on this path:
+//   * stb_image loads (stbi_is_16_bit / stbi_load / stbi_load_16 with req_comp 0,
+//     Depth.cpp:56-100 and :304-351): PNG (bit depths 1..16, gray / gray+alpha / RGB / RGBA /
+//     palette, non-interlaced) and binary PGM/PPM, at the file's own channel count, as stb
+//     returns them (palette expanded to RGB or RGBA, sub-8-bit gray scaled to 0..255);
+//   * load_pfm (Depth.cpp:376-452): "PF"/"Pf" portable float maps, the reference's endian rule;
+//   * Save16BitPNG (Depth.cpp:27-32, cv::imwrite of a CV_16UC1 Mat) and stbi_write_png:
+//     16-bit / 8-bit PNG writers on zlib.
+// JPEG decoding (stb's baseline/progressive decoder, used for the LeReS tiles and some
+// baselines) is not provided: a JPEG input is rejected with a message naming the file.
+#pragma once
+
+#include <cstdint>
+#include <string>
+#include <vector>
+
+namespace pfio {
+
+struct Image {
+    int w = 0, h = 0, c = 0;
+    bool is16 = false;               // samples in px16 (else px8)
+    std::vector<uint8_t> px8;        // [h][w][c]
+    std::vector<uint16_t> px16;      // [h][w][c]
+};
+
+// stbi_is_16_bit: a 16-bit PNG or a PGM/PPM with maxval > 255.
+bool is_16bit(const std::string& fn);
+bool load_image(const std::string& fn, Image& out, std::string& err);
+// Returns a malloc'd [h][w][c] float buffer (free with std::free) or nullptr.
+float* load_pfm(const std::string& fn, int* w, int* h, int* c, std::string& err);
+bool save_png16(const std::string& fn, const uint16_t* data, int w, int h, std::string& err);
+bool save_png8(const std::string& fn, const uint8_t* data, int w, int h, int c,
+               std::string& err);
+
+}  // namespace pfio

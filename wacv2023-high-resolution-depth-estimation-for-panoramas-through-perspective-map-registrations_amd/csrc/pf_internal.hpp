@@ -11,6 +11,8 @@
 #include <hip/hip_runtime.h>
 #include <cstdint>
 
+#include "../../include/panofuse.h"
+
 #pragma clang fp contract(off)
 
 #define PF_MYPI 3.14159265359  // Basic.h:11
@@ -210,5 +212,19 @@ void launch_warp_rgb(hipStream_t s, const RgbCam* cams, const TileGeom* geom, in
                      long long npix_total, const long long* pix_prefix,
                      const long long* rgb_off, const uint8_t* pano, int pw, int ph,
                      long long pstride, uint8_t* tiles, long long tstride, int batch);
+
+// Accuracy metrics (pf_metrics.hip).
+struct MetricsJob {
+    const float* gt;
+    int gw, gh, gc;
+    const float* given;
+    const uint16_t* given16;
+    int w, h, gc_given, batch;
+    int h0, h1;  // compared rows, inclusive, clipped to [0, h-1]
+    int align_way, cap_depth;
+};
+size_t metrics_workspace_bytes(int batch);
+void launch_d2d_map(hipStream_t s, float* data, long long npx, int c, const float* abcd);
+void launch_metrics(hipStream_t s, const MetricsJob& j, void* ws, pf_metrics* out);
 
 }  // namespace pf

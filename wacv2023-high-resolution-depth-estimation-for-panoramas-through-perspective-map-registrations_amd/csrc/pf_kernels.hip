@@ -387,6 +387,16 @@ __global__ void __launch_bounds__(kBlock) k_apply_cubic(const TileGeom* __restri
         t[i * g.c] = cubic_map(t[i * g.c], abcd.x, abcd.y, abcd.z, abcd.w);
 }
 
+// Depth2DepthTransform of one map (PerspectiveMap::Depth2DepthTransform, Depth.cpp:245-274),
+// channel 0 of every pixel, in place.
+__global__ void __launch_bounds__(kBlock) k_d2d_map(float* __restrict__ data, long long npx,
+                                                    int c, float a, float b, float cc, float d)
+{
+    for (long long i = (long long)blockIdx.x * kBlock + threadIdx.x; i < npx;
+         i += (long long)gridDim.x * kBlock)
+        data[i * c] = cubic_map(data[i * c], a, b, cc, d);
+}
+
 // E->P RGB warp with the GL camera (a18).
 __global__ void __launch_bounds__(kBlock) k_warp_rgb(const RgbCam* __restrict__ cams,
                                                      const TileGeom* __restrict__ geom,
@@ -529,6 +539,15 @@ void launch_apply_cubic(hipStream_t s, const TileGeom* geom, int ntiles, long lo
     dim3 grid(gx, ntiles, batch);
     hipLaunchKernelGGL(k_apply_cubic, grid, dim3(kBlock), 0, s, geom, ntiles, tiles, tstride,
                        coeffs);
+}
+
+void launch_d2d_map(hipStream_t s, float* data, long long npx, int c, const float* abcd)
+{
+    unsigned gx = nblocks(npx);
+    if (gx > 4096) gx = 4096;
+    if (gx == 0) gx = 1;
+    hipLaunchKernelGGL(k_d2d_map, dim3(gx), dim3(kBlock), 0, s, data, npx, c, abcd[0], abcd[1],
+                       abcd[2], abcd[3]);
 }
 
 void launch_warp_rgb(hipStream_t s, const RgbCam* cams, const TileGeom* geom, int ntiles,

@@ -1,0 +1,48 @@
+// panofuse_main -- the reference's command line (Main.cpp:864-895) for the fusion path:
+//   panofuse_main 0 <rgb_dir> <gt_dir> <baseline_dir> <result_dir> [--tiles DIR]
+//                 [--ext auto|jpg|png] [--width W] [--device D]
+// Mode 0 = CreateDepthPanoramas (Main.cpp:331-687) minus the OpenGL tile export: the perspective
+// depth tiles are read from --tiles (default "test_images", the reference's LeReS folder) named
+// <raw>.<a0>_<a1>_<z0>_<z1>.<ext>; "auto" takes .jpg when present, else .png (MiDaS naming).
+#include "../../include/pf_depth.h"
+
+#include <hip/hip_runtime.h>
+
+#include <cstdlib>
+#include <iostream>
+#include <string>
+
+int main(int argc, char* argv[])
+{
+    if (argc < 2) {
+        std::cout << "usage: " << argv[0]
+                  << " 0 <rgb_dir> <gt_dir> <baseline_dir> <result_dir> [--tiles DIR]"
+                     " [--ext auto|jpg|png] [--width W] [--device D]"
+                  << std::endl;
+        return 0;
+    }
+    const std::string cmd(argv[1]);
+    if (cmd != "0") return 0;  // Main.cpp:889-893: other commands do nothing
+    if (argc < 6) {
+        std::cout << "[CreateDepthPanormas] error: need argc>=6" << std::endl;
+        return 1;
+    }
+    std::string tiles = "test_images", ext = "auto";
+    int width = 2048, device = 0;
+    for (int i = 6; i + 1 < argc; i += 2) {
+        const std::string k(argv[i]), v(argv[i + 1]);
+        if (k == "--tiles") tiles = v;
+        else if (k == "--ext") ext = v;
+        else if (k == "--width") width = std::atoi(v.c_str());
+        else if (k == "--device") device = std::atoi(v.c_str());
+        else {
+            std::cout << "unknown option " << k << std::endl;
+            return 2;
+        }
+    }
+    if (hipSetDevice(device) != hipSuccess) {
+        std::cout << "no HIP device " << device << std::endl;
+        return 1;
+    }
+    return pf_create_depth_panoramas(argv[2], argv[3], argv[4], argv[5], tiles, ext, width);
+}

@@ -1,0 +1,382 @@
+// Accuracy metrics of a fused panorama against ground truth:
+// ErrorData (Depth.cpp:1980-2213, the u16 result) and ErrorEmap (Depth.cpp:2215-2458, a float
+// equirectangular map such as the baseline), with the median-shift (align_way 1) and
+// least-squares (align_way 2) alignments.
+//
+// The reference sorts two std::lists per panorama for the medians and accumulates in fp32 on one
+// core.  Here every panorama of a batch is one slice of the grid:
+//   * exact medians by a three-pass radix select over order-preserving float keys (11/11/10
+//     bits): each pass histograms one digit in LDS (16 KB per block for the two streams gt and
+//     given), merges the non-empty bins into a per-panorama global histogram, and one block per
+//     (panorama, stream) scans it to fix the digit and the remaining rank.  The result is the
+//     element at index n/2 of the sorted list, bit for bit (Depth.cpp:2061-2086);
+//   * the error sums in fp64 per block, reduced in a fixed order by one block per panorama, so
+//     the result is deterministic (the reference's sequential fp32 sums carry ~1e-5 relative
+//     rounding of their own: the parity bar for the means is a tolerance, for the counts and the
+//     deltas it is exact).  align_way 2 solves its normal equations in fp64: the reference's
+//     fp32 sums drift by percents at 1M samples, so {s, o} are pinned to an fp64 solve.
+// Per pixel the work is HBM-bound byte movement (one gt read + one u16/f32 read per pass); no
+// MFMA.
+#include "pf_internal.hpp"
+
+namespace pf {
+
+namespace {
+
+constexpr int MB = 256;        // threads per block
+constexpr int MNBLK = 128;     // blocks per panorama (fixed: the fp64 reduction order is fixed)
+constexpr int HBINS = 2048;    // bins of one radix digit (11 bits)
+
+struct MArgs {
+    const float* gt;
+    int gw, gh, gc;
+    long long gstride;
+    const float* gv;          // ErrorEmap: the given map (channel 0 of gvc)
+    const uint16_t* gv16;     // ErrorData: the u16 result
+    int w, h, gvc;
+    long long vstride;
+    int h0, h1;               // rows [h0, h1] inclusive, already clipped to [0, h-1]
+    float rx, ry;             // (float)gt.width / (float)w, (float)gt.height / (float)h
+    int cap;
+    float depth_max;
+    int abs_median;           // ErrorEmap skips abs(val0) < 1e-4 in its median pass
+};
+
+// Depth.cpp:2033-2053 (ErrorData) / :2248-2268 (ErrorEmap): band row, nearest gt pixel, skip
+// invalid gt, cap at 10 m.
+__device__ __forceinline__ bool eval_px(const MArgs& a, int b, int x, int y, bool abs_skip,
+                                        float& v0, float& v1)
+{
+    int X = (int)((float)x * a.rx);
+    int Y = (int)((float)y * a.ry);
+    X = X < a.gw - 1 ? X : a.gw - 1;
+    Y = Y < a.gh - 1 ? Y : a.gh - 1;
+    v0 = a.gt[(long long)b * a.gstride + ((long long)Y * a.gw + X) * a.gc];
+    if (a.gv16)
+        v1 = (float)a.gv16[(long long)b * a.vstride + (long long)y * a.w + x] / 65535.0f;
+    else
+        v1 = a.gv[(long long)b * a.vstride + ((long long)y * a.w + x) * a.gvc];
+    const float t = abs_skip ? fabsf(v0) : v0;
+    if ((double)t < 1e-4) return false;
+    if (a.cap) {
+        v0 = v0 < a.depth_max ? v0 : a.depth_max;  // MIN2(val, depth_max)
+        v1 = v1 < a.depth_max ? v1 : a.depth_max;
+    }
+    return true;
+}
+
+__device__ __forceinline__ uint32_t fkey(float v)
+{
+    uint32_t u = __float_as_uint(v);
+    return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
+}
+
+__device__ __forceinline__ float fkey_inv(uint32_t k)
+{
+    return __uint_as_float((k & 0x80000000u) ? (k & 0x7FFFFFFFu) : ~k);
+}
+
+// Per (panorama, stream): prefix digits so far, remaining rank, element count, final key.
+struct SelState {
+    uint32_t prefix, rank, n, key;
+};
+
+__device__ __forceinline__ int digit_shift(int pass) { return pass == 0 ? 21 : (pass == 1 ? 10 : 0); }
+__device__ __forceinline__ uint32_t digit_mask(int pass) { return pass == 2 ? 0x3FFu : 0x7FFu; }
+
+__global__ __launch_bounds__(MB) void k_med_hist(MArgs a, int pass, const SelState* st,
+                                                 uint32_t* hist)
+{
+    __shared__ uint32_t h[2][HBINS];
+    const int b = blockIdx.y;
+    for (int i = threadIdx.x; i < 2 * HBINS; i += MB) (&h[0][0])[i] = 0;
+    __syncthreads();
+    const int sh = digit_shift(pass);
+    const uint32_t msk = digit_mask(pass);
+    uint32_t pre[2] = {0, 0};
+    if (pass > 0) {
+        pre[0] = st[b * 2 + 0].prefix;
+        pre[1] = st[b * 2 + 1].prefix;
+    }
+    const int psh = pass == 1 ? 21 : 10;
+    const long long npx = (long long)(a.h1 - a.h0 + 1) * a.w;
+    for (long long i = (long long)blockIdx.x * MB + threadIdx.x; i < npx;
+         i += (long long)gridDim.x * MB) {
+        const int y = a.h0 + (int)(i / a.w), x = (int)(i % a.w);
+        float v0, v1;
+        if (!eval_px(a, b, x, y, a.abs_median != 0, v0, v1)) continue;
+        const uint32_t k0 = fkey(v0), k1 = fkey(v1);
+        if (pass == 0 || (k0 >> psh) == pre[0]) atomicAdd(&h[0][(k0 >> sh) & msk], 1u);
+        if (pass == 0 || (k1 >> psh) == pre[1]) atomicAdd(&h[1][(k1 >> sh) & msk], 1u);
+    }
+    __syncthreads();
+    uint32_t* g = hist + (long long)b * 2 * HBINS;
+    for (int i = threadIdx.x; i < 2 * HBINS; i += MB) {
+        const uint32_t v = (&h[0][0])[i];
+        if (v) atomicAdd(&g[i], v);
+    }
+}
+
+// One block per (panorama, stream): find the bin holding the element of rank `rank`.
+__global__ __launch_bounds__(MB) void k_med_scan(int pass, const uint32_t* hist, SelState* st)
+{
+    constexpr int PER = HBINS / MB;  // 8 bins per thread
+    __shared__ uint32_t part[MB];
+    const int s = blockIdx.x;  // b * 2 + stream
+    const uint32_t* g = hist + (long long)s * HBINS;
+    const int nb = pass == 2 ? 1024 : HBINS;
+    uint32_t loc[PER], sum = 0;
+    for (int j = 0; j < PER; ++j) {
+        const int bin = threadIdx.x * PER + j;
+        loc[j] = bin < nb ? g[bin] : 0u;
+        sum += loc[j];
+    }
+    part[threadIdx.x] = sum;
+    __syncthreads();
+    // inclusive Hillis-Steele scan over 256 partial sums
+    for (int off = 1; off < MB; off <<= 1) {
+        const uint32_t v = threadIdx.x >= off ? part[threadIdx.x - off] : 0u;
+        __syncthreads();
+        part[threadIdx.x] += v;
+        __syncthreads();
+    }
+    const uint32_t total = part[MB - 1];
+    SelState S = st[s];
+    if (pass == 0) {
+        S.n = total;
+        S.rank = total / 2;  // Depth.cpp:2065 count == size()/2
+        S.prefix = 0;
+    }
+    if (S.n == 0) {  // empty list: the reference's median stays 0
+        if (threadIdx.x == 0) {
+            S.key = fkey(0.0f);
+            st[s] = S;
+        }
+        return;
+    }
+    const uint32_t excl = threadIdx.x ? part[threadIdx.x - 1] : 0u;
+    if (S.rank >= excl && S.rank < part[threadIdx.x]) {
+        uint32_t c = excl;
+        for (int j = 0; j < PER; ++j) {
+            if (S.rank < c + loc[j]) {
+                const uint32_t bin = threadIdx.x * PER + j;
+                S.rank -= c;
+                S.prefix = pass == 0 ? bin : ((S.prefix << (pass == 2 ? 10 : 11)) | bin);
+                if (pass == 2) S.key = S.prefix;
+                st[s] = S;
+                break;
+            }
+            c += loc[j];
+        }
+    }
+}
+
+__device__ __forceinline__ double wave_sum(double v)
+{
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+    return v;
+}
+
+// Depth.cpp:2096-2134 / :2315-2352: least-squares sums (fp64 accumulation of the fp32 terms).
+constexpr int NLS = 5;
+__global__ __launch_bounds__(MB) void k_ls_sums(MArgs a, double* part)
+{
+    const int b = blockIdx.y;
+    double s[NLS] = {0, 0, 0, 0, 0};
+    const long long npx = (long long)(a.h1 - a.h0 + 1) * a.w;
+    for (long long i = (long long)blockIdx.x * MB + threadIdx.x; i < npx;
+         i += (long long)gridDim.x * MB) {
+        const int y = a.h0 + (int)(i / a.w), x = (int)(i % a.w);
+        float v0, v1;
+        if (!eval_px(a, b, x, y, false, v0, v1)) continue;
+        s[0] += (double)(v1 * v1);
+        s[1] += (double)v1;
+        s[2] += 1.0;
+        s[3] += (double)(v0 * v1);
+        s[4] += (double)v0;
+    }
+    __shared__ double red[MB / 64][NLS];
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    for (int k = 0; k < NLS; ++k) {
+        const double v = wave_sum(s[k]);
+        if (lane == 0) red[wv][k] = v;
+    }
+    __syncthreads();
+    if (threadIdx.x < NLS) {
+        double v = 0;
+        for (int w = 0; w < MB / 64; ++w) v += red[w][threadIdx.x];
+        part[((long long)b * gridDim.x + blockIdx.x) * NLS + threadIdx.x] = v;
+    }
+}
+
+// Per panorama: the alignment parameters (median shift or {s, o}) in the reference's fp32 forms.
+struct Align {
+    float shift, s, o, gt_med, gv_med;
+};
+
+__global__ __launch_bounds__(64) void k_align(int align_way, const SelState* st,
+                                              const double* lspart, int nblk, Align* al)
+{
+    const int b = blockIdx.x;
+    if (threadIdx.x != 0) return;
+    Align A{1.0f, 0.0f, 0.0f, 0.0f, 0.0f};
+    if (align_way == 1) {
+        A.gt_med = fkey_inv(st[b * 2 + 0].key);
+        A.gv_med = fkey_inv(st[b * 2 + 1].key);
+        A.shift = A.gt_med / A.gv_med;  // Depth.cpp:2088
+    } else if (align_way == 2) {
+        double acc[NLS] = {0, 0, 0, 0, 0};
+        for (int i = 0; i < nblk; ++i)
+            for (int k = 0; k < NLS; ++k) acc[k] += lspart[((long long)b * nblk + i) * NLS + k];
+        // Depth.cpp:2121-2126 in fp64 (the reference's fp32 forms cancel badly at ~1M samples),
+        // rounded to the reference's float {s, o}
+        const double a00 = acc[0], a01 = acc[1], a11 = acc[2], b0 = acc[3], b1 = acc[4];
+        const double det = a00 * a11 - a01 * a01;
+        A.s = (float)((a11 * b0 - a01 * b1) / det);
+        A.o = (float)((-a01 * b0 + a00 * b1) / det);
+    }
+    al[b] = A;
+}
+
+// Depth.cpp:2140-2203 / :2358-2420: the error terms.
+constexpr int NSUM = 8;  // mse, mae, mre, mselog, n, nlog, fail1, fail2 (fail3 in slot 8)
+__global__ __launch_bounds__(MB) void k_err_sums(MArgs a, int align_way, const Align* al,
+                                                 double* part)
+{
+    const int b = blockIdx.y;
+    const Align A = al[b];
+    double s[NSUM + 1] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
+    const long long npx = (long long)(a.h1 - a.h0 + 1) * a.w;
+    for (long long i = (long long)blockIdx.x * MB + threadIdx.x; i < npx;
+         i += (long long)gridDim.x * MB) {
+        const int y = a.h0 + (int)(i / a.w), x = (int)(i % a.w);
+        float v0, v1;
+        if (!eval_px(a, b, x, y, false, v0, v1)) continue;
+        if (align_way == 1)
+            v1 *= A.shift;
+        else if (align_way == 2)
+            v1 = v1 * A.s + A.o;
+        const float d = v0 - v1;
+        s[0] += (double)d * (double)d;          // pow(val0 - val1, 2)
+        s[1] += (double)fabsf(d);
+        s[2] += (double)(fabsf(d) / v0);
+        if ((double)v0 > 1e-4 && (double)v1 > 1e-4) {
+            const float lg = log10f(v0) - log10f(v1);
+            s[3] += (double)lg * (double)lg;
+            s[5] += 1.0;
+        }
+        if (v0 > 0 && v1 > 0) {
+            const float r01 = v0 / v1, r10 = v1 / v0;
+            const float rm = r01 > r10 ? r01 : r10;  // MAX2
+            if ((double)rm >= 1.25) s[6] += 1.0;
+            if ((double)rm >= 1.5625) s[7] += 1.0;
+            if ((double)rm >= 1.953125) s[8] += 1.0;
+        }
+        s[4] += 1.0;
+    }
+    __shared__ double red[MB / 64][NSUM + 1];
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    for (int k = 0; k <= NSUM; ++k) {
+        const double v = wave_sum(s[k]);
+        if (lane == 0) red[wv][k] = v;
+    }
+    __syncthreads();
+    if (threadIdx.x <= NSUM) {
+        double v = 0;
+        for (int w = 0; w < MB / 64; ++w) v += red[w][threadIdx.x];
+        part[((long long)b * gridDim.x + blockIdx.x) * (NSUM + 1) + threadIdx.x] = v;
+    }
+}
+
+__global__ __launch_bounds__(64) void k_err_final(const double* part, int nblk, const Align* al,
+                                                  pf_metrics* out)
+{
+    const int b = blockIdx.x;
+    if (threadIdx.x != 0) return;
+    double acc[NSUM + 1] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
+    for (int i = 0; i < nblk; ++i)
+        for (int k = 0; k <= NSUM; ++k) acc[k] += part[((long long)b * nblk + i) * (NSUM + 1) + k];
+    const int n = (int)acc[4], nlog = (int)acc[5];
+    const int f1 = (int)acc[6], f2 = (int)acc[7], f3 = (int)acc[8];
+    pf_metrics m;
+    m.mse = (float)acc[0] / (float)n;  // Depth.cpp:2206-2212
+    m.mae = (float)acc[1] / (float)n;
+    m.mre = (float)acc[2] / (float)n;
+    m.mselog = (float)acc[3] / (float)nlog;
+    m.delta1 = (float)(n - f1) / (float)n;
+    m.delta2 = (float)(n - f2) / (float)n;
+    m.delta3 = (float)(n - f3) / (float)n;
+    const Align A = al[b];
+    m.median_shift = A.shift;
+    m.ls_s = A.s;
+    m.ls_o = A.o;
+    m.gt_median = A.gt_med;
+    m.given_median = A.gv_med;
+    m.n = n;
+    m.nlog = nlog;
+    m.reserved[0] = m.reserved[1] = 0;
+    out[b] = m;
+}
+
+}  // namespace
+
+size_t metrics_workspace_bytes(int batch)
+{
+    const size_t hist = sizeof(uint32_t) * 2 * HBINS * batch;
+    const size_t st = sizeof(SelState) * 2 * batch;
+    const size_t part = sizeof(double) * (NSUM + 1) * MNBLK * batch;
+    const size_t al = sizeof(Align) * batch;
+    return ((hist + 255) & ~(size_t)255) + ((st + 255) & ~(size_t)255) +
+           ((part + 255) & ~(size_t)255) + al + 256;
+}
+
+void launch_metrics(hipStream_t s, const MetricsJob& j, void* ws, pf_metrics* out)
+{
+    MArgs a;
+    a.gt = j.gt;
+    a.gw = j.gw;
+    a.gh = j.gh;
+    a.gc = j.gc;
+    a.gstride = (long long)j.gw * j.gh * j.gc;
+    a.gv = j.given;
+    a.gv16 = j.given16;
+    a.w = j.w;
+    a.h = j.h;
+    a.gvc = j.given16 ? 1 : j.gc_given;
+    a.vstride = (long long)j.w * j.h * a.gvc;
+    a.h0 = j.h0;
+    a.h1 = j.h1;
+    a.rx = (float)j.gw / (float)j.w;
+    a.ry = (float)j.gh / (float)j.h;
+    a.cap = j.cap_depth;
+    const float to_matterport = 65535.0f / 4000.0f;  // Depth.cpp:1999-2000
+    a.depth_max = 10.0f / to_matterport;
+    a.abs_median = j.given16 ? 0 : 1;
+
+    char* p = (char*)ws;
+    auto carve = [&](size_t bytes) {
+        char* r = p;
+        p += (bytes + 255) & ~(size_t)255;
+        return (void*)r;
+    };
+    uint32_t* hist = (uint32_t*)carve(sizeof(uint32_t) * 2 * HBINS * j.batch);
+    SelState* st = (SelState*)carve(sizeof(SelState) * 2 * j.batch);
+    double* part = (double*)carve(sizeof(double) * (NSUM + 1) * MNBLK * j.batch);
+    Align* al = (Align*)carve(sizeof(Align) * j.batch);
+
+    const dim3 grid(MNBLK, j.batch);
+    if (j.align_way == 1) {
+        for (int pass = 0; pass < 3; ++pass) {
+            (void)hipMemsetAsync(hist, 0, sizeof(uint32_t) * 2 * HBINS * j.batch, s);
+            hipLaunchKernelGGL(k_med_hist, grid, dim3(MB), 0, s, a, pass, st, hist);
+            hipLaunchKernelGGL(k_med_scan, dim3(2 * j.batch), dim3(MB), 0, s, pass, hist, st);
+        }
+    } else if (j.align_way == 2) {
+        hipLaunchKernelGGL(k_ls_sums, grid, dim3(MB), 0, s, a, part);
+    }
+    hipLaunchKernelGGL(k_align, dim3(j.batch), dim3(64), 0, s, j.align_way, st, part, MNBLK, al);
+    hipLaunchKernelGGL(k_err_sums, grid, dim3(MB), 0, s, a, j.align_way, al, part);
+    hipLaunchKernelGGL(k_err_final, dim3(j.batch), dim3(64), 0, s, part, MNBLK, al, out);
+}
+
+}  // namespace pf

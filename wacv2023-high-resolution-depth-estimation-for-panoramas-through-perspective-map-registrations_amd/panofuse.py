@@ -23,7 +23,8 @@ EXPORTS = [
     "pf_create", "pf_destroy", "pf_last_error", "pf_set_stream", "pf_synchronize",
     "pf_version", "pf_set_tiles", "pf_register", "pf_fuse", "pf_merge", "pf_warp_depth",
     "pf_warp_rgb", "pf_level_info", "pf_fuse_partial", "pf_fuse_seed", "pf_fuse_finish_level",
-    "pf_probe_taps", "pf_profile_enable", "pf_profile_read",
+    "pf_probe_taps", "pf_profile_enable", "pf_profile_read", "pf_error_metrics",
+    "pf_depth_transform",
 ]
 
 STAGES = ["warp", "register", "seed", "targets", "jacobi", "quantize"]
@@ -78,6 +79,9 @@ def load():
     L.pf_fuse_seed.argtypes = [vp, vp, ip, ip, ip, vp, ip, ip, fp, fp, ip, vp]
     L.pf_fuse_finish_level.argtypes = [vp, vp, vp, ip, ip, fp, fp, ip, vp, vp]
     L.pf_probe_taps.argtypes = [vp, ip, ip, fp, fp, ip, vp]
+    L.pf_depth_transform.argtypes = [vp, vp, C.c_longlong, ip, vp]
+    L.pf_error_metrics.argtypes = [vp, vp, ip, ip, ip, vp, vp, ip, ip, ip, ip, fp, fp, ip, ip,
+                                   vp]
     L.pf_profile_enable.argtypes = [vp, ip]
     L.pf_profile_read.argtypes = [vp, C.POINTER(C.c_double), C.POINTER(C.c_double),
                                   C.POINTER(C.c_longlong)]
@@ -113,6 +117,11 @@ def _emap_dims(emap):
     if emap.dim() == 3:
         return emap.shape[2], emap.shape[1], 1
     return emap.shape[2], emap.shape[1], emap.shape[3]
+
+
+# pf_metrics field order (include/panofuse.h)
+METRIC_KEYS = ("mse", "mae", "mre", "mselog", "delta1", "delta2", "delta3", "median_shift",
+               "ls_s", "ls_o", "gt_median", "given_median")
 
 
 class Fuser:
@@ -196,6 +205,34 @@ class Fuser:
     def warp_rgb(self, pano, tiles):
         B, ph, pw, _ = pano.shape
         self._check(self.L.pf_warp_rgb(self.h, _ptr(pano), pw, ph, B, _ptr(tiles)))
+
+    def error_metrics(self, gt, given, zr, align_way=1, cap_depth=True):
+        """ErrorData (given: int16/uint16 [B,h,w] result bits) or ErrorEmap (given: float32
+        [B,h,w] or [B,h,w,c]) against gt float32 [B,gh,gw] or [B,gh,gw,gc]
+        (Depth.cpp:1980-2458).  Returns a list (one per panorama) of dicts of METRIC_KEYS +
+        n, nlog."""
+        import torch
+        gw, gh, gc = _emap_dims(gt)
+        B, h, w = given.shape[:3]
+        out = torch.zeros((B, 16), dtype=torch.int32, device=gt.device)
+        if given.dtype in (torch.int16, torch.uint16):
+            self._check(self.L.pf_error_metrics(self.h, _ptr(gt), gw, gh, gc, None, _ptr(given),
+                                                w, h, 1, B, float(zr[0]), float(zr[1]),
+                                                int(align_way), int(cap_depth), _ptr(out)))
+        else:
+            gvc = given.shape[3] if given.dim() == 4 else 1
+            self._check(self.L.pf_error_metrics(self.h, _ptr(gt), gw, gh, gc, _ptr(given), None,
+                                                w, h, gvc, B, float(zr[0]), float(zr[1]),
+                                                int(align_way), int(cap_depth), _ptr(out)))
+        self.synchronize()
+        o = out.cpu()
+        f = o[:, :12].view(torch.float32)
+        res = []
+        for b in range(B):
+            d = {k: float(f[b, i]) for i, k in enumerate(METRIC_KEYS)}
+            d["n"], d["nlog"] = int(o[b, 12]), int(o[b, 13])
+            res.append(d)
+        return res
 
     def probe_taps(self, out_w, zr, level):
         import torch
