@@ -231,6 +231,13 @@ def main():
     for _ in range(args.prof_steps):
         step()
     prof = fz.profile_read()
+    # Accuracy metrics (ErrorData of each result against its ground truth, median alignment,
+    # Depth.cpp:1980-2213): not part of the step (the reference computes them only when a
+    # ground-truth file is given), timed the same way on the same batch.
+    mres = torch.zeros((B, 16), dtype=torch.int32, device=dev)
+    for _ in range(max(1, args.prof_steps)):
+        fz.error_metrics_async(gt, out, zr, mres, 1, True)
+    prof["metrics"] = fz.profile_read()["metrics"]
     fz.profile(False)
     nprof = max(1, args.prof_steps)
     if world > 1:
@@ -295,6 +302,14 @@ def main():
                               "flop_per_update": 14,
                               "updates_per_step": jbytes / 12.0 / nprof},
             "stages": stages,
+            # metrics stage (outside the timed step): algorithmic bytes = one read of the
+            # compared band of gt (4 B) and result (2 B) per pixel; the kernels make 4 passes
+            "roofline_metrics": {"bound": "hbm", "achieved": stages["metrics"]["GBps"],
+                                 "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                                 "frac": stages["metrics"]["GBps"] / HBM_PEAK_GBS,
+                                 "kernel": "pf_error_metrics (k_med_hist x3, k_med_scan x3, "
+                                           "k_err_sums, k_align, k_err_final)",
+                                 "ms_per_batch": stages["metrics"]["ms_per_step"]},
             "nonzero_px_pano0": nz,
         }
         if not args.no_cpu_baseline:

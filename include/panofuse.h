@@ -124,7 +124,8 @@ int pf_fuse_finish_level(pf_ctx* ctx, const float* lsum, const float* cnt, int o
 #define PF_STAGE_TARGETS 3
 #define PF_STAGE_JACOBI 4
 #define PF_STAGE_QUANTIZE 5
-#define PF_NSTAGES 6
+#define PF_STAGE_METRICS 6
+#define PF_NSTAGES 7
 int pf_profile_enable(pf_ctx* ctx, int on);
 int pf_profile_read(pf_ctx* ctx, double* ms, double* bytes, long long* launches);
 

@@ -189,3 +189,21 @@ def test_metrics_edge_cases(fuser):
     got = fuser.error_metrics(_dev(gt3), _dev(gv), ZR, 1, True)
     for b in range(2):
         _check(got[b], O.error_metrics(gt3[b], gv[b], ZR, 1, True), 1)
+
+
+def test_metrics_batch16_and_fast_float_path(fuser):
+    """16 panoramas of C2 geometry (uniform noise: every bin populated), each panorama's
+    medians and counts exact; and the vectorised ErrorEmap path (float result of the gt's own
+    size)."""
+    rng = np.random.default_rng(11)
+    B = 16
+    gt = rng.uniform(0, 0.5, (B, 1024, 2048)).astype(np.float32)
+    gt[:, :, :100] = 0
+    res = rng.integers(0, 30000, (B, 1024, 2048), dtype=np.uint16)
+    got = fuser.error_metrics(_dev(gt), _dev(res.view(np.int16)), ZR, 1, True)
+    for b in (0, 13, 14, 15):
+        _check(got[b], O.error_metrics(gt[b], res[b], ZR, 1, True), 1)
+    gv = (gt[:2] * 1.1 + 0.01).astype(np.float32)
+    got = fuser.error_metrics(_dev(gt[:2]), _dev(gv), ZR, 1, True)
+    for b in range(2):
+        _check(got[b], O.error_metrics(gt[b], gv[b], ZR, 1, True), 1)

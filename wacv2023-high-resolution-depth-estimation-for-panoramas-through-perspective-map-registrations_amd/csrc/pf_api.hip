@@ -1267,6 +1267,13 @@ int pf_error_metrics(pf_ctx* c, const float* gt, int gw, int gh, int gc, const f
     j.cap_depth = cap_depth ? 1 : 0;
     int rc;
     if ((rc = ensure(c, c->metrics_ws, metrics_workspace_bytes(batch)))) return rc;
+    // algorithmic bytes: one read of the compared band of gt (4 B, channel 0) and of the
+    // result (2 B u16 / 4 B f32); the kernels make 4 passes (3 radix digits + the sums) for
+    // align_way 1, 2 for align_way 2, 1 otherwise
+    const double band = (double)(j.h1 - j.h0 + 1) * w;
+    const int passes = align_way == 1 ? 4 : (align_way == 2 ? 2 : 1);
+    StageTimer t(c, PF_STAGE_METRICS, batch * band * (4.0 + (given16 ? 2.0 : 4.0)),
+                 align_way == 1 ? 9 : passes + 2);
     launch_metrics(c->stream, j, c->metrics_ws.p, out);
     HIPCHK(c, hipGetLastError());
     return PF_OK;

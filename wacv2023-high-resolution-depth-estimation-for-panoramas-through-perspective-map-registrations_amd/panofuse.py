@@ -27,7 +27,7 @@ EXPORTS = [
     "pf_depth_transform",
 ]
 
-STAGES = ["warp", "register", "seed", "targets", "jacobi", "quantize"]
+STAGES = ["warp", "register", "seed", "targets", "jacobi", "quantize", "metrics"]
 
 
 class PanofuseError(RuntimeError):
@@ -206,15 +206,11 @@ class Fuser:
         B, ph, pw, _ = pano.shape
         self._check(self.L.pf_warp_rgb(self.h, _ptr(pano), pw, ph, B, _ptr(tiles)))
 
-    def error_metrics(self, gt, given, zr, align_way=1, cap_depth=True):
-        """ErrorData (given: int16/uint16 [B,h,w] result bits) or ErrorEmap (given: float32
-        [B,h,w] or [B,h,w,c]) against gt float32 [B,gh,gw] or [B,gh,gw,gc]
-        (Depth.cpp:1980-2458).  Returns a list (one per panorama) of dicts of METRIC_KEYS +
-        n, nlog."""
+    def error_metrics_async(self, gt, given, zr, out, align_way=1, cap_depth=True):
+        """pf_error_metrics into out (int32 [B,16] device tensor = B pf_metrics), no sync."""
         import torch
         gw, gh, gc = _emap_dims(gt)
         B, h, w = given.shape[:3]
-        out = torch.zeros((B, 16), dtype=torch.int32, device=gt.device)
         if given.dtype in (torch.int16, torch.uint16):
             self._check(self.L.pf_error_metrics(self.h, _ptr(gt), gw, gh, gc, None, _ptr(given),
                                                 w, h, 1, B, float(zr[0]), float(zr[1]),
@@ -224,6 +220,16 @@ class Fuser:
             self._check(self.L.pf_error_metrics(self.h, _ptr(gt), gw, gh, gc, _ptr(given), None,
                                                 w, h, gvc, B, float(zr[0]), float(zr[1]),
                                                 int(align_way), int(cap_depth), _ptr(out)))
+
+    def error_metrics(self, gt, given, zr, align_way=1, cap_depth=True):
+        """ErrorData (given: int16/uint16 [B,h,w] result bits) or ErrorEmap (given: float32
+        [B,h,w] or [B,h,w,c]) against gt float32 [B,gh,gw] or [B,gh,gw,gc]
+        (Depth.cpp:1980-2458).  Returns a list (one per panorama) of dicts of METRIC_KEYS +
+        n, nlog."""
+        import torch
+        B = given.shape[0]
+        out = torch.zeros((B, 16), dtype=torch.int32, device=gt.device)
+        self.error_metrics_async(gt, given, zr, out, align_way, cap_depth)
         self.synchronize()
         o = out.cpu()
         f = o[:, :12].view(torch.float32)
