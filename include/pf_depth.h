@@ -148,6 +148,11 @@ int pf_create_depth_panoramas(const std::string& rgb_folder, const std::string& 
                               const std::string& baseline_folder,
                               const std::string& result_folder, const std::string& tile_dir,
                               const std::string& tile_ext, int out_width);
+/* The RGB tile export of mode 0 (Main.cpp:399-430 + SaveCubeMap :242-326): every panorama of
+ * rgb_folder (8/16-bit PNG, PGM/PPM) warped on the GPU (pf_warp_rgb) into the 15 LeReS tiles
+ * of 1024 x round(1024/aspect) px, written as <tile_dir>/<raw>.<a0>_<a1>_<z0>_<z1>.png (rows
+ * top-first, like the reference's flipped JPEG write; PNG instead of JPEG q=100). */
+int pf_export_rgb_tiles(const std::string& rgb_folder, const std::string& tile_dir);
 /* The active LeReS layout (Main.cpp:788-843): 15 FOVs and ranges. */
 void pf_leres_layout(std::vector<Vec4f>& fovs, std::vector<Vec4f>& ranges);
 

@@ -121,3 +121,59 @@ def test_mode0_cli_end_to_end(tmp_path):
     # second run: every output exists -> skipped (Main.cpp:552-561)
     r = subprocess.run(cmd, capture_output=True, text=True, timeout=300)
     assert r.returncode == 0 and r.stdout.count("skip!") == 2
+
+
+def _png8_read(path):
+    d = open(path, "rb").read()
+    pos, idat = 8, b""
+    while pos < len(d):
+        n = struct.unpack(">I", d[pos:pos + 4])[0]
+        t, body = d[pos + 4:pos + 8], d[pos + 8:pos + 8 + n]
+        if t == b"IHDR":
+            w, h, depth, ct = struct.unpack(">IIBB", body[:10])
+            assert depth == 8 and ct == 2
+        elif t == b"IDAT":
+            idat += body
+        pos += 12 + n
+    raw = zlib.decompress(idat)
+    return np.frombuffer(b"".join(raw[y * (3 * w + 1) + 1:(y + 1) * (3 * w + 1)]
+                                  for y in range(h)), np.uint8).reshape(h, w, 3)
+
+
+def _png8_write_rgb(path, a):
+    h, w, _ = a.shape
+    raw = b"".join(b"\0" + a[y].tobytes() for y in range(h))
+
+    def chunk(t, d):
+        return struct.pack(">I", len(d)) + t + d + struct.pack(">I", zlib.crc32(t + d))
+    open(path, "wb").write(b"\x89PNG\r\n\x1a\n" +
+                           chunk(b"IHDR", struct.pack(">IIBBBBB", w, h, 8, 2, 0, 0, 0)) +
+                           chunk(b"IDAT", zlib.compress(raw, 1)) + chunk(b"IEND", b""))
+
+
+def test_export_rgb_tiles(tmp_path):
+    """`panofuse_main export`: the tile render of mode 0 (SaveCubeMap, Main.cpp:242-326) for
+    the LeReS layout at 1024 x 988 px, against the oracle's restatement of the GL camera within
+    1 LSB (the a18 bar of test_gpu_parity.py); OpenGL rasterisation parity is unpinned."""
+    (tmp_path / "rgb").mkdir()
+    h, w = 512, 1024
+    rs = np.random.RandomState(9)
+    yy, xx = np.mgrid[0:h, 0:w]
+    pano = np.stack([(xx * 255 // (w - 1)), (yy * 255 // (h - 1)),
+                     rs.randint(0, 256, size=(h, w))], -1).astype(np.uint8)
+    _png8_write_rgb(tmp_path / "rgb" / "room7.png", pano)
+    r = subprocess.run([BIN, "export", str(tmp_path / "rgb"), str(tmp_path / "tiles")],
+                       capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stdout + r.stderr
+    lay = PL.leres_layout(1024, 988)
+    tiles_o, _ = O.make_tiles(lay)
+    ref = O.warp_rgb(pano, tiles_o)
+    off = 0
+    for t in range(lay.ntiles):
+        f = [_cround(float(v) / MYPI * 180.0) for v in lay.fovs[t]]
+        got = _png8_read(tmp_path / "tiles" / f"room7.{f[0]}_{f[1]}_{f[2]}_{f[3]}.png")
+        assert got.shape == (988, 1024, 3)
+        n = 988 * 1024 * 3
+        d = np.abs(got.reshape(-1).astype(np.int32) - ref[off:off + n].astype(np.int32))
+        off += n
+        assert d.max() <= 1 and (d > 0).mean() < 1e-3, (t, d.max(), (d > 0).mean())

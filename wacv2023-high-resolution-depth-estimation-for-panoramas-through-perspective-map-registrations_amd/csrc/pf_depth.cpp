@@ -684,6 +684,93 @@ int pf_create_depth_panoramas(const std::string& rgb_folder, const std::string& 
     return 0;
 }
 
+// ---- RGB tile export (Main.cpp:242-326 SaveCubeMap, called for every panorama by
+// CreateDepthPanoramas, Main.cpp:399-430) ----
+// Tile size as SaveCubeMap sizes its viewport: width 1024, height round(1024 / aspect) with
+// aspect = tan(fovx/2) / tan(fovy/2) (the window-size clamps of a small screen do not apply).
+static void rgb_tile_size(const Vec4f& f, int& w, int& h)
+{
+    const float fovx = (float)((f[1] - f[0]) / PF_MYPI_D * 180.0);
+    const float fovy = (float)((f[3] - f[2]) / PF_MYPI_D * 180.0);
+    const float aspect = (float)(std::tan(PF_D2R(fovx) / 2) / std::tan(PF_D2R(fovy) / 2));
+    w = 1024;
+    h = (int)std::round((float)w / aspect);
+}
+
+int pf_export_rgb_tiles(const std::string& rgb_folder, const std::string& tile_dir)
+{
+    namespace fs = std::filesystem;
+    std::vector<Vec4f> fovs, ranges;
+    pf_leres_layout(fovs, ranges);
+    pf_ctx* c = facade_ctx();
+    if (!c) return 1;
+    const int n = (int)fovs.size();
+    std::vector<pf_window> fw(n), rw(n);
+    std::vector<int> tw(n), th(n);
+    size_t total = 0;
+    for (int i = 0; i < n; ++i) {
+        fw[i] = pf_window{fovs[i][0], fovs[i][1], fovs[i][2], fovs[i][3]};
+        rw[i] = pf_window{ranges[i][0], ranges[i][1], ranges[i][2], ranges[i][3]};
+        rgb_tile_size(fovs[i], tw[i], th[i]);
+        total += (size_t)tw[i] * th[i] * 3;
+    }
+    if (!pf_ok(c, pf_set_tiles(c, fw.data(), rw.data(), n, tw.data(), th.data(), 1, 1),
+               "pf_set_tiles"))
+        return 1;
+    std::vector<std::string> rgb;
+    std::error_code ec;
+    for (const auto& e : fs::directory_iterator(rgb_folder, ec))
+        if (!e.is_directory()) rgb.push_back(e.path().string());
+    if (ec) {
+        std::cout << "[SaveCubeMap] cannot list " << rgb_folder << std::endl;
+        return 1;
+    }
+    std::sort(rgb.begin(), rgb.end());
+    fs::create_directories(tile_dir, ec);
+    std::vector<uint8_t> tiles(total);
+    for (const std::string& fn : rgb) {
+        pfio::Image im;
+        std::string err;
+        if (!pfio::load_image(fn, im, err)) {
+            std::cout << "[SaveCubeMap] " << err << std::endl;
+            return 1;
+        }
+        // the GL texture is RGB8: gray replicated, alpha dropped, 16-bit reduced to the top byte
+        std::vector<uint8_t> pano((size_t)im.w * im.h * 3);
+        for (size_t p = 0; p < (size_t)im.w * im.h; ++p)
+            for (int k = 0; k < 3; ++k) {
+                const int ch = im.c >= 3 ? k : 0;
+                pano[p * 3 + k] = im.is16 ? (uint8_t)(im.px16[p * im.c + ch] >> 8)
+                                          : im.px8[p * im.c + ch];
+            }
+        DevMem dp(pano.size()), dt(total);
+        if (!upload(dp, pano.data(), pano.size()) || !dt.ok) return 1;
+        if (!pf_ok(c, pf_warp_rgb(c, dp.as<uint8_t>(), im.w, im.h, 1, dt.as<uint8_t>()),
+                   "pf_warp_rgb") ||
+            !hip_ok(hipMemcpy(tiles.data(), dt.p, total, hipMemcpyDeviceToHost), "download"))
+            return 1;
+        const std::string base = fs::path(fn).filename().string();
+        const std::string rawname = base.substr(0, base.find_last_of('.'));
+        size_t off = 0;
+        for (int i = 0; i < n; ++i) {
+            char name[512];
+            std::snprintf(name, sizeof(name), "%s.%d_%d_%d_%d.png", rawname.c_str(),
+                          (int)std::round(fovs[i][0] / PF_MYPI_D * 180.0),
+                          (int)std::round(fovs[i][1] / PF_MYPI_D * 180.0),
+                          (int)std::round(fovs[i][2] / PF_MYPI_D * 180.0),
+                          (int)std::round(fovs[i][3] / PF_MYPI_D * 180.0));
+            if (!pfio::save_png8((fs::path(tile_dir) / name).string(), tiles.data() + off, tw[i],
+                                 th[i], 3, err)) {
+                std::cout << "[SaveCubeMap] " << err << std::endl;
+                return 1;
+            }
+            off += (size_t)tw[i] * th[i] * 3;
+        }
+        std::cout << "[SaveCubeMap] " << fn << ": " << n << " tiles" << std::endl;
+    }
+    return 0;
+}
+
 // ---- C-ABI helpers for bindings and tests (include/pf_depth.h) ----
 extern "C" int pfd_load_map(const char* fn, int is_emap, float* out, long long cap, int* w, int* h,
                             int* c)

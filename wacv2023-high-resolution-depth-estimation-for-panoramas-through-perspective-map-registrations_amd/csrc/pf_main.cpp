@@ -1,6 +1,9 @@
 // panofuse_main -- the reference's command line (Main.cpp:864-895) for the fusion path:
 //   panofuse_main 0 <rgb_dir> <gt_dir> <baseline_dir> <result_dir> [--tiles DIR]
 //                 [--ext auto|jpg|png] [--width W] [--device D]
+//   panofuse_main export <rgb_dir> <tile_dir> [--device D]
+// "export" is the tile render of mode 0 (Main.cpp:399-430, SaveCubeMap :242-326) on the GPU:
+// each RGB panorama becomes the 15 LeReS perspective tiles the depth network consumes.
 // Mode 0 = CreateDepthPanoramas (Main.cpp:331-687) minus the OpenGL tile export: the perspective
 // depth tiles are read from --tiles (default "test_images", the reference's LeReS folder) named
 // <raw>.<a0>_<a1>_<z0>_<z1>.<ext>; "auto" takes .jpg when present, else .png (MiDaS naming).
@@ -17,11 +20,24 @@ int main(int argc, char* argv[])
     if (argc < 2) {
         std::cout << "usage: " << argv[0]
                   << " 0 <rgb_dir> <gt_dir> <baseline_dir> <result_dir> [--tiles DIR]"
-                     " [--ext auto|jpg|png] [--width W] [--device D]"
-                  << std::endl;
+                     " [--ext auto|jpg|png] [--width W] [--device D]\n       "
+                  << argv[0] << " export <rgb_dir> <tile_dir> [--device D]" << std::endl;
         return 0;
     }
     const std::string cmd(argv[1]);
+    if (cmd == "export") {
+        if (argc < 4) {
+            std::cout << "usage: " << argv[0] << " export <rgb_dir> <tile_dir> [--device D]"
+                      << std::endl;
+            return 1;
+        }
+        const int dev = argc >= 6 && std::string(argv[4]) == "--device" ? std::atoi(argv[5]) : 0;
+        if (hipSetDevice(dev) != hipSuccess) {
+            std::cout << "no HIP device " << dev << std::endl;
+            return 1;
+        }
+        return pf_export_rgb_tiles(argv[2], argv[3]);
+    }
     if (cmd != "0") return 0;  // Main.cpp:889-893: other commands do nothing
     if (argc < 6) {
         std::cout << "[CreateDepthPanormas] error: need argc>=6" << std::endl;
