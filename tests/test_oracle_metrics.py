@@ -67,3 +67,16 @@ def test_metrics_oracle_empty_is_nan():
     got = O.error_metrics(np.zeros((64, 128), np.float32), np.ones((32, 64), np.uint16),
                           PL.ZENITH_RANGE, 1, True)
     assert got["n"] == 0 and np.isnan(got["mse"]) and np.isnan(got["median_shift"])
+
+
+def test_u16_unit_reciprocal_form_is_exact():
+    """The metrics kernel's u16_unit (x * rcp refined by one fma, pf_metrics.hip) equals the
+    correctly rounded (float)u / 65535.0f for every u16: emulated here with fp64 (the fma
+    products are exact in fp64, the single roundings are np.float32 casts)."""
+    u = np.arange(65536, dtype=np.float64)
+    rcp = np.float64(np.float32(1.0) / np.float32(65535.0))
+    q = np.float32(u * rcp).astype(np.float64)
+    r = np.float32(u - q * 65535.0).astype(np.float64)
+    q2 = np.float32(r * rcp + q)
+    ref = u.astype(np.float32) / np.float32(65535.0)
+    assert np.array_equal(q2, ref)
