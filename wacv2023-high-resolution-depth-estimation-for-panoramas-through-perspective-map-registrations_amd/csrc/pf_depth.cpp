@@ -19,6 +19,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <filesystem>
+#include <future>
 #include <iostream>
 #include <map>
 #include <mutex>
@@ -485,9 +486,17 @@ bool MergeDepthMaps(std::string& emap_fn, std::vector<std::string>& pmap_fns,
         return false;
     }
     pmaps.resize(pmap_fns.size());
+    {  // the tiles decode in parallel host threads (zlib inflate is the host-side cost)
+        std::vector<std::future<bool>> loads;
+        for (size_t i = 0; i < pmap_fns.size(); i++)
+            loads.push_back(std::async(std::launch::async,
+                                       [&, i] { return pmaps[i].Load(pmap_fns[i]); }));
+        bool ok = true;
+        for (auto& f : loads) ok = f.get() && ok;
+        if (!ok) return false;
+    }
     for (size_t i = 0; i < pmap_fns.size(); i++) {  // Depth.cpp:773-787
         PerspectiveMap& p = pmaps[i];
-        if (!p.Load(pmap_fns[i])) return false;
         p.SetWindow(fovs[i][0], fovs[i][1], fovs[i][2], fovs[i][3]);
         p.ranges[0] = cap_range(ranges[i][0]);
         p.ranges[1] = cap_range(ranges[i][1]);
