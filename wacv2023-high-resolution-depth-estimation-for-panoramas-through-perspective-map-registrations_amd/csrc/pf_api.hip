@@ -50,6 +50,8 @@ struct pf_ctx {
     // layout
     int ntiles = 0, tile_c = 1;
     std::vector<pf_window> fov, rng;
+    std::vector<int> tw_h, th_h;
+    bool layout_ok = false;  // the stored layout was set completely
     std::vector<TileGeom> geom_h;
     std::vector<RegGrid> reg_h;
     long long tile_elems = 0, npix_max = 0, rgb_elems = 0;
@@ -425,11 +427,31 @@ int pf_set_tiles(pf_ctx* c, const pf_window* fovs, const pf_window* ranges, int 
         return fail(c, PF_EINVAL, "pf_set_tiles: bad arguments (ntiles=%d, tile_c=%d)", ntiles,
                     tile_c);
     HIPCHK(c, hipSetDevice(c->device));
+    const double cap = 359.9 / 180.0 * PF_MYPI;  // D2R(359.9), MergeDepthMaps :783-784
+    {
+        // The same layout again (a per-panorama caller such as the DepthNamespace facade):
+        // keep the per-layout caches (level boxes, tap maps, registration grids, warp maps).
+        bool same = c->layout_ok && c->ntiles == ntiles && c->tile_c == tile_c &&
+                    (int)c->tw_h.size() == ntiles && (int)c->th_h.size() == ntiles;
+        for (int i = 0; same && i < ntiles; i++) {
+            pf_window r = ranges[i];
+            if (cap_ranges) {
+                r.az_left = (float)((double)r.az_left < cap ? (double)r.az_left : cap);
+                r.az_right = (float)((double)r.az_right < cap ? (double)r.az_right : cap);
+            }
+            same = !memcmp(&c->fov[i], &fovs[i], sizeof(pf_window)) &&
+                   !memcmp(&c->rng[i], &r, sizeof(pf_window)) && c->tw_h[i] == tile_w[i] &&
+                   c->th_h[i] == tile_h[i];
+        }
+        if (same) return PF_OK;
+    }
+    c->layout_ok = false;
     c->ntiles = ntiles;
     c->tile_c = tile_c;
     c->fov.assign(fovs, fovs + ntiles);
     c->rng.assign(ranges, ranges + ntiles);
-    const double cap = 359.9 / 180.0 * PF_MYPI;  // D2R(359.9), MergeDepthMaps :783-784
+    c->tw_h.assign(tile_w, tile_w + ntiles);
+    c->th_h.assign(tile_h, tile_h + ntiles);
     c->geom_h.resize(ntiles);
     c->reg_h.resize(ntiles);
     std::vector<RgbCam> cams(ntiles);
@@ -494,6 +516,7 @@ int pf_set_tiles(pf_ctx* c, const pf_window* fovs, const pf_window* ranges, int 
     if ((rc = upload(c, c->geom, c->geom_h))) return rc;
     if ((rc = upload(c, c->cams, cams))) return rc;
     if ((rc = upload(c, c->rgb_off, rgb_off))) return rc;
+    c->layout_ok = true;
     return PF_OK;
 }
 
