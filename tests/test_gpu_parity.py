@@ -410,3 +410,30 @@ def test_tile_sharded_pipeline_equals_fuse(fuser):
     pf_dist.fuse_tile_sharded(SumBackend(), nlev, lay.ntiles, 0, 1)
     torch.cuda.synchronize()
     assert int((out != ref).sum().item()) == 0
+
+
+def test_layout_reuse_and_switch_bit_exact(fuser):
+    """pf_set_tiles with the same layout again keeps the per-layout caches; switching layouts
+    (C1 -> C2 -> C1, and the same windows with other ranges) rebuilds them.  Every merge stays
+    bit-exact against the oracle."""
+    def run(cfg, lay=None):
+        out_w, ew = CFGS[cfg]
+        lay = lay or PL.config_layout(cfg)
+        fuser.set_tiles(lay)
+        tiles, total = O.make_tiles(lay)
+        seeds = pf_synth.seeds_for(1, 4242)
+        emap = pf_synth.baseline_emap(seeds, ew, ew // 2).numpy()
+        gt = pf_synth.scene_depth(seeds, out_w, out_w // 2).numpy()
+        data = O.warp_depth(gt[0], tiles, total, O.responses(pf_synth.responses(seeds, lay.ntiles)))
+        out = torch.zeros((1, out_w // 2, out_w), dtype=torch.int16, device=DEV)
+        fuser.merge(_dev(emap), _dev(data[None]), out, ZR)
+        ref, _ = O.merge(emap[0], tiles, data.copy(), out_w, ZR)
+        assert int((out.cpu().numpy().view(np.uint16)[0] != ref).sum()) == 0, cfg
+
+    for cfg in ("C1", "C1", "C2", "C1"):
+        run(cfg)
+    lay = PL.config_layout("C1")
+    shifted = PL.Layout(lay.name, lay.fovs.copy(), lay.ranges.copy(), lay.tile_w, lay.tile_h)
+    shifted.ranges[:, 2] += np.float32(0.02)  # same windows, other valid zenith ranges
+    run("C1", shifted)
+    run("C1")

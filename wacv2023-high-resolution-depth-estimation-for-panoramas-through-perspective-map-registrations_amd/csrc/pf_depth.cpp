@@ -479,6 +479,17 @@ bool MergeDepthMaps(std::string& emap_fn, std::vector<std::string>& pmap_fns,
     const auto t_begin = std::chrono::steady_clock::now();
     EquirectangularMap emap;
     std::vector<PerspectiveMap> pmaps;
+    // the ground truth decodes on a host thread while the tiles load and the GPU fuses
+    EquirectangularMap gt;
+    std::future<bool> gt_loaded;
+    if (gt_fn) gt_loaded = std::async(std::launch::async, [&] { return gt.Load(*gt_fn); });
+    struct Join {  // never leave with the loader still writing into `gt`
+        std::future<bool>& f;
+        ~Join()
+        {
+            if (f.valid()) f.wait();
+        }
+    } join{gt_loaded};
     if (!emap.Load(emap_fn)) return false;
     const int out_height = out_width / 2;
     if (fovs.size() < pmap_fns.size() || ranges.size() < pmap_fns.size()) {
@@ -542,8 +553,7 @@ bool MergeDepthMaps(std::string& emap_fn, std::vector<std::string>& pmap_fns,
     if (gt_fn) {  // Depth.cpp:920-1037
         const int align_way = 1;
         const bool cap_depth = true;
-        EquirectangularMap gt;
-        if (gt.Load(*gt_fn)) {
+        if (gt_loaded.get()) {
             Metrics local;
             Metrics& M = metrics ? *metrics : local;
             ErrorEmap(gt, emap, M.mse_given, M.mae_given, M.mre_given, M.mselog_given,
@@ -571,14 +581,17 @@ bool MergeDepthMaps(std::string& emap_fn, std::vector<std::string>& pmap_fns,
                     }
                 Save16BitPNG(o.data(), w, h, fn.c_str());
             };
-            mask(out_width, out_height,
-                 [&](int x, int y) { return data[(size_t)y * out_width + x]; },
-                 out_fn + ".res.png");
+            auto res = std::async(std::launch::async, [&] {
+                mask(out_width, out_height,
+                     [&](int x, int y) { return data[(size_t)y * out_width + x]; },
+                     out_fn + ".res.png");
+            });
             mask(emap.width, emap.height,
                  [&](int x, int y) {
                      return (unsigned short)(emap.ValueAtXY(x, y) * 65535.0f);
                  },
                  out_fn + ".giv.png");
+            res.get();
         }
     }
     return true;
