@@ -20,7 +20,7 @@
  * Errors: false returns with a message on std::cout, as the reference prints its diagnostics.
  * Threading: one host thread per device (the facade keeps one pf_ctx per device).
  *
- * Not provided: JPEG decoding (stb_image's), SolveDisparityToDepth / SolveDepthToDepth2 /
+ * Not provided: progressive JPEG, SolveDisparityToDepth / SolveDepthToDepth2 /
  * SolveDepthBySmoothing (dead code in the reference's mode 0), ErrorCompare / ErrorLaplacian,
  * SolveDepthToDepth with more than one active map (MergeDepthMaps never does that).
  */

@@ -177,3 +177,56 @@ def test_export_rgb_tiles(tmp_path):
         d = np.abs(got.reshape(-1).astype(np.int32) - ref[off:off + n].astype(np.int32))
         off += n
         assert d.max() <= 1 and (d > 0).mean() < 1e-3, (t, d.max(), (d > 0).mean())
+
+
+def test_mode0_cli_jpeg_inputs(tmp_path):
+    """The reference's own file conventions: LeReS tiles as 8-bit gray JPEG in test_images
+    naming (<raw>.<a0>_<a1>_<z0>_<z1>.jpg, Main.cpp:576-578) and a bifuse baseline <raw>.jpg
+    (Main.cpp:499).  The oracle is fed the same decoded floats (the library's loader), so the
+    fused u16 output is still bit-exact."""
+    import ctypes as C
+    Image = pytest.importorskip("PIL.Image")
+    L = C.CDLL(os.path.join(os.path.dirname(panofuse.LIB_PATH), "libpanofuse_depth.so"))
+    L.pfd_load_map.argtypes = [C.c_char_p, C.c_int, C.POINTER(C.c_float), C.c_longlong,
+                               C.POINTER(C.c_int), C.POINTER(C.c_int), C.POINTER(C.c_int)]
+
+    def load(fn, is_emap):
+        w, h, c = C.c_int(), C.c_int(), C.c_int()
+        buf = np.zeros(1 << 22, np.float32)
+        assert L.pfd_load_map(str(fn).encode(), is_emap, buf.ctypes.data_as(C.POINTER(C.c_float)),
+                              buf.size, C.byref(w), C.byref(h), C.byref(c)) == 0
+        return buf[:w.value * h.value * c.value].reshape(h.value, w.value, c.value)
+
+    d = {k: tmp_path / k for k in ("rgb", "gt", "base", "result", "test_images")}
+    for p in d.values():
+        p.mkdir()
+    lay = PL.leres_layout(512, 494)
+    tiles_o, total = O.make_tiles(lay)
+    raw = "room_rgb"
+    (d["rgb"] / (raw + ".png")).write_bytes(b"\x89PNG")
+    seeds = pf_synth.seeds_for(1, 20261015 + 555)
+    gt = _q16(pf_synth.scene_depth(seeds, 2048, 1024)[0].numpy())
+    _png16_write(d["gt"] / "room_depth.png", gt)
+    base8 = (np.clip(pf_synth.baseline_emap(seeds, 512, 256)[0].numpy(), 0, 1) * 255 + 0.5
+             ).astype(np.uint8)
+    Image.fromarray(base8, "L").save(d["base"] / (raw + ".jpg"), "JPEG", quality=95)
+    gt_f = gt.astype(np.float32) / np.float32(65535.0)
+    tdata = O.warp_depth(gt_f, tiles_o, total, O.responses(pf_synth.responses(seeds, lay.ntiles)))
+    t8 = (np.clip(tdata, 0, 1) * 255 + 0.5).astype(np.uint8)
+    dec = []
+    off = 0
+    for t in range(lay.ntiles):
+        f = [_cround(float(v) / MYPI * 180.0) for v in lay.fovs[t]]
+        fn = d["test_images"] / f"{raw}.{f[0]}_{f[1]}_{f[2]}_{f[3]}.jpg"
+        Image.fromarray(t8[off:off + 512 * 494].reshape(494, 512), "L").save(fn, "JPEG",
+                                                                              quality=95)
+        dec.append(load(fn, 0)[..., 0].reshape(-1))
+        off += 512 * 494
+    base_f = load(d["base"] / (raw + ".jpg"), 1)[..., 0]
+    ref, _ = O.merge(base_f, tiles_o, np.concatenate(dec), 2048, ZR)
+    cmd = [BIN, "0", str(d["rgb"]), str(d["gt"]), str(d["base"]), str(d["result"]), "--tiles",
+           str(d["test_images"])]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stdout + r.stderr
+    got = _png16_read(d["result"] / (raw + ".png"))
+    assert int((got != ref).sum()) == 0

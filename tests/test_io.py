@@ -190,3 +190,55 @@ def test_cli_binary_usage():
     assert out.returncode == 0 and "usage" in out.stdout
     out = subprocess.run([BIN, "0", "a"], capture_output=True, text=True, timeout=60)
     assert out.returncode == 1 and "argc>=6" in out.stdout
+
+
+@pytest.mark.parametrize("mode,sub,restart", [("L", None, 0), ("RGB", 0, 0), ("RGB", 2, 0),
+                                              ("RGB", 1, 0), ("L", None, 4), ("RGB", 2, 3)])
+def test_jpeg_decoder_vs_libjpeg(lib, tmp_path, mode, sub, restart):
+    """The baseline JPEG decoder behind the loaders (pf_jpeg.cpp; the reference reads its LeReS
+    tiles and some baselines as JPEG through stb_image) against PIL's libjpeg on PIL-encoded
+    files: gray, 4:4:4, 4:2:0, 4:2:2, restart intervals, odd sizes.  Bar: within 2 levels (the
+    integer IDCTs and fixed-point colour conversion of stb and libjpeg differ from each other by
+    about as much), 3 with subsampled chroma (the upsampler rounds as stb does, +8/+2, where
+    libjpeg alternates +8/+7, and a 1-level chroma difference becomes 1.772 levels of blue);
+    mean under 0.3.  Parity with stb itself is unpinned (no stb build here)."""
+    Image = pytest.importorskip("PIL.Image")
+    rng = np.random.default_rng(6)
+    h, w = 75, 101
+    yy, xx = np.mgrid[0:h, 0:w]
+    base = (np.sin(xx / 9.0) * 60 + np.cos(yy / 7.0) * 50 + 128)
+    if mode == "L":
+        a = np.clip(base + rng.normal(0, 4, (h, w)), 0, 255).astype(np.uint8)
+    else:
+        a = np.clip(np.stack([base, 255 - base, (xx * 2 + yy) % 256], -1) +
+                    rng.normal(0, 4, (h, w, 3)), 0, 255).astype(np.uint8)
+    im = Image.fromarray(a, mode)
+    kw = {"quality": 92}
+    if sub is not None:
+        kw["subsampling"] = sub
+    if restart:
+        kw["restart_marker_blocks"] = restart
+    fn = tmp_path / "t.jpg"
+    try:
+        im.save(fn, "JPEG", **kw)
+    except TypeError:
+        kw.pop("restart_marker_blocks", None)
+        im.save(fn, "JPEG", **kw)
+    ref = np.asarray(Image.open(fn).convert(mode)).astype(np.int32)
+    got = _load(lib, fn, 0)
+    assert got is not None
+    got = np.rint(got * 255.0).astype(np.int32)
+    if mode == "L":
+        assert got.shape == (h, w, 1)
+        got = got[..., 0]
+    else:
+        assert got.shape == (h, w, 3)
+    d = np.abs(got - ref)
+    assert d.max() <= (3 if sub in (1, 2) else 2) and d.mean() < 0.3, (d.max(), d.mean())
+
+
+def test_jpeg_progressive_rejected(lib, tmp_path):
+    Image = pytest.importorskip("PIL.Image")
+    a = np.random.default_rng(1).integers(0, 255, (32, 32), dtype=np.uint8)
+    Image.fromarray(a, "L").save(tmp_path / "p.jpg", "JPEG", progressive=True)
+    assert _load(lib, tmp_path / "p.jpg") is None

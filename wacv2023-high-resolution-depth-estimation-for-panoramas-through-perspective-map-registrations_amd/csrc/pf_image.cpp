@@ -261,8 +261,10 @@ bool load_image(const std::string& fn, Image& out, std::string& err)
     if (!read_file(fn, f)) return err = "cannot open " + fn, false;
     if (f.size() >= 8 && !std::memcmp(f.data(), kSig, 8)) return decode_png(f, out, err);
     if (f.size() > 2 && f[0] == 'P' && (f[1] == '5' || f[1] == '6')) return decode_pnm(f, out, err);
-    if (f.size() > 2 && f[0] == 0xFF && f[1] == 0xD8)
-        return err = "JPEG input is not supported by this build (convert to PNG): " + fn, false;
+    if (f.size() > 2 && f[0] == 0xFF && f[1] == 0xD8) {
+        if (!decode_jpeg(f, out, err)) return err += ": " + fn, false;
+        return true;
+    }
     return err = "unknown image format: " + fn, false;
 }
 

@@ -8,8 +8,8 @@
 //   * load_pfm (Depth.cpp:376-452): "PF"/"Pf" portable float maps, the reference's endian rule;
 //   * Save16BitPNG (Depth.cpp:27-32, cv::imwrite of a CV_16UC1 Mat) and stbi_write_png:
 //     16-bit / 8-bit PNG writers on zlib.
-// JPEG decoding (stb's baseline/progressive decoder, used for the LeReS tiles and some
-// baselines) is not provided: a JPEG input is rejected with a message naming the file.
+//   * stb's JPEG decoding (the LeReS tiles and some baselines): baseline / extended-sequential
+//     Huffman JPEG in pf_jpeg.cpp (progressive files are rejected with a message).
 #pragma once
 
 #include <cstdint>
@@ -31,6 +31,8 @@ bool load_image(const std::string& fn, Image& out, std::string& err);
 // Returns a malloc'd [h][w][c] float buffer (free with std::free) or nullptr.
 float* load_pfm(const std::string& fn, int* w, int* h, int* c, std::string& err);
 bool save_png16(const std::string& fn, const uint16_t* data, int w, int h, std::string& err);
+// Baseline JPEG (pf_jpeg.cpp): 8-bit, 1 or 3 components, output like stbi_load(req_comp 0).
+bool decode_jpeg(const std::vector<uint8_t>& f, Image& out, std::string& err);
 bool save_png8(const std::string& fn, const uint8_t* data, int w, int h, int c,
                std::string& err);
 
