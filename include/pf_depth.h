@@ -142,12 +142,15 @@ bool ErrorEmap(EquirectangularMap& emap_gt, EquirectangularMap& emap_given, floa
 }  // namespace DepthNamespace
 
 /* The mode-0 driver (Main.cpp:331-687 CreateDepthPanoramas) over std::filesystem; tile_ext is
- * "png" (MiDaS naming, Main.cpp:570-573) or "jpg" (LeReS naming, :576-578); the LeReS layout
- * of Main.cpp:788-843 is used.  Returns the process exit code. */
+ * "png" (MiDaS naming, Main.cpp:570-573), "jpg" (LeReS naming, :576-578) or "auto"; the LeReS
+ * layout of Main.cpp:788-843 is used.  shard / nshards: this process takes the panoramas
+ * shard, shard + nshards, ... of the sorted folder (one process per GPU, no communication).
+ * Returns the process exit code. */
 int pf_create_depth_panoramas(const std::string& rgb_folder, const std::string& gt_folder,
                               const std::string& baseline_folder,
                               const std::string& result_folder, const std::string& tile_dir,
-                              const std::string& tile_ext, int out_width);
+                              const std::string& tile_ext, int out_width, int shard = 0,
+                              int nshards = 1);
 /* The RGB tile export of mode 0 (Main.cpp:399-430 + SaveCubeMap :242-326): every panorama of
  * rgb_folder (8/16-bit PNG, PGM/PPM) warped on the GPU (pf_warp_rgb) into the 15 LeReS tiles
  * of 1024 x round(1024/aspect) px, written as <tile_dir>/<raw>.<a0>_<a1>_<z0>_<z1>.png (rows

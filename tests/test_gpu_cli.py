@@ -100,8 +100,13 @@ def test_mode0_cli_end_to_end(tmp_path):
 
     cmd = [BIN, "0", str(d["rgb"]), str(d["gt"]), str(d["base"]), str(d["result_hohonet"]),
            "--tiles", str(d["tiles"])]
-    r = subprocess.run(cmd, capture_output=True, text=True, timeout=300)
-    assert r.returncode == 0, r.stdout + r.stderr
+    # one process per shard (as one per GPU): shard 0/2 takes scene01, 1/2 scene02
+    for k, raw in enumerate(sorted(expected)):
+        r = subprocess.run(cmd + ["--shard", f"{k}/2"], capture_output=True, text=True,
+                           timeout=300)
+        assert r.returncode == 0, r.stdout + r.stderr
+        assert "#RGB_filenames:1" in r.stdout
+        assert (d["result_hohonet"] / (raw + ".png")).exists()
     for raw, (out, gt_f, base_f) in expected.items():
         got = _png16_read(d["result_hohonet"] / (raw + ".png"))
         assert got.shape == (1024, 2048)

@@ -190,6 +190,9 @@ def test_cli_binary_usage():
     assert out.returncode == 0 and "usage" in out.stdout
     out = subprocess.run([BIN, "0", "a"], capture_output=True, text=True, timeout=60)
     assert out.returncode == 1 and "argc>=6" in out.stdout
+    out = subprocess.run([BIN, "0", "a", "b", "c", "d", "--shard", "2/2"], capture_output=True,
+                         text=True, timeout=60)
+    assert out.returncode == 2 and "bad --shard" in out.stdout
 
 
 @pytest.mark.parametrize("mode,sub,restart", [("L", None, 0), ("RGB", 0, 0), ("RGB", 2, 0),

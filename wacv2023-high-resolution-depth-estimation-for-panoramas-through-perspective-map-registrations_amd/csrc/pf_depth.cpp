@@ -625,7 +625,8 @@ void pf_leres_layout(std::vector<Vec4f>& fovs, std::vector<Vec4f>& ranges)
 int pf_create_depth_panoramas(const std::string& rgb_folder, const std::string& gt_folder,
                               const std::string& baseline_folder,
                               const std::string& result_folder, const std::string& tile_dir,
-                              const std::string& tile_ext, int out_width)
+                              const std::string& tile_ext, int out_width, int shard,
+                              int nshards)
 {
     namespace fs = std::filesystem;
     std::vector<Vec4f> fovs, ranges;
@@ -639,6 +640,11 @@ int pf_create_depth_panoramas(const std::string& rgb_folder, const std::string& 
         return 1;
     }
     std::sort(rgb.begin(), rgb.end());
+    if (nshards > 1) {  // panorama sharding over processes / GPUs
+        std::vector<std::string> mine;
+        for (size_t i = (size_t)shard; i < rgb.size(); i += (size_t)nshards) mine.push_back(rgb[i]);
+        rgb.swap(mine);
+    }
     std::cout << "[CreateDepthPanormas] #RGB_filenames:" << rgb.size() << std::endl;
     auto join = [](const std::string& dir, const std::string& name) {
         return (fs::path(dir) / name).string();

@@ -1,6 +1,6 @@
 // panofuse_main -- the reference's command line (Main.cpp:864-895) for the fusion path:
 //   panofuse_main 0 <rgb_dir> <gt_dir> <baseline_dir> <result_dir> [--tiles DIR]
-//                 [--ext auto|jpg|png] [--width W] [--device D]
+//                 [--ext auto|jpg|png] [--width W] [--device D] [--shard R/N]
 //   panofuse_main export <rgb_dir> <tile_dir> [--device D]
 // "export" is the tile render of mode 0 (Main.cpp:399-430, SaveCubeMap :242-326) on the GPU:
 // each RGB panorama becomes the 15 LeReS perspective tiles the depth network consumes.
@@ -11,6 +11,7 @@
 
 #include <hip/hip_runtime.h>
 
+#include <cstdio>
 #include <cstdlib>
 #include <iostream>
 #include <string>
@@ -20,7 +21,7 @@ int main(int argc, char* argv[])
     if (argc < 2) {
         std::cout << "usage: " << argv[0]
                   << " 0 <rgb_dir> <gt_dir> <baseline_dir> <result_dir> [--tiles DIR]"
-                     " [--ext auto|jpg|png] [--width W] [--device D]\n       "
+                     " [--ext auto|jpg|png] [--width W] [--device D] [--shard R/N]\n       "
                   << argv[0] << " export <rgb_dir> <tile_dir> [--device D]" << std::endl;
         return 0;
     }
@@ -44,13 +45,20 @@ int main(int argc, char* argv[])
         return 1;
     }
     std::string tiles = "test_images", ext = "auto";
-    int width = 2048, device = 0;
+    int width = 2048, device = 0, shard = 0, nshards = 1;
     for (int i = 6; i + 1 < argc; i += 2) {
         const std::string k(argv[i]), v(argv[i + 1]);
         if (k == "--tiles") tiles = v;
         else if (k == "--ext") ext = v;
         else if (k == "--width") width = std::atoi(v.c_str());
         else if (k == "--device") device = std::atoi(v.c_str());
+        else if (k == "--shard") {  // R/N: one process per GPU over the sorted folder
+            if (std::sscanf(v.c_str(), "%d/%d", &shard, &nshards) != 2 || nshards < 1 ||
+                shard < 0 || shard >= nshards) {
+                std::cout << "bad --shard " << v << " (want R/N, 0 <= R < N)" << std::endl;
+                return 2;
+            }
+        }
         else {
             std::cout << "unknown option " << k << std::endl;
             return 2;
@@ -60,5 +68,6 @@ int main(int argc, char* argv[])
         std::cout << "no HIP device " << device << std::endl;
         return 1;
     }
-    return pf_create_depth_panoramas(argv[2], argv[3], argv[4], argv[5], tiles, ext, width);
+    return pf_create_depth_panoramas(argv[2], argv[3], argv[4], argv[5], tiles, ext, width, shard,
+                                     nshards);
 }
