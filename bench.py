@@ -89,6 +89,12 @@ def pmc_traffic(family):
         return None
 
 
+def _metrics_traffic():
+    """PMC HBM bytes of one pf_error_metrics call (align_way 1): 3 k_med_hist + k_err_sums."""
+    h, e = pmc_traffic("pf::k_med_hist"), pmc_traffic("pf::k_err_sums")
+    return 3 * h + e if h is not None and e is not None else None
+
+
 def run_c5(args, rank, world, local, dev):
     """BASELINE config C5: one 8192x4096 panorama, 80 tiles of 1024^2 sharded over the ranks.
     Each rank warps and registers its own tiles (a sub-layout context writing into its slice of
@@ -305,6 +311,8 @@ def main():
             # metrics stage (outside the timed step): algorithmic bytes = one read of the
             # compared band of gt (4 B) and result (2 B) per pixel; the kernels make 4 passes
             "roofline_metrics": {"bound": "hbm", "achieved": stages["metrics"]["GBps"],
+                                 # HBM bytes of one call: 3 histogram passes + the sums pass
+                                 "traffic": _metrics_traffic(),
                                  "peak": HBM_PEAK_GBS, "unit": "GB/s",
                                  "frac": stages["metrics"]["GBps"] / HBM_PEAK_GBS,
                                  "kernel": "pf_error_metrics (k_med_hist x3, k_med_scan x3, "

@@ -21,6 +21,7 @@ import sys
 
 
 def family(name):
+    name = name.replace("(anonymous namespace)::", "")
     short = name.split("(")[0].replace("void ", "").strip()
     return short.split("<")[0]
 
