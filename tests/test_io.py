@@ -245,3 +245,37 @@ def test_jpeg_progressive_rejected(lib, tmp_path):
     a = np.random.default_rng(1).integers(0, 255, (32, 32), dtype=np.uint8)
     Image.fromarray(a, "L").save(tmp_path / "p.jpg", "JPEG", progressive=True)
     assert _load(lib, tmp_path / "p.jpg") is None
+
+
+def test_image_decoders_fuzz_sanitized(tmp_path):
+    """Mutated PNG / JPEG / PFM files through the loaders, built host-only with ASan + UBSan
+    (tools/fuzz/fuzz_images.cpp): corrupt inputs must be rejected, never read out of bounds."""
+    import shutil
+    Image = pytest.importorskip("PIL.Image")
+    if shutil.which("g++") is None:
+        pytest.skip("no g++")
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    csrc = os.path.join(os.path.dirname(os.path.dirname(panofuse.LIB_PATH)), "csrc")
+    exe = tmp_path / "fuzz"
+    r = subprocess_run(["g++", "-std=c++17", "-O1", "-g", "-fsanitize=address,undefined",
+                        "-fno-sanitize-recover=all", "-I", csrc,
+                        os.path.join(root, "tools", "fuzz", "fuzz_images.cpp"),
+                        os.path.join(csrc, "pf_image.cpp"), os.path.join(csrc, "pf_jpeg.cpp"),
+                        "-lz", "-o", str(exe)])
+    assert r.returncode == 0, r.stderr
+    rng = np.random.default_rng(0)
+    a = rng.integers(0, 255, (40, 57, 3), dtype=np.uint8)
+    Image.fromarray(a).save(tmp_path / "a.jpg", quality=90, subsampling=2)
+    Image.fromarray(a[..., 0]).save(tmp_path / "b.jpg", quality=90)
+    Image.fromarray(a).save(tmp_path / "c.png")
+    Image.fromarray(a[..., 0].astype(np.uint16) * 257).save(tmp_path / "d.png")
+    (tmp_path / "e.pfm").write_bytes(b"Pf\n5 4\n-1.0\n" + np.ones((4, 5), np.float32).tobytes())
+    seeds = [str(tmp_path / n) for n in ("a.jpg", "b.jpg", "c.png", "d.png", "e.pfm")]
+    r = subprocess_run([str(exe), "600", str(tmp_path / "cur.bin")] + seeds, timeout=300)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "decoded" in r.stdout
+
+
+def subprocess_run(cmd, timeout=300):
+    import subprocess
+    return subprocess.run(cmd, capture_output=True, text=True, timeout=timeout)

@@ -88,7 +88,7 @@ struct Bits {
     }
 };
 
-void build_huff(Huff& h, const uint8_t* counts, const uint8_t* vals, int nvals)
+bool build_huff(Huff& h, const uint8_t* counts, const uint8_t* vals, int nvals)
 {
     h.present = true;
     std::memcpy(h.vals, vals, nvals);
@@ -97,6 +97,7 @@ void build_huff(Huff& h, const uint8_t* counts, const uint8_t* vals, int nvals)
     for (int l = 1; l <= 16; ++l) {
         h.valptr[l] = k;
         h.mincode[l] = code;
+        if (code + counts[l - 1] > (1 << l)) return h.present = false;  // over-full code space
         for (int i = 0; i < counts[l - 1]; ++i, ++k, ++code) {
             if (l <= 9) {
                 const int base = code << (9 - l);
@@ -110,6 +111,7 @@ void build_huff(Huff& h, const uint8_t* counts, const uint8_t* vals, int nvals)
         code <<= 1;
     }
     h.maxcode[17] = 0x7FFFFFFF;
+    return true;
 }
 
 int decode_sym(Bits& b, const Huff& h)
@@ -214,14 +216,20 @@ bool decode_jpeg(const std::vector<uint8_t>& f, Image& out, std::string& err)
         const int m = f[p + 1];
         if (m == 0xFF) { ++p; continue; }
         if (m == 0xD9) break;
+        if (m == 0x01 || (m >= 0xD0 && m <= 0xD7)) {  // standalone markers
+            p += 2;
+            continue;
+        }
         const int len = u16(p + 2);
+        if (len < 2) return err = "JPEG: bad segment length", false;
         const size_t seg = p + 4, segend = p + 2 + len;
         if (segend > f.size()) return err = "JPEG: truncated segment", false;
         if (m == 0xDB) {  // DQT
             size_t i = seg;
             while (i < segend) {
                 const int pq = f[i] >> 4, tq = f[i] & 15;
-                if (tq > 3) return err = "JPEG: bad DQT", false;
+                if (tq > 3 || pq > 1 || i + 1 + (pq ? 128 : 64) > segend)
+                    return err = "JPEG: bad DQT", false;
                 ++i;
                 for (int k = 0; k < 64; ++k) {
                     qt[tq][kZig[k]] = pq ? (uint16_t)u16(i + 2 * k) : f[i + k];
@@ -238,16 +246,19 @@ bool decode_jpeg(const std::vector<uint8_t>& f, Image& out, std::string& err)
                 int n = 0;
                 for (int l = 0; l < 16; ++l) n += counts[l];
                 if (n > 256 || i + 17 + n > segend) return err = "JPEG: bad DHT", false;
-                build_huff(tc ? hac[th] : hdc[th], counts, &f[i + 17], n);
+                if (!build_huff(tc ? hac[th] : hdc[th], counts, &f[i + 17], n))
+                    return err = "JPEG: bad Huffman table", false;
                 i += 17 + n;
             }
         } else if (m == 0xC0 || m == 0xC1) {  // SOF0 / SOF1
-            if (f[seg] != 8) return err = "JPEG: only 8-bit samples are supported", false;
+            if (len < 8 || f[seg] != 8)
+                return err = "JPEG: only 8-bit samples are supported", false;
             H = u16(seg + 1);
             W = u16(seg + 3);
             const int nc = f[seg + 5];
-            if (W <= 0 || H <= 0 || (nc != 1 && nc != 3))
+            if (W <= 0 || H <= 0 || (nc != 1 && nc != 3) || seg + 6 + 3 * nc > segend)
                 return err = "JPEG: only 1- or 3-component images are supported", false;
+            if ((long long)W * H > (1ll << 28)) return err = "JPEG: image too large", false;
             comps.resize(nc);
             for (int k = 0; k < nc; ++k) {
                 Comp& c = comps[k];
@@ -265,10 +276,12 @@ bool decode_jpeg(const std::vector<uint8_t>& f, Image& out, std::string& err)
             return err = "JPEG: progressive / lossless / arithmetic coding is not supported",
                    false;
         } else if (m == 0xDD) {  // DRI
+            if (len < 4) return err = "JPEG: bad DRI", false;
             restart = u16(seg);
         } else if (m == 0xDA) {  // SOS: one interleaved scan with every component
             if (!frame) return err = "JPEG: scan before frame", false;
             const int ns = f[seg];
+            if (seg + 1 + 2 * (size_t)ns > segend) return err = "JPEG: bad SOS", false;
             if (ns != (int)comps.size())
                 return err = "JPEG: non-interleaved scans are not supported", false;
             if (ns == 1) {  // a single-component scan is non-interleaved: one block per MCU
@@ -277,6 +290,7 @@ bool decode_jpeg(const std::vector<uint8_t>& f, Image& out, std::string& err)
             }
             for (int k = 0; k < ns; ++k) {
                 const int cid = f[seg + 1 + 2 * k], tbl = f[seg + 2 + 2 * k];
+                if ((tbl >> 4) > 3 || (tbl & 15) > 3) return err = "JPEG: bad table selector", false;
                 for (Comp& c : comps)
                     if (c.id == cid) c.td = tbl >> 4, c.ta = tbl & 15;
             }
