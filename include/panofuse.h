@@ -72,6 +72,13 @@ int pf_register(pf_ctx* ctx, const float* emap, int ew, int eh, int ec, float* t
                 int batch, float zr0, float zr1, int degree, int apply, float* coeffs,
                 double* coeffs64);
 
+/* SolveDepthToDepth with several active maps (Depth.cpp:1261-1414: the sample grids of every
+ * active tile in one least-squares problem): active is a HOST int[ntiles] mask; coeffs
+ * ([batch][4] floats) / coeffs64 ([batch][4] doubles) are device pointers (either may be NULL). */
+int pf_register_joint(pf_ctx* ctx, const float* emap, int ew, int eh, int ec, const float* tiles,
+                      int batch, float zr0, float zr1, int degree, const int* active,
+                      float* coeffs, double* coeffs64);
+
 /* SolveDepthAll (Depth.cpp:1416-1771): multi-level Laplacian-target scatter + damped Jacobi,
  * u16 output.  coeffs (optional, from pf_register with apply = 0) fuses Depth2DepthTransform
  * into the tile gather instead of rewriting the tiles. */

@@ -21,8 +21,7 @@
  * Threading: one host thread per device (the facade keeps one pf_ctx per device).
  *
  * Not provided: progressive JPEG, SolveDisparityToDepth / SolveDepthToDepth2 /
- * SolveDepthBySmoothing (dead code in the reference's mode 0), ErrorCompare / ErrorLaplacian,
- * SolveDepthToDepth with more than one active map (MergeDepthMaps never does that).
+ * SolveDepthBySmoothing (dead code in the reference's mode 0), ErrorCompare / ErrorLaplacian.
  */
 #pragma once
 

@@ -437,3 +437,30 @@ def test_layout_reuse_and_switch_bit_exact(fuser):
     shifted.ranges[:, 2] += np.float32(0.02)  # same windows, other valid zenith ranges
     run("C1", shifted)
     run("C1")
+
+
+def test_register_joint_matches_lstsq(fuser):
+    """SolveDepthToDepth with several active maps (Depth.cpp:1274-1376): the samples of every
+    active tile in one problem.  Against an fp64 lstsq over the concatenated samples (the fitted
+    values within 1e-6, the bar of test_register_degree1_and_lstsq); a single active tile equals
+    pf_register's per-tile solve bit for bit."""
+    lay, emap, gt, tiles, total, data, _ = _inputs("C1")
+    fuser.set_tiles(lay)
+    t_emap, t_data = _dev(emap)[None], _dev(data)[None].contiguous()
+    for active in ([0, 2], [1, 3, 4], list(range(lay.ntiles))):
+        c64 = torch.zeros((1, 4), dtype=torch.float64, device=DEV)
+        fuser.register_joint(t_emap, t_data, ZR, active, coeffs64=c64)
+        xs, ys = [], []
+        for p in active:
+            x, y, _, _ = O.reg_samples(tiles[p], data, emap, ZR)
+            xs.append(x)
+            ys.append(y)
+        xs, ys = np.concatenate(xs), np.concatenate(ys)
+        A = np.stack([xs ** k for k in range(3, -1, -1)], 1)
+        sol, *_ = np.linalg.lstsq(A, ys, rcond=None)
+        assert np.max(np.abs(A @ c64.cpu().numpy()[0] - A @ sol)) < 1e-6, active
+    per = torch.zeros((1, lay.ntiles, 4), dtype=torch.float32, device=DEV)
+    fuser.register(t_emap, t_data, ZR, apply=False, coeffs=per)
+    one = torch.zeros((1, 4), dtype=torch.float32, device=DEV)
+    fuser.register_joint(t_emap, t_data, ZR, [3], coeffs=one)
+    assert torch.equal(one[0], per[0, 3])

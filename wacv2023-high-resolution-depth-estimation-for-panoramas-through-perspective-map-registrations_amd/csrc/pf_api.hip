@@ -65,7 +65,7 @@ struct pf_ctx {
     int wmap_pw = 0, wmap_ph = 0, npatch = 0;
     DevBuf wmap, wfxy, wpatch;
     // workspace
-    DevBuf buf[3], lnorm, coeffs, lsum_ws, metrics_ws;
+    DevBuf buf[3], lnorm, coeffs, lsum_ws, metrics_ws, reg_sums, reg_active;
     // stage profiling
     struct Span {
         int stage;
@@ -328,7 +328,8 @@ void pf_destroy(pf_ctx* c)
     (void)hipStreamSynchronize(c->stream);
     DevBuf* all[] = {&c->geom, &c->reg, &c->rcols, &c->rrows, &c->cams, &c->rgb_off,
                      &c->buf[0], &c->buf[1], &c->buf[2], &c->lnorm, &c->coeffs, &c->lsum_ws,
-                     &c->wmap, &c->wfxy, &c->wpatch, &c->metrics_ws};
+                     &c->wmap, &c->wfxy, &c->wpatch, &c->metrics_ws, &c->reg_sums,
+                     &c->reg_active};
     for (DevBuf* b : all) release(*b);
     for (int l = 0; l < 4; l++) {
         release(c->lc.box[l]);
@@ -1310,6 +1311,39 @@ int pf_depth_transform(pf_ctx* c, float* data, long long npix, int channels, con
         return fail(c, PF_EINVAL, "pf_depth_transform: bad arguments");
     if (npix == 0) return PF_OK;
     launch_d2d_map(c->stream, data, npix, channels, abcd);
+    HIPCHK(c, hipGetLastError());
+    return PF_OK;
+}
+
+int pf_register_joint(pf_ctx* c, const float* emap, int ew, int eh, int ec, const float* tiles,
+                      int batch, float zr0, float zr1, int degree, const int* active,
+                      float* coeffs, double* coeffs64)
+{
+    int rc;
+    if ((rc = check_common(c, batch))) return rc;
+    if ((rc = check_emap(c, emap, ew, eh, ec))) return rc;
+    if (!tiles || !active) return fail(c, PF_EINVAL, "tiles/active is NULL");
+    if (degree < 0 || degree > 3) return fail(c, PF_EINVAL, "degree %d not in [0,3]", degree);
+    if ((rc = prepare_registration(c, zr0, zr1))) return rc;
+    std::vector<int> act(active, active + c->ntiles);
+    int nact = 0;
+    for (int v : act) nact += v != 0;
+    if (nact == 0) return fail(c, PF_EINVAL, "pf_register_joint: no active tile");
+    if ((rc = upload(c, c->reg_active, act))) return rc;
+    if ((rc = ensure(c, c->reg_sums,
+                     sizeof(double) * register_sums_per_tile() * c->ntiles * batch)))
+        return rc;
+    float* cf = coeffs;
+    if (!cf) {
+        if ((rc = ensure(c, c->coeffs, sizeof(float) * 4 * batch))) return rc;
+        cf = (float*)c->coeffs.p;
+    }
+    launch_register(c->stream, (const TileGeom*)c->geom.p, (const RegGrid*)c->reg.p,
+                    (const GridCol*)c->rcols.p, (const GridRow*)c->rrows.p, c->ntiles, emap, ew,
+                    eh, ec, (long long)ew * eh * ec, tiles, c->tile_elems, degree, nullptr,
+                    nullptr, batch, (double*)c->reg_sums.p);
+    launch_register_joint(c->stream, (const double*)c->reg_sums.p, (const int*)c->reg_active.p,
+                          c->ntiles, batch, degree, cf, coeffs64);
     HIPCHK(c, hipGetLastError());
     return PF_OK;
 }

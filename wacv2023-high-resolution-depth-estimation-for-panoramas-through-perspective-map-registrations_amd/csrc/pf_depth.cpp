@@ -398,26 +398,27 @@ void Metrics::Print()
 bool SolveDepthToDepth(EquirectangularMap& emap, std::vector<PerspectiveMap>& pmaps,
                        std::vector<bool>& actives, Vec2f& zr, Vec4f& abcd)
 {
-    int act = -1, nact = 0;
+    // every active map's sample grid in one least-squares problem (Depth.cpp:1274-1376)
+    std::vector<PerspectiveMap*> pm;
     for (size_t i = 0; i < actives.size() && i < pmaps.size(); ++i)
-        if (actives[i]) act = (int)i, ++nact;
-    if (nact != 1) {
-        std::cout << "[SolveDepthToDepth] exactly one active map is supported (got " << nact
-                  << ")" << std::endl;
+        if (actives[i]) pm.push_back(&pmaps[i]);
+    if (pm.empty()) {
+        std::cout << "[SolveDepthToDepth] no active map" << std::endl;
         return false;
     }
     pf_ctx* c = facade_ctx();
     if (!c || !emap.data) return false;
-    std::vector<PerspectiveMap*> pm{&pmaps[act]};
     std::vector<float> packed;
     if (!set_layout(c, pm, packed)) return false;
     const size_t ne = (size_t)emap.width * emap.height * emap.channels;
     DevMem de(ne * 4), dt(packed.size() * 4), dc(4 * sizeof(float));
     if (!upload(de, emap.data, ne) || !upload(dt, packed.data(), packed.size()) || !dc.ok)
         return false;
-    if (!pf_ok(c, pf_register(c, de.as<float>(), emap.width, emap.height, emap.channels,
-                              dt.as<float>(), 1, zr[0], zr[1], 3, 0, dc.as<float>(), nullptr),
-               "pf_register"))
+    const std::vector<int> all(pm.size(), 1);
+    if (!pf_ok(c, pf_register_joint(c, de.as<float>(), emap.width, emap.height, emap.channels,
+                                    dt.as<float>(), 1, zr[0], zr[1], 3, all.data(),
+                                    dc.as<float>(), nullptr),
+               "pf_register_joint"))
         return false;
     float k[4];
     if (!hip_ok(hipMemcpy(k, dc.p, sizeof(k), hipMemcpyDeviceToHost), "download")) return false;

@@ -308,12 +308,29 @@ __device__ int solve_normal(const double* S, int degree, double* coef)
     return 0;
 }
 
+// Degree-d least squares from the normal-equation sums (falling back to lower degrees when the
+// system is singular), stored as {a, b, c, d} with the unused high-order terms 0.
+__device__ void solve_store(const double* S, int degree, float* coeffs, double* coeffs64,
+                            long long o)
+{
+    double coef[4] = {0, 0, 0, 0};
+    int d = degree, rc = -1;
+    while (d >= 0 && (rc = solve_normal(S, d, coef)) != 0) d--;
+    if (rc != 0) { coef[0] = 0.0; d = 0; }
+    double full[4] = {0, 0, 0, 0};
+    for (int i = 0; i <= d; i++) full[3 - d + i] = coef[i];
+    for (int i = 0; i < 4; i++) {
+        if (coeffs) coeffs[o + i] = (float)full[i];
+        if (coeffs64) coeffs64[o + i] = full[i];
+    }
+}
+
 __global__ void __launch_bounds__(kRegLanes) k_register(
     const TileGeom* __restrict__ geom, const RegGrid* __restrict__ grids,
     const GridCol* __restrict__ rcols, const GridRow* __restrict__ rrows, int ntiles,
     const float* __restrict__ emap, int ew, int eh, int ec, long long estride,
     const float* __restrict__ tiles, long long tstride, int degree, float* __restrict__ coeffs,
-    double* __restrict__ coeffs64)
+    double* __restrict__ coeffs64, double* __restrict__ sums)
 {
     __shared__ double part[kRegSums][kRegLanes];
     const int p = blockIdx.x, b = blockIdx.y, l = threadIdx.x;
@@ -357,18 +374,29 @@ __global__ void __launch_bounds__(kRegLanes) k_register(
     if (l == 0) {
         double S[kRegSums];
         for (int k = 0; k < kRegSums; k++) S[k] = part[k][0];
-        double coef[4] = {0, 0, 0, 0};
-        int d = degree, rc = -1;
-        while (d >= 0 && (rc = solve_normal(S, d, coef)) != 0) d--;
-        if (rc != 0) { coef[0] = 0.0; d = 0; }
-        double full[4] = {0, 0, 0, 0};
-        for (int i = 0; i <= d; i++) full[3 - d + i] = coef[i];
-        long long o = ((long long)b * ntiles + p) * 4;
-        for (int i = 0; i < 4; i++) {
-            if (coeffs) coeffs[o + i] = (float)full[i];
-            if (coeffs64) coeffs64[o + i] = full[i];
+        if (sums) {  // joint solve: hand the tile's normal-equation sums to k_register_joint
+            for (int k = 0; k < kRegSums; k++) sums[((long long)b * ntiles + p) * kRegSums + k] = S[k];
+            return;
         }
+        solve_store(S, degree, coeffs, coeffs64, ((long long)b * ntiles + p) * 4);
     }
+}
+
+// SolveDepthToDepth with several active maps (Depth.cpp:1274-1376: every active map's sample
+// grid feeds one problem): the active tiles' sums added in tile order, one solve per panorama.
+__global__ void k_register_joint(const double* __restrict__ sums, const int* __restrict__ active,
+                                 int ntiles, int batch, int degree, float* __restrict__ coeffs,
+                                 double* __restrict__ coeffs64)
+{
+    const int b = blockIdx.x * blockDim.x + threadIdx.x;
+    if (b >= batch) return;
+    double S[kRegSums];
+    for (int k = 0; k < kRegSums; k++) S[k] = 0.0;
+    for (int p = 0; p < ntiles; p++)
+        if (active[p])
+            for (int k = 0; k < kRegSums; k++)
+                S[k] = S[k] + sums[((long long)b * ntiles + p) * kRegSums + k];
+    solve_store(S, degree, coeffs, coeffs64, (long long)b * 4);
 }
 
 // Depth2DepthTransform on all tiles (channel 0), in place.
@@ -521,12 +549,22 @@ void launch_quantize(hipStream_t s, const float* buf, long long bstride, int n, 
 void launch_register(hipStream_t s, const TileGeom* geom, const RegGrid* grids,
                      const GridCol* rcols, const GridRow* rrows, int ntiles, const float* emap,
                      int ew, int eh, int ec, long long estride, const float* tiles,
-                     long long tstride, int degree, float* coeffs, double* coeffs64, int batch)
+                     long long tstride, int degree, float* coeffs, double* coeffs64, int batch,
+                     double* sums)
 {
     dim3 grid(ntiles, batch);
     hipLaunchKernelGGL(k_register, grid, dim3(kRegLanes), 0, s, geom, grids, rcols, rrows,
                        ntiles, emap, ew, eh, ec, estride, tiles, tstride, degree, coeffs,
-                       coeffs64);
+                       coeffs64, sums);
+}
+
+int register_sums_per_tile() { return kRegSums; }
+
+void launch_register_joint(hipStream_t s, const double* sums, const int* active, int ntiles,
+                           int batch, int degree, float* coeffs, double* coeffs64)
+{
+    hipLaunchKernelGGL(k_register_joint, dim3((batch + 63) / 64), dim3(64), 0, s, sums, active,
+                       ntiles, batch, degree, coeffs, coeffs64);
 }
 
 void launch_apply_cubic(hipStream_t s, const TileGeom* geom, int ntiles, long long tile_elems,

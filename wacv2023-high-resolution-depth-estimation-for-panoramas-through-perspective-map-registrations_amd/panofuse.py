@@ -24,7 +24,7 @@ EXPORTS = [
     "pf_version", "pf_set_tiles", "pf_register", "pf_fuse", "pf_merge", "pf_warp_depth",
     "pf_warp_rgb", "pf_level_info", "pf_fuse_partial", "pf_fuse_seed", "pf_fuse_finish_level",
     "pf_probe_taps", "pf_profile_enable", "pf_profile_read", "pf_error_metrics",
-    "pf_depth_transform",
+    "pf_depth_transform", "pf_register_joint",
 ]
 
 STAGES = ["warp", "register", "seed", "targets", "jacobi", "quantize", "metrics"]
@@ -80,6 +80,7 @@ def load():
     L.pf_fuse_finish_level.argtypes = [vp, vp, vp, ip, ip, fp, fp, ip, vp, vp]
     L.pf_probe_taps.argtypes = [vp, ip, ip, fp, fp, ip, vp]
     L.pf_depth_transform.argtypes = [vp, vp, C.c_longlong, ip, vp]
+    L.pf_register_joint.argtypes = [vp, vp, ip, ip, ip, vp, ip, fp, fp, ip, vp, vp, vp]
     L.pf_error_metrics.argtypes = [vp, vp, ip, ip, ip, vp, vp, ip, ip, ip, ip, fp, fp, ip, ip,
                                    vp]
     L.pf_profile_enable.argtypes = [vp, ip]
@@ -205,6 +206,17 @@ class Fuser:
     def warp_rgb(self, pano, tiles):
         B, ph, pw, _ = pano.shape
         self._check(self.L.pf_warp_rgb(self.h, _ptr(pano), pw, ph, B, _ptr(tiles)))
+
+    def register_joint(self, emap, tiles, zr, active, degree=3, coeffs=None, coeffs64=None):
+        """SolveDepthToDepth with the tiles of `active` (list of tile indices) in one problem;
+        coeffs / coeffs64: [B, 4] device tensors."""
+        ew, eh, ec = _emap_dims(emap)
+        B = emap.shape[0]
+        mask = (C.c_int * self.layout.ntiles)(*[1 if i in set(active) else 0
+                                                 for i in range(self.layout.ntiles)])
+        self._check(self.L.pf_register_joint(self.h, _ptr(emap), ew, eh, ec, _ptr(tiles), B,
+                                             float(zr[0]), float(zr[1]), int(degree), mask,
+                                             _ptr(coeffs), _ptr(coeffs64)))
 
     def error_metrics_async(self, gt, given, zr, out, align_way=1, cap_depth=True):
         """pf_error_metrics into out (int32 [B,16] device tensor = B pf_metrics), no sync."""
