@@ -355,8 +355,10 @@ __global__ __launch_bounds__(MB) void k_err_sums(MArgs a, int align_way, const A
             s[5] += 1.0;
         }
         if (v0 > 0 && v1 > 0) {
-            const float r01 = v0 / v1, r10 = v1 / v0;
-            const float rm = r01 > r10 ? r01 : r10;  // MAX2
+            // MAX2(v0 / v1, v1 / v0) with one division: the quotient of the larger by the
+            // smaller is >= 1 and the other <= 1 after rounding (rounding is monotonic), so the
+            // max is exactly fl(larger / smaller)
+            const float rm = v0 > v1 ? v0 / v1 : v1 / v0;
             if ((double)rm >= 1.25) s[6] += 1.0;
             if ((double)rm >= 1.5625) s[7] += 1.0;
             if ((double)rm >= 1.953125) s[8] += 1.0;
