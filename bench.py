@@ -11,10 +11,12 @@ launched on 8 GPUs it is C4 (512 panoramas, 64 per GPU, no collective on the dat
     python bench.py [--gpus N --steps K --warmup W --batch B]
     python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N
 
-Rank 0 prints one JSON line.  `roofline` is for the dominant kernel (the Jacobi sweep):
-algorithmic bytes (12 B per pixel-update) over its hipEvent-measured time inside the
-timed region.  `cpu_baseline` is the CPU oracle (the C restatement of Depth.cpp, OpenMP) running the
-same per-panorama pipeline on this host's cores over a bounded sample.
+Rank 0 prints one JSON line.  `roofline` is for the dominant kernel (the Jacobi sweep) against
+its real roof, VALU issue: algorithmic FLOP (14 per pixel-update) per launch over its average
+hipEvent-measured launch time; `roofline_hbm` puts the same kernel's measured PMC traffic on the
+HBM roof and `effective_hbm` keeps SURVEY.md 8d's 12 B/update as an effective rate.
+`cpu_baseline` is the CPU oracle (the C restatement of Depth.cpp, OpenMP) running the same
+per-panorama pipeline on every usable host core and on one core, over a bounded sample.
 """
 import argparse
 import json
@@ -48,19 +50,28 @@ def parse():
     return ap.parse_args()
 
 
-def cpu_baseline(seconds, out_w=2048, ew=512):
-    """The oracle (C/OpenMP restatement, kind=port) on this host: warp + register + fuse per
-    panorama, until `seconds` of work (at least one panorama)."""
-    sys.path.insert(0, os.path.join(ROOT, "oracle"))
-    import pf_layouts as PL
-    import pf_synth
-    import pyoracle as O
-    threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or min(16, os.cpu_count() or 1)
+def host_cpus():
+    """CPUs this process may run on: the affinity mask, capped by a cgroup-v2 CPU quota when
+    one is set (the GPU box shares its host, and os.cpu_count() reports the whole machine)."""
+    n = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            quota, period = f.read().split()[:2]
+        if quota != "max":
+            n = min(n, max(1, int(-(-int(quota) // int(period)))))
+    except (OSError, ValueError):
+        pass
+    return max(1, n)
+
+
+def _oracle_rate(O, PL, pf_synth, threads, seconds, max_panos, out_w=2048, ew=512):
+    """Panoramas/s of the oracle pipeline (warp + register + fuse) at `threads` OpenMP threads,
+    over at least one panorama and until `seconds` of work or `max_panos` panoramas."""
     O.set_threads(threads)
     lay = PL.config_layout("C2")
     tiles, total = O.make_tiles(lay)
     done, t_work = 0, 0.0
-    while done < 1 or t_work < seconds:
+    while done < 1 or (t_work < seconds and done < max_panos):
         seeds = pf_synth.seeds_for(1, 90000 + done)
         gt = pf_synth.scene_depth(seeds, out_w, out_w // 2)[0].numpy()
         emap = pf_synth.baseline_emap(seeds, ew, ew // 2)[0].numpy()
@@ -70,11 +81,27 @@ def cpu_baseline(seconds, out_w=2048, ew=512):
         O.merge(emap, tiles, data, out_w, PL.ZENITH_RANGE)
         t_work += time.perf_counter() - t0
         done += 1
-        if done >= 32:
-            break
-    return {"value": done / t_work, "unit": "panoramas/s", "cores": threads, "kind": "port",
+    return done / t_work, done, t_work
+
+
+def cpu_baseline(seconds):
+    """The oracle (C/OpenMP restatement of Depth.cpp, kind=port) on this host's cores: the same
+    per-panorama pipeline as the GPU step (warp + registration + 3-level fusion), timed on every
+    CPU this process may use ("all host cores, nproc reported") and on 1 core."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import pf_layouts as PL
+    import pf_synth
+    import pyoracle as O
+    threads = host_cpus()
+    v, done, t_work = _oracle_rate(O, PL, pf_synth, threads, seconds, 64)
+    v1, done1, t1 = _oracle_rate(O, PL, pf_synth, 1, min(seconds, 5.0), 8)
+    return {"value": v, "unit": "panoramas/s", "cores": threads, "kind": "port",
+            "nproc": os.cpu_count(), "cpus_usable": threads,
+            "value_1core": v1,
             "sample": f"{done} panoramas of C2 (2048x1024, 20 tiles of 512^2): warp + registration"
-                      f" + 3-level fusion, {t_work:.1f} s of work, OpenMP {threads} threads"}
+                      f" + 3-level fusion, {t_work:.1f} s of work, OpenMP {threads} threads "
+                      f"(every CPU usable by this process; nproc={os.cpu_count()}); 1 core: "
+                      f"{done1} panoramas in {t1:.1f} s"}
 
 
 def pmc_traffic(family):
@@ -256,6 +283,7 @@ def main():
     jms, jbytes, jlaunch = prof["jacobi"]
     achieved = jbytes / (jms * 1e-3) / 1e9 if jms > 0 else 0.0
     jtf = jbytes / 12.0 * 14.0 / (jms * 1e-3) / 1e12 if jms > 0 else 0.0
+    jtraffic = pmc_traffic("pf::k_jlag")
     wms, wbytes, wlaunch = prof["warp"]  # read 4 B/pano pixel + write 4 B/tile pixel (8d)
     wach = wbytes / (wms * 1e-3) / 1e9 if wms > 0 else 0.0
     stages = {k: {"ms_per_step": v[0] / nprof,
@@ -283,14 +311,34 @@ def main():
                                    f"20 tiles of 512x512 (5x4 layout), 512x256 baseline",
                        "global_batch": B * world, "out": "2048x1024", "tiles": "20x512x512",
                        "parallelism": f"dp{world} (panorama sharding, no collective)"},
-            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS,
-                         "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
+            # Headline: the dominant kernel (k_jlag, the temporally blocked Jacobi) against its
+            # real roof, VALU issue: algorithmic FLOP = 14 fp32 operations per pixel-update as the
+            # reference writes them (Depth.cpp:1680-1717: 4 mul + 4 add for Lcur; sub, mul, add;
+            # 2 mul, add for b'), per average launch, over the hipEvent launch time, against the
+            # vector FP32 peak (MI355X_MICROARCH.md).  `traffic` is the HBM bytes per launch
+            # measured by the rocprofv3 PMC passes (profiles/pmc_traffic.json).
+            "roofline": {"bound": "valu", "achieved": jtf, "peak": VALU_PEAK_TF,
+                         "unit": "TFLOP/s", "frac": jtf / VALU_PEAK_TF,
                          "traffic": pmc_traffic("pf::k_jlag"),
-                         "kernel": "k_jlag (all Jacobi passes of the 3 levels, aggregated)",
+                         "kernel": "k_jlag (all Jacobi passes of the levels, aggregated)",
+                         "flop_per_update": 14,
                          "avg_launch_us": (jms / jlaunch * 1e3) if jlaunch else None,
-                         "bytes_per_launch": (jbytes / jlaunch) if jlaunch else None,
-                         "traffic_source": "profiles/pmc_traffic.json (FETCH_SIZE x2 + WRITE_SIZE, "
+                         "flop_per_launch": (jbytes / 12.0 * 14.0 / jlaunch) if jlaunch else None,
+                         "updates_per_step": jbytes / 12.0 / nprof,
+                         "traffic_source": "profiles/pmc_traffic.json (FETCH_SIZE + WRITE_SIZE, "
                                            "B per launch, averaged over every k_jlag dispatch)"},
+            # the same kernel on the HBM roof with its MEASURED traffic (temporal blocking moves
+            # T sweeps per pass through HBM once), and the 12 B/update algorithmic rate of
+            # SURVEY.md 8d as an "effective" bandwidth (> peak by construction: not a fraction)
+            "roofline_hbm": {"bound": "hbm", "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                             "achieved": (jtraffic / (jms / jlaunch * 1e-3) / 1e9)
+                             if (jtraffic and jlaunch) else None,
+                             "frac": (jtraffic / (jms / jlaunch * 1e-3) / 1e9 / HBM_PEAK_GBS)
+                             if (jtraffic and jlaunch) else None,
+                             "kernel": "k_jlag", "basis": "measured PMC bytes per launch"},
+            "effective_hbm": {"achieved": achieved, "unit": "GB/s",
+                              "basis": "12 B per pixel-update (SURVEY.md 8d) / Jacobi time; "
+                                       "temporal blocking keeps T-1 of every T sweeps on chip"},
             # north_star's named target: >= 60% of the HBM roofline on the warp kernel
             "roofline_warp": {"bound": "hbm", "achieved": wach, "peak": HBM_PEAK_GBS,
                               "unit": "GB/s", "frac": wach / HBM_PEAK_GBS,
@@ -298,15 +346,6 @@ def main():
                               "kernel": "k_warp_depth",
                               "avg_launch_us": (wms / wlaunch * 1e3) if wlaunch else None,
                               "bytes_per_launch": (wbytes / wlaunch) if wlaunch else None},
-            # the Jacobi sweep's real bound is VALU issue (temporal blocking moves it off the
-            # HBM roof): algorithmic FLOP = 14 fp32 operations per pixel-update as the
-            # reference writes them (Depth.cpp:1680-1717: 4 mul + 4 add for Lcur, sub, mul,
-            # add, 2 mul, add for b'), against the vector FP32 peak (MI355X_MICROARCH.md)
-            "roofline_valu": {"bound": "valu", "achieved": jtf, "peak": VALU_PEAK_TF,
-                              "unit": "TFLOP/s", "frac": jtf / VALU_PEAK_TF,
-                              "kernel": "k_jlag (all Jacobi passes of the 3 levels, aggregated)",
-                              "flop_per_update": 14,
-                              "updates_per_step": jbytes / 12.0 / nprof},
             "stages": stages,
             # metrics stage (outside the timed step): algorithmic bytes = one read of the
             # compared band of gt (4 B) and result (2 B) per pixel; the kernels make 4 passes

@@ -6,6 +6,7 @@ reference (section 6, Appendix A/C) and by independent re-derivations (numpy lst
 registration, a numpy Jacobi for the sweep, the committed regression fixture).
 """
 import os
+import sys
 
 import numpy as np
 import pytest
@@ -208,3 +209,21 @@ def test_golden_fixture_regression():
         lv = O.level_dims(512, 256, ZR, level)
         got = hashlib.sha256(O.probe_taps(tiles, lv).tobytes()).digest()
         assert got == g[f"taps_sha256_l{level}"].tobytes()
+
+
+def test_golden_large_regression():
+    """The committed 4-level checksums (tools/make_golden_large.py): the W4096 case is re-run
+    here in full (SHA-256 of the u16 output and its strided subsample); the C5 case is checked
+    on the GPU box (tests/test_gpu_configs.py), which runs the oracle beside the kernel."""
+    import hashlib
+    sys.path.insert(0, os.path.join(ROOT, "tools"))
+    import make_golden_large as G
+    g = np.load(os.path.join(ROOT, "tests", "golden", "large_merge.npz"))
+    O.set_threads(min(8, os.cpu_count() or 1))
+    lay, tiles, emap, data, out_w = G.case_inputs("W4096")
+    assert hashlib.sha256(np.concatenate([emap.ravel(), data.ravel()]).tobytes()).digest() == \
+        g["W4096_in_sha256"].tobytes()
+    out, abcd = O.merge(emap, tiles, data.copy(), out_w, ZR)
+    assert np.array_equal(abcd, g["W4096_abcd"])
+    assert np.array_equal(out.ravel()[::int(g["stride"])], g["W4096_out_sub"])
+    assert hashlib.sha256(out.tobytes()).digest() == g["W4096_out_sha256"].tobytes()
