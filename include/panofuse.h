@@ -63,11 +63,21 @@ const char* pf_version(void);
 int pf_set_tiles(pf_ctx* ctx, const pf_window* fovs, const pf_window* ranges, int ntiles,
                  const int* tile_w, const int* tile_h, int tile_c, int cap_ranges);
 
+/* Registration solver for degree 3 (the reference's cubic FunctorDepth2Depth3):
+ *   PF_SOLVER_LM (default) -- the reference's Ceres 1.13 Levenberg-Marquardt (DENSE_SCHUR,
+ *     default options, from (1,1,1,1); Depth.cpp:1270-1274, 1399-1404), run per tile from the
+ *     fp64 moment sums of its samples;
+ *   PF_SOLVER_NORMAL -- the exact least-squares minimiser (fp64 normal equations).
+ * Lower degrees always take the normal equations (the reference has no lower-degree solve). */
+#define PF_SOLVER_NORMAL 0
+#define PF_SOLVER_LM 1
+int pf_set_solver(pf_ctx* ctx, int solver);
+
 /* SolveDepthToDepth (Depth.cpp:1261-1414) for every tile with only that tile active
- * (MergeDepthMaps' loop, Depth.cpp:794-805), closed-form fp64 least squares of degree
- * `degree` (3 = the reference's FunctorDepth2Depth3; 1 = scale/shift); coeffs may be NULL.
- * coeffs64 (optional, [batch][ntiles][4] doubles) receives the unrounded solution.
- * apply != 0 then runs Depth2DepthTransform (Depth.cpp:245-274) on the tiles in place. */
+ * (MergeDepthMaps' loop, Depth.cpp:794-805), fp64 least squares of degree `degree`
+ * (3 = the reference's FunctorDepth2Depth3, with the context's solver; 1 = scale/shift);
+ * coeffs may be NULL.  coeffs64 (optional, [batch][ntiles][4] doubles) receives the unrounded
+ * solution.  apply != 0 then runs Depth2DepthTransform (Depth.cpp:245-274) on the tiles. */
 int pf_register(pf_ctx* ctx, const float* emap, int ew, int eh, int ec, float* tiles,
                 int batch, float zr0, float zr1, int degree, int apply, float* coeffs,
                 double* coeffs64);

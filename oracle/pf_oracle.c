@@ -258,10 +258,10 @@ int pfo_reg_samples(const pfo_tile* t, const float* tiles, const float* emap, in
 }
 
 #define REG_LANES 256
-#define REG_NSUM 14
+#define REG_NSUM 15
 
 /* Jacobian row J = (X3, X2, X, 1) of FunctorDepth2Depth3 (Depth.cpp:1124-1130, Weight = 1):
- * X2 = x*x, X3 = x*x*x.  The 14 sums are the upper triangle of J^T J and J^T y. */
+ * X2 = x*x, X3 = x*x*x.  The 15 sums are the upper triangle of J^T J, J^T y and y^T y. */
 static inline void reg_terms(double x, double y, double o[REG_NSUM])
 {
     double X = x, X2 = x * x, X3 = x * x * x;
@@ -269,6 +269,7 @@ static inline void reg_terms(double x, double y, double o[REG_NSUM])
     o[4] = X2 * X2; o[5] = X2 * X;  o[6] = X2;
     o[7] = X * X;   o[8] = X;       o[9] = 1.0;
     o[10] = X3 * y; o[11] = X2 * y; o[12] = X * y; o[13] = y;
+    o[14] = y * y;
 }
 
 /* Solve the (deg+1)x(deg+1) normal equations by partially pivoted Gaussian elimination.
@@ -307,6 +308,14 @@ static int solve_normal(const double S[REG_NSUM], int degree, double* coef)
 int pfo_register_tile(const pfo_tile* t, const float* tiles, const float* emap, int ew, int eh,
                       int ec, float zr0, float zr1, int degree, double* coef64, float* abcd)
 {
+    return pfo_register_tile_solver(t, tiles, emap, ew, eh, ec, zr0, zr1, degree,
+                                    PFO_SOLVER_NORMAL, coef64, abcd);
+}
+
+int pfo_register_tile_solver(const pfo_tile* t, const float* tiles, const float* emap, int ew,
+                             int eh, int ec, float zr0, float zr1, int degree, int solver,
+                             double* coef64, float* abcd)
+{
     int cols, rows;
     float zt, zd;
     int ns = pfo_reg_grid(t, zr0, zr1, &cols, &rows, &zt, &zd);
@@ -328,6 +337,16 @@ int pfo_register_tile(const pfo_tile* t, const float* tiles, const float* emap, 
             for (int k = 0; k < REG_NSUM; k++) part[l][k] = part[l][k] + part[l + stride][k];
     free(xs);
     free(ys);
+    if (solver == PFO_SOLVER_LM && degree == 3) {
+        /* the reference's solver: Ceres LM from (1,1,1,1), in the moment form (pf_oracle_lm.c) */
+        double c[4];
+        pfo_lm_moments(part[0], c, NULL);
+        for (int i = 0; i < 4; i++) {
+            if (coef64) coef64[i] = c[i];
+            abcd[i] = (float)c[i];
+        }
+        return 3;
+    }
     double coef[4] = {0, 0, 0, 0};
     int d = degree, rc = -1;
     while (d >= 0 && (rc = solve_normal(part[0], d, coef)) != 0) d--; /* rank-deficient fallback */
@@ -585,13 +604,13 @@ int pfo_solve_depth_all(const float* emap, int ew, int eh, int ec, const pfo_til
 }
 
 int pfo_merge(const float* emap, int ew, int eh, int ec, const pfo_tile* tiles, int ntiles,
-              float* tile_data, int out_w, float zr0, float zr1, int degree, uint16_t* out,
-              float* abcd_out)
+              float* tile_data, int out_w, float zr0, float zr1, int degree, int solver,
+              uint16_t* out, float* abcd_out)
 { /* Depth.cpp:789-913 */
     for (int p = 0; p < ntiles; p++) {
         float abcd[4];
-        if (pfo_register_tile(&tiles[p], tile_data, emap, ew, eh, ec, zr0, zr1, degree, NULL,
-                              abcd) < 0)
+        if (pfo_register_tile_solver(&tiles[p], tile_data, emap, ew, eh, ec, zr0, zr1, degree,
+                                     solver, NULL, abcd) < 0)
             return -2;
         pfo_depth_to_depth(&tiles[p], tile_data, abcd);
         if (abcd_out) memcpy(abcd_out + 4 * p, abcd, sizeof(abcd));

@@ -74,7 +74,35 @@ int  pfo_reg_samples(const pfo_tile* t, const float* tiles, const float* emap, i
  * the Vec4f rounding (Depth.cpp:1408) padded with leading zeros to 4 floats. */
 int  pfo_register_tile(const pfo_tile* t, const float* tiles, const float* emap, int ew, int eh,
                        int ec, float zr0, float zr1, int degree, double* coef64, float* abcd);
+/* Solver selection (degree 3 only; lower degrees always take the normal equations):
+ * PFO_SOLVER_NORMAL = the fp64 normal equations above; PFO_SOLVER_LM = the reference's Ceres LM
+ * run from the same moment sums (pfo_lm_moments, pf_oracle_lm.c) -- the HIP default. */
+enum { PFO_SOLVER_NORMAL = 0, PFO_SOLVER_LM = 1 };
+int  pfo_register_tile_solver(const pfo_tile* t, const float* tiles, const float* emap, int ew,
+                              int eh, int ec, float zr0, float zr1, int degree, int solver,
+                              double* coef64, float* abcd);
 void pfo_depth_to_depth(const pfo_tile* t, float* tiles, const float abcd[4]);
+
+/* The reference's registration solver itself: Ceres 1.13 trust-region Levenberg-Marquardt with
+ * DENSE_SCHUR and default options from (1,1,1,1) (pf_oracle_lm.c cites each rule it restates). */
+enum { PFO_LM_NO_CONVERGENCE = 0, PFO_LM_FUNCTION_TOL = 1, PFO_LM_PARAMETER_TOL = 2,
+       PFO_LM_GRADIENT_TOL = 3, PFO_LM_MIN_RADIUS = 4, PFO_LM_FAILURE = 5 };
+typedef struct pfo_lm_summary {
+    int iterations, successful, unsuccessful, termination;
+    double initial_cost, final_cost;
+} pfo_lm_summary;
+/* Fit of y ~ a x^3 + b x^2 + c x + d over the samples (FunctorDepth2Depth3 residuals),
+ * sample-wise exactly as Ceres evaluates it. */
+int  pfo_lm_fit(const double* xs, const double* ys, int n, double coef[4], pfo_lm_summary* s);
+int  pfo_register_tile_lm(const pfo_tile* t, const float* tiles, const float* emap, int ew,
+                          int eh, int ec, float zr0, float zr1, double* coef64, float* abcd,
+                          pfo_lm_summary* s);
+/* The same LM run from the 15 moment sums (J'J upper triangle, J'y, y'y): the HIP kernel's form. */
+int  pfo_lm_moments(const double S[15], double coef[4], pfo_lm_summary* s);
+/* MergeDepthMaps core with the sample-wise LM registration (tile_data transformed in place). */
+int  pfo_merge_lm(const float* emap, int ew, int eh, int ec, const pfo_tile* tiles, int ntiles,
+                  float* tile_data, int out_w, float zr0, float zr1, uint16_t* out,
+                  float* abcd_out);
 
 /* ---------------- fusion (Depth.cpp:1416-1771) ---------------- */
 typedef struct pfo_level {
@@ -104,8 +132,8 @@ int  pfo_solve_depth_all(const float* emap, int ew, int eh, int ec, const pfo_ti
 /* MergeDepthMaps core (Depth.cpp:789-913): per-tile registration + transform, then fusion.
  * tile_data is modified in place (as the reference's pmaps are). */
 int  pfo_merge(const float* emap, int ew, int eh, int ec, const pfo_tile* tiles, int ntiles,
-               float* tile_data, int out_w, float zr0, float zr1, int degree, uint16_t* out,
-               float* abcd_out);
+               float* tile_data, int out_w, float zr0, float zr1, int degree, int solver,
+               uint16_t* out, float* abcd_out);
 
 /* ---------------- E->P depth warp (a5 mapping, Depth.cpp:157-166 + 2960-2971) ------------ */
 void pfo_warp_depth(const float* pano, int pw, int ph, const pfo_tile* tiles, int ntiles,

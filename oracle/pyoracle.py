@@ -35,6 +35,15 @@ class Level(C.Structure):
                 ("iters", C.c_int), ("max_level", C.c_int)]
 
 
+class LmSummary(C.Structure):
+    _fields_ = [("iterations", C.c_int), ("successful", C.c_int), ("unsuccessful", C.c_int),
+                ("termination", C.c_int), ("initial_cost", C.c_double),
+                ("final_cost", C.c_double)]
+
+
+LM_TERMINATION = ("no_convergence", "function_tolerance", "parameter_tolerance",
+                  "gradient_tolerance", "min_trust_region_radius", "failure")
+
 _lib = None
 
 
@@ -64,6 +73,9 @@ def lib():
                                       C.c_float, dp, dp]
         L.pfo_register_tile.argtypes = [TP, fp, fp, C.c_int, C.c_int, C.c_int, C.c_float,
                                         C.c_float, C.c_int, dp, fp]
+        L.pfo_register_tile_solver.argtypes = [TP, fp, fp, C.c_int, C.c_int, C.c_int, C.c_float,
+                                               C.c_float, C.c_int, C.c_int, dp, fp]
+        L.pfo_lm_moments.argtypes = [dp, dp, C.POINTER(LmSummary)]
         L.pfo_depth_to_depth.argtypes = [TP, fp, fp]
         L.pfo_level_dims.argtypes = [C.c_int, C.c_int, C.c_float, C.c_float, C.c_int,
                                      C.POINTER(Level)]
@@ -80,7 +92,8 @@ def lib():
                                           C.c_int, C.c_int, C.c_float, C.c_float,
                                           C.POINTER(C.c_uint16), C.POINTER(C.c_longlong)]
         L.pfo_merge.argtypes = [fp, C.c_int, C.c_int, C.c_int, TP, C.c_int, fp, C.c_int,
-                                C.c_float, C.c_float, C.c_int, C.POINTER(C.c_uint16), fp]
+                                C.c_float, C.c_float, C.c_int, C.c_int, C.POINTER(C.c_uint16),
+                                fp]
         L.pfo_warp_depth.argtypes = [fp, C.c_int, C.c_int, TP, C.c_int, C.POINTER(Response), fp]
         L.pfo_warp_rgb.argtypes = [C.POINTER(C.c_uint8), C.c_int, C.c_int, TP, C.c_int,
                                    C.POINTER(C.c_uint8)]
@@ -88,6 +101,11 @@ def lib():
         L.pfo_hash32.restype = C.c_uint32
         L.pfo_set_threads.argtypes = [C.c_int]
         L.pfo_nan_marker.restype = C.c_uint32
+        L.pfo_lm_fit.argtypes = [dp, dp, C.c_int, dp, C.POINTER(LmSummary)]
+        L.pfo_register_tile_lm.argtypes = [TP, fp, fp, C.c_int, C.c_int, C.c_int, C.c_float,
+                                           C.c_float, dp, fp, C.POINTER(LmSummary)]
+        L.pfo_merge_lm.argtypes = [fp, C.c_int, C.c_int, C.c_int, TP, C.c_int, fp, C.c_int,
+                                   C.c_float, C.c_float, C.POINTER(C.c_uint16), fp]
         L.pfo_error_metrics.argtypes = [fp, C.c_int, C.c_int, C.c_int, fp, C.POINTER(C.c_uint16),
                                         C.c_int, C.c_int, C.c_int, C.c_float, C.c_float,
                                         C.c_int, C.c_int, fp, C.POINTER(C.c_int)]
@@ -191,14 +209,29 @@ def solve_depth_all(emap, tiles, tile_data, out_w, zr):
     return out.reshape(out_w // 2, out_w), oops.value
 
 
-def register_tile(tile, tile_data, emap, zr, degree=3):
+SOLVERS = {"normal": 0, "lm": 1}  # PFO_SOLVER_*; "lm" (the reference's Ceres LM) is the default
+
+
+def register_tile(tile, tile_data, emap, zr, degree=3, solver="lm"):
+    """SolveDepthToDepth for one tile from the fixed-order moment sums: (c64, abcd, degree)."""
     eh, ew = emap.shape[:2]
     ec = emap.shape[2] if emap.ndim == 3 else 1
     c64 = np.zeros(4, np.float64)
     abcd = np.zeros(4, np.float32)
-    d = lib().pfo_register_tile(C.byref(tile), _p(tile_data), _p(np.ascontiguousarray(emap, np.float32)),
-                                ew, eh, ec, zr[0], zr[1], degree, _p(c64, C.c_double), _p(abcd))
+    d = lib().pfo_register_tile_solver(C.byref(tile), _p(tile_data),
+                                       _p(np.ascontiguousarray(emap, np.float32)), ew, eh, ec,
+                                       zr[0], zr[1], degree, SOLVERS[solver],
+                                       _p(c64, C.c_double), _p(abcd))
     return c64, abcd, d
+
+
+def lm_moments(S):
+    """Moment-form LM (the HIP kernel's form) on 15 sums: (coef[4], summary dict)."""
+    S = np.ascontiguousarray(S, np.float64)
+    c = np.zeros(4, np.float64)
+    s = LmSummary()
+    lib().pfo_lm_moments(_p(S, C.c_double), _p(c, C.c_double), C.byref(s))
+    return c, _lm_dict(s)
 
 
 def reg_samples(tile, tile_data, emap, zr):
@@ -216,11 +249,57 @@ def reg_samples(tile, tile_data, emap, zr):
     return xs, ys, cols.value, rows.value
 
 
+def lm_fit(xs, ys):
+    """Ceres-LM restatement (pf_oracle_lm.c) on samples: (coef[4] fp64, summary dict)."""
+    xs = np.ascontiguousarray(xs, np.float64)
+    ys = np.ascontiguousarray(ys, np.float64)
+    c = np.zeros(4, np.float64)
+    s = LmSummary()
+    if lib().pfo_lm_fit(_p(xs, C.c_double), _p(ys, C.c_double), xs.size, _p(c, C.c_double),
+                        C.byref(s)) != 0:
+        raise ValueError("pfo_lm_fit failed")
+    return c, _lm_dict(s)
+
+
+def _lm_dict(s):
+    return {"iterations": s.iterations, "successful": s.successful,
+            "unsuccessful": s.unsuccessful, "termination": LM_TERMINATION[s.termination],
+            "initial_cost": s.initial_cost, "final_cost": s.final_cost}
+
+
+def register_tile_lm(tile, tile_data, emap, zr):
+    """SolveDepthToDepth for one tile with the Ceres-LM restatement: (c64, abcd f32, summary)."""
+    eh, ew = emap.shape[:2]
+    ec = emap.shape[2] if emap.ndim == 3 else 1
+    c64 = np.zeros(4, np.float64)
+    abcd = np.zeros(4, np.float32)
+    s = LmSummary()
+    if lib().pfo_register_tile_lm(C.byref(tile), _p(tile_data),
+                                  _p(np.ascontiguousarray(emap, np.float32)), ew, eh, ec, zr[0],
+                                  zr[1], _p(c64, C.c_double), _p(abcd), C.byref(s)) != 0:
+        raise ValueError("pfo_register_tile_lm failed")
+    return c64, abcd, _lm_dict(s)
+
+
+def merge_lm(emap, tiles, tile_data, out_w, zr):
+    """MergeDepthMaps core with the Ceres-LM registration; tile_data is transformed in place."""
+    eh, ew = emap.shape[:2]
+    ec = emap.shape[2] if emap.ndim == 3 else 1
+    out = np.zeros(out_w * (out_w // 2), np.uint16)
+    abcd = np.zeros(4 * len(tiles), np.float32)
+    rc = lib().pfo_merge_lm(_p(np.ascontiguousarray(emap, np.float32)), ew, eh, ec, tiles,
+                            len(tiles), _p(tile_data), out_w, zr[0], zr[1],
+                            _p(out, C.c_uint16), _p(abcd))
+    if rc != 0:
+        raise ValueError(f"pfo_merge_lm rc={rc}")
+    return out.reshape(out_w // 2, out_w), abcd.reshape(-1, 4)
+
+
 def depth_to_depth(tile, tile_data, abcd):
     lib().pfo_depth_to_depth(C.byref(tile), _p(tile_data), _p(np.asarray(abcd, np.float32)))
 
 
-def merge(emap, tiles, tile_data, out_w, zr, degree=3):
+def merge(emap, tiles, tile_data, out_w, zr, degree=3, solver="lm"):
     """MergeDepthMaps core; tile_data is transformed in place."""
     eh, ew = emap.shape[:2]
     ec = emap.shape[2] if emap.ndim == 3 else 1
@@ -228,7 +307,7 @@ def merge(emap, tiles, tile_data, out_w, zr, degree=3):
     abcd = np.zeros(4 * len(tiles), np.float32)
     rc = lib().pfo_merge(_p(np.ascontiguousarray(emap, np.float32)), ew, eh, ec, tiles,
                          len(tiles), _p(tile_data), out_w, zr[0], zr[1], degree,
-                         _p(out, C.c_uint16), _p(abcd))
+                         SOLVERS[solver], _p(out, C.c_uint16), _p(abcd))
     if rc != 0:
         raise ValueError(f"pfo_merge rc={rc}")
     return out.reshape(out_w // 2, out_w), abcd.reshape(-1, 4)

@@ -114,9 +114,11 @@ def test_register_bit_exact(fuser, cfg):
 
 
 def test_register_degree1_and_lstsq(fuser):
-    """Scale/shift mode (north_star's 2x2 system) and agreement with an fp64 lstsq."""
+    """Scale/shift mode (north_star's 2x2 system) and agreement with an fp64 lstsq (the
+    normal-equation solver; the default LM solver is checked in test_gpu_lm.py)."""
     lay, emap, gt, tiles, total, data, _ = _inputs("C1")
     fuser.set_tiles(lay)
+    fuser.set_solver("normal")
     for degree in (1, 2, 3):
         coeffs = torch.zeros((1, lay.ntiles, 4), dtype=torch.float32, device=DEV)
         c64 = torch.zeros((1, lay.ntiles, 4), dtype=torch.float64, device=DEV)
@@ -128,6 +130,7 @@ def test_register_degree1_and_lstsq(fuser):
             sol, *_ = np.linalg.lstsq(A, ys, rcond=None)
             got = c64.cpu().numpy()[0, p][3 - degree:]
             assert np.max(np.abs(A @ got - A @ sol)) < 1e-6
+    fuser.set_solver("lm")
 
 
 @pytest.mark.parametrize("cfg", ["C1", "C2"])
@@ -446,6 +449,7 @@ def test_register_joint_matches_lstsq(fuser):
     pf_register's per-tile solve bit for bit."""
     lay, emap, gt, tiles, total, data, _ = _inputs("C1")
     fuser.set_tiles(lay)
+    fuser.set_solver("normal")
     t_emap, t_data = _dev(emap)[None], _dev(data)[None].contiguous()
     for active in ([0, 2], [1, 3, 4], list(range(lay.ntiles))):
         c64 = torch.zeros((1, 4), dtype=torch.float64, device=DEV)
@@ -459,6 +463,7 @@ def test_register_joint_matches_lstsq(fuser):
         A = np.stack([xs ** k for k in range(3, -1, -1)], 1)
         sol, *_ = np.linalg.lstsq(A, ys, rcond=None)
         assert np.max(np.abs(A @ c64.cpu().numpy()[0] - A @ sol)) < 1e-6, active
+    fuser.set_solver("lm")
     per = torch.zeros((1, lay.ntiles, 4), dtype=torch.float32, device=DEV)
     fuser.register(t_emap, t_data, ZR, apply=False, coeffs=per)
     one = torch.zeros((1, 4), dtype=torch.float32, device=DEV)

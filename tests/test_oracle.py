@@ -116,7 +116,7 @@ def test_registration_matches_lstsq():
         xs, ys, cols, rows = O.reg_samples(tiles[p], data, emap, ZR)
         assert xs.size == (cols + 1) * (rows + 1)
         assert xs.min() >= 1e-4 and xs.max() <= 1 - 1e-4
-        c64, abcd, deg = O.register_tile(tiles[p], data, emap, ZR)
+        c64, abcd, deg = O.register_tile(tiles[p], data, emap, ZR, solver="normal")
         assert deg == 3
         A = np.stack([xs ** 3, xs ** 2, xs, np.ones_like(xs)], 1)
         sol, *_ = np.linalg.lstsq(A, ys, rcond=None)
@@ -129,8 +129,13 @@ def test_registration_rank_deficient_falls_back():
     tiles, total = O.make_tiles(lay)
     data = np.full(total, 0.5, np.float32)  # constant tile: only the constant term is defined
     emap = np.full((64, 128), 0.25, np.float32)
-    c64, abcd, deg = O.register_tile(tiles[0], data, emap, ZR)
+    c64, abcd, deg = O.register_tile(tiles[0], data, emap, ZR, solver="normal")
     assert deg == 0 and abs(c64[3] - 0.25) < 1e-12 and not c64[:3].any()
+    # the reference's solver (Ceres LM, damped) needs no fallback: it stops at a point that fits
+    c64, abcd, deg = O.register_tile(tiles[0], data, emap, ZR, solver="lm")
+    assert deg == 3
+    x = 0.5
+    assert abs(((c64[0] * x + c64[1]) * x + c64[2]) * x + c64[3] - 0.25) < 1e-5
 
 
 def _numpy_jacobi(buf, Lnorm, lv, iters):

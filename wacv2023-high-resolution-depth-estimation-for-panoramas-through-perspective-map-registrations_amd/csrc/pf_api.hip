@@ -49,6 +49,7 @@ struct pf_ctx {
     std::string err;
     // layout
     int ntiles = 0, tile_c = 1;
+    int solver = PF_SOLVER_LM;  // degree-3 registration solver (pf_set_solver)
     std::vector<pf_window> fov, rng;
     std::vector<int> tw_h, th_h;
     bool layout_ok = false;  // the stored layout was set completely
@@ -355,6 +356,15 @@ void pf_destroy(pf_ctx* c)
 }
 
 const char* pf_last_error(const pf_ctx* c) { return c ? c->err.c_str() : "null context"; }
+
+int pf_set_solver(pf_ctx* c, int solver)
+{
+    if (!c) return PF_EINVAL;
+    if (solver != PF_SOLVER_LM && solver != PF_SOLVER_NORMAL)
+        return fail(c, PF_EINVAL, "pf_set_solver: unknown solver %d", solver);
+    c->solver = solver;
+    return PF_OK;
+}
 
 int pf_set_stream(pf_ctx* c, void* s)
 {
@@ -1080,8 +1090,8 @@ int pf_register(pf_ctx* c, const float* emap, int ew, int eh, int ec, float* til
                      apply ? 2 : 1);
         launch_register(c->stream, (const TileGeom*)c->geom.p, (const RegGrid*)c->reg.p,
                         (const GridCol*)c->rcols.p, (const GridRow*)c->rrows.p, c->ntiles, emap,
-                        ew, eh, ec, (long long)ew * eh * ec, tiles, c->tile_elems, degree, cf,
-                        coeffs64, batch);
+                        ew, eh, ec, (long long)ew * eh * ec, tiles, c->tile_elems, degree,
+                        c->solver, cf, coeffs64, batch);
         if (apply)
             launch_apply_cubic(c->stream, (const TileGeom*)c->geom.p, c->ntiles,
                                c->tile_elems / c->tile_c, tiles, c->tile_elems, cf, batch);
@@ -1340,10 +1350,10 @@ int pf_register_joint(pf_ctx* c, const float* emap, int ew, int eh, int ec, cons
     }
     launch_register(c->stream, (const TileGeom*)c->geom.p, (const RegGrid*)c->reg.p,
                     (const GridCol*)c->rcols.p, (const GridRow*)c->rrows.p, c->ntiles, emap, ew,
-                    eh, ec, (long long)ew * eh * ec, tiles, c->tile_elems, degree, nullptr,
-                    nullptr, batch, (double*)c->reg_sums.p);
+                    eh, ec, (long long)ew * eh * ec, tiles, c->tile_elems, degree, c->solver,
+                    nullptr, nullptr, batch, (double*)c->reg_sums.p);
     launch_register_joint(c->stream, (const double*)c->reg_sums.p, (const int*)c->reg_active.p,
-                          c->ntiles, batch, degree, cf, coeffs64);
+                          c->ntiles, batch, degree, c->solver, cf, coeffs64);
     HIPCHK(c, hipGetLastError());
     return PF_OK;
 }

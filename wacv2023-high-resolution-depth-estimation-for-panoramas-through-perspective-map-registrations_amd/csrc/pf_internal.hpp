@@ -196,11 +196,11 @@ void launch_quantize(hipStream_t s, const float* buf, long long bstride, int n, 
 void launch_register(hipStream_t s, const TileGeom* geom, const RegGrid* grids,
                      const GridCol* rcols, const GridRow* rrows, int ntiles, const float* emap,
                      int ew, int eh, int ec, long long estride, const float* tiles,
-                     long long tstride, int degree, float* coeffs, double* coeffs64,
+                     long long tstride, int degree, int solver, float* coeffs, double* coeffs64,
                      int batch, double* sums = nullptr);
 int register_sums_per_tile();
 void launch_register_joint(hipStream_t s, const double* sums, const int* active, int ntiles,
-                           int batch, int degree, float* coeffs, double* coeffs64);
+                           int batch, int degree, int solver, float* coeffs, double* coeffs64);
 void launch_apply_cubic(hipStream_t s, const TileGeom* geom, int ntiles, long long tile_elems,
                         float* tiles, long long tstride, const float* coeffs, int batch);
 int warp_patch_edge();

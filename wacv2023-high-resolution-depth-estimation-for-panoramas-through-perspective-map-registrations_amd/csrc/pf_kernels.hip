@@ -264,12 +264,12 @@ __global__ void __launch_bounds__(kBlock) k_quantize(const float* __restrict__ b
 }
 
 // ---------------------------------------------------------------------------------------------
-// Registration: one workgroup per (tile, panorama).  Lane l accumulates the 14 fp64 sums of
-// J^T J / J^T y over samples l, l+256, ... (J = (x^3, x^2, x, 1) of FunctorDepth2Depth3,
-// Depth.cpp:1122-1138), then a fixed pairwise tree; lane 0 solves the normal equations.  The
-// order is fixed, so the result is reproducible and identical to the oracle's restatement.
+// Registration: one workgroup per (tile, panorama).  Lane l accumulates the 15 fp64 sums of
+// J^T J / J^T y / y^T y over samples l, l+256, ... (J = (x^3, x^2, x, 1) of FunctorDepth2Depth3,
+// Depth.cpp:1122-1138), then a fixed pairwise tree; lane 0 solves.  The order is fixed, so the
+// result is reproducible and identical to the oracle's restatement.
 static constexpr int kRegLanes = 256;
-static constexpr int kRegSums = 14;
+static constexpr int kRegSums = 15;
 
 __device__ __forceinline__ double clamp_depth(double v)
 {
@@ -308,11 +308,219 @@ __device__ int solve_normal(const double* S, int degree, double* coef)
     return 0;
 }
 
+
+// ---------------------------------------------------------------------------------------------
+// The reference's registration solver: Ceres 1.13 trust-region Levenberg-Marquardt, DENSE_SCHUR,
+// default options, from (1,1,1,1) (Depth.cpp:1270-1274, 1399-1404), evaluated from the 15 moment
+// sums -- the residuals are linear in (a,b,c,d), so cost, gradient and J'J are exact functions of
+// them.  Every rule (Jacobi column scaling, LM diagonal and radius updates, step validity and
+// quality, the parameter/function/gradient tolerances, returning the best accepted point) is
+// cited in oracle/pf_oracle_lm.c, whose pfo_lm_moments is this function operation for operation
+// (fp64 +, -, *, /, sqrt only, no contraction), so the two agree bit for bit.
+namespace {
+constexpr int kLmMaxIter = 50;
+constexpr double kLmInitRadius = 1e4, kLmMaxRadius = 1e16, kLmMinRadius = 1e-32;
+constexpr double kLmMinRelDecrease = 1e-3, kLmMinDiag = 1e-6, kLmMaxDiag = 1e32;
+constexpr int kLmMaxInvalid = 5;
+constexpr double kLmFuncTol = 1e-6, kLmGradTol = 1e-10, kLmParamTol = 1e-8;
+
+struct Mom {
+    double M[4][4], Jy[4], yy;
+};
+
+__device__ double mom_cost(const Mom& m, const double p[4])
+{
+    double pMp = 0.0, pJy = 0.0;
+    for (int i = 0; i < 4; i++) {
+        double q = 0.0;
+        for (int j = 0; j < 4; j++) q = q + m.M[i][j] * p[j];
+        pMp = pMp + p[i] * q;
+        pJy = pJy + p[i] * m.Jy[i];
+    }
+    return 0.5 * ((m.yy - 2.0 * pJy) + pMp);
+}
+
+__device__ void mom_gradient(const Mom& m, const double p[4], double g[4])
+{
+    for (int i = 0; i < 4; i++) {
+        double q = 0.0;
+        for (int j = 0; j < 4; j++) q = q + m.M[i][j] * p[j];
+        g[i] = q - m.Jy[i];
+    }
+}
+
+__device__ double inv_psd1(double v)
+{  // Eigen LLT of a 1x1 block solved against 1 (InvertPSDMatrix, full rank)
+    const double l = sqrt(v);
+    return (1.0 / l) / l;
+}
+
+__device__ bool llt3_solve(double S[3][3], const double rhs[3], double z[3])
+{  // Eigen LLT<Upper> of the 3x3 reduced Schur system (schur_complement_solver.cc:197-213)
+    double L[3][3] = {{0, 0, 0}, {0, 0, 0}, {0, 0, 0}};
+    for (int k = 0; k < 3; k++) {
+        double x = S[k][k];
+        if (k > 0) {
+            double sq = 0.0;
+            for (int i = 0; i < k; i++) sq = sq + L[k][i] * L[k][i];
+            x = x - sq;
+        }
+        if (!(x > 0.0)) return false;
+        L[k][k] = x = sqrt(x);
+        for (int j = k + 1; j < 3; j++) {
+            double a = S[k][j];
+            for (int i = 0; i < k; i++) a = a - L[j][i] * L[k][i];
+            L[j][k] = a / x;
+        }
+    }
+    double y[3] = {rhs[0], rhs[1], rhs[2]};
+    for (int k = 0; k < 3; k++) {
+        y[k] = y[k] / L[k][k];
+        for (int j = k + 1; j < 3; j++) y[j] = y[j] - L[j][k] * y[k];
+    }
+    for (int k = 2; k >= 0; k--) {
+        y[k] = y[k] / L[k][k];
+        for (int j = 0; j < k; j++) y[j] = y[j] - L[k][j] * y[k];
+    }
+    z[0] = y[0]; z[1] = y[1]; z[2] = y[2];
+    return true;
+}
+
+__device__ double norm4(const double v[4])
+{
+    return sqrt(v[0] * v[0] + v[1] * v[1] + v[2] * v[2] + v[3] * v[3]);
+}
+}  // namespace
+
+__device__ void lm_moments(const double* S, double coef[4])
+{
+    Mom m;
+    const int idx[4][4] = {{0, 1, 2, 3}, {1, 4, 5, 6}, {2, 5, 7, 8}, {3, 6, 8, 9}};
+    for (int i = 0; i < 4; i++) {
+        for (int j = 0; j < 4; j++) m.M[i][j] = S[idx[i][j]];
+        m.Jy[i] = S[10 + i];
+    }
+    m.yy = S[14];
+    double x[4] = {1.0, 1.0, 1.0, 1.0}, best[4] = {1.0, 1.0, 1.0, 1.0};
+    double sc[4], Ms[4][4], g[4], gs[4], diag[4] = {0, 0, 0, 0}, D[4], step[4], cand[4];
+    for (int k = 0; k < 4; k++) sc[k] = 1.0 / (1.0 + sqrt(m.M[k][k]));
+    for (int i = 0; i < 4; i++)
+        for (int j = 0; j < 4; j++) Ms[i][j] = (m.M[i][j] * sc[i]) * sc[j];
+    double radius = kLmInitRadius, decrease = 2.0, x_norm = -1.0;
+    bool reuse_diag = false, successful = true;
+    int invalid_run = 0, iteration = 0;
+    double x_cost = mom_cost(m, x);
+    mom_gradient(m, x, g);
+    double min_cost = DBL_MAX;
+    for (;;) {
+        if (successful && x_cost < min_cost) {
+            min_cost = x_cost;
+            for (int k = 0; k < 4; k++) best[k] = x[k];
+        }
+        if (iteration >= kLmMaxIter) break;
+        if (successful) {
+            double gmax = 0.0;
+            for (int k = 0; k < 4; k++) {
+                const double d = fabs(x[k] - (x[k] + -g[k]));
+                if (d > gmax) gmax = d;
+            }
+            if (gmax <= kLmGradTol) break;
+        }
+        if (radius <= kLmMinRadius) break;
+        iteration++;
+        if (!reuse_diag)
+            for (int k = 0; k < 4; k++) {
+                const double d = Ms[k][k] > kLmMinDiag ? Ms[k][k] : kLmMinDiag;
+                diag[k] = d < kLmMaxDiag ? d : kLmMaxDiag;
+            }
+        for (int k = 0; k < 4; k++) D[k] = sqrt(diag[k] / radius);
+        for (int k = 0; k < 4; k++) gs[k] = sc[k] * g[k];
+        const double ete = D[0] * D[0] + Ms[0][0];
+        double R[3][3], rhs[3], z[3];
+        for (int a = 0; a < 3; a++)
+            for (int b = a; b < 3; b++)
+                R[a][b] = Ms[1 + a][1 + b] + (a == b ? D[1 + a] * D[1 + a] : 0.0);
+        const double inv = inv_psd1(ete);
+        const double inv_g = inv * gs[0];
+        for (int a = 0; a < 3; a++) rhs[a] = gs[1 + a] - Ms[0][1 + a] * inv_g;
+        for (int a = 0; a < 3; a++) {
+            const double bt = Ms[0][1 + a] * inv;
+            for (int b = a; b < 3; b++) R[a][b] = R[a][b] - bt * Ms[0][1 + b];
+        }
+        bool ok = llt3_solve(R, rhs, z);
+        if (ok) {
+            double ya = gs[0];
+            for (int a = 0; a < 3; a++) ya = ya - Ms[0][1 + a] * z[a];
+            step[0] = inv * ya;
+            step[1] = z[0]; step[2] = z[1]; step[3] = z[2];
+            for (int k = 0; ok && k < 4; k++) ok = isfinite(step[k]);
+        }
+        reuse_diag = true;
+        double mcc = 0.0;
+        bool valid = false;
+        if (ok) {
+            for (int k = 0; k < 4; k++) step[k] = step[k] * -1.0;
+            double sJr = 0.0, sMs = 0.0;
+            for (int i = 0; i < 4; i++) {
+                double q = 0.0;
+                for (int j = 0; j < 4; j++) q = q + Ms[i][j] * step[j];
+                sMs = sMs + step[i] * q;
+                sJr = sJr + step[i] * gs[i];
+            }
+            mcc = -(sJr + sMs / 2.0);
+            valid = mcc > 0.0;
+        }
+        if (!valid) {
+            if (++invalid_run >= kLmMaxInvalid) break;
+            radius = radius / decrease;
+            decrease *= 2.0;
+            successful = false;
+            continue;
+        }
+        invalid_run = 0;
+        for (int k = 0; k < 4; k++) cand[k] = x[k] + step[k] * sc[k];
+        double cand_cost = mom_cost(m, cand);
+        if (!isfinite(cand_cost)) cand_cost = DBL_MAX;
+        double dx[4];
+        for (int k = 0; k < 4; k++) dx[k] = x[k] - cand[k];
+        if (norm4(dx) <= kLmParamTol * (x_norm + kLmParamTol)) break;
+        if (fabs(x_cost - cand_cost) <= kLmFuncTol * x_cost) break;
+        const double rel = (x_cost - cand_cost) / mcc;
+        if (rel > kLmMinRelDecrease) {
+            for (int k = 0; k < 4; k++) x[k] = cand[k];
+            x_norm = norm4(x);
+            x_cost = mom_cost(m, x);
+            mom_gradient(m, x, g);
+            const double q = 2.0 * rel - 1.0;
+            const double f = 1.0 - q * q * q;
+            radius = radius / (f > 1.0 / 3.0 ? f : 1.0 / 3.0);
+            radius = radius < kLmMaxRadius ? radius : kLmMaxRadius;
+            decrease = 2.0;
+            reuse_diag = false;
+            successful = true;
+        } else {
+            radius = radius / decrease;
+            decrease *= 2.0;
+            successful = false;
+        }
+    }
+    for (int k = 0; k < 4; k++) coef[k] = best[k];
+}
+
 // Degree-d least squares from the normal-equation sums (falling back to lower degrees when the
 // system is singular), stored as {a, b, c, d} with the unused high-order terms 0.
-__device__ void solve_store(const double* S, int degree, float* coeffs, double* coeffs64,
-                            long long o)
+__device__ void solve_store(const double* S, int degree, int solver, float* coeffs,
+                            double* coeffs64, long long o)
 {
+    if (solver == PF_SOLVER_LM && degree == 3) {
+        double c[4];
+        lm_moments(S, c);
+        for (int i = 0; i < 4; i++) {
+            if (coeffs) coeffs[o + i] = (float)c[i];  // Vec4f(vars), Depth.cpp:1408
+            if (coeffs64) coeffs64[o + i] = c[i];
+        }
+        return;
+    }
     double coef[4] = {0, 0, 0, 0};
     int d = degree, rc = -1;
     while (d >= 0 && (rc = solve_normal(S, d, coef)) != 0) d--;
@@ -329,8 +537,8 @@ __global__ void __launch_bounds__(kRegLanes) k_register(
     const TileGeom* __restrict__ geom, const RegGrid* __restrict__ grids,
     const GridCol* __restrict__ rcols, const GridRow* __restrict__ rrows, int ntiles,
     const float* __restrict__ emap, int ew, int eh, int ec, long long estride,
-    const float* __restrict__ tiles, long long tstride, int degree, float* __restrict__ coeffs,
-    double* __restrict__ coeffs64, double* __restrict__ sums)
+    const float* __restrict__ tiles, long long tstride, int degree, int solver,
+    float* __restrict__ coeffs, double* __restrict__ coeffs64, double* __restrict__ sums)
 {
     __shared__ double part[kRegSums][kRegLanes];
     const int p = blockIdx.x, b = blockIdx.y, l = threadIdx.x;
@@ -362,6 +570,7 @@ __global__ void __launch_bounds__(kRegLanes) k_register(
         acc[9] = acc[9] + 1.0;
         acc[10] = acc[10] + X3 * Yv; acc[11] = acc[11] + X2 * Yv; acc[12] = acc[12] + X * Yv;
         acc[13] = acc[13] + Yv;
+        acc[14] = acc[14] + Yv * Yv;
     }
 #pragma unroll
     for (int k = 0; k < kRegSums; k++) part[k][l] = acc[k];
@@ -378,15 +587,15 @@ __global__ void __launch_bounds__(kRegLanes) k_register(
             for (int k = 0; k < kRegSums; k++) sums[((long long)b * ntiles + p) * kRegSums + k] = S[k];
             return;
         }
-        solve_store(S, degree, coeffs, coeffs64, ((long long)b * ntiles + p) * 4);
+        solve_store(S, degree, solver, coeffs, coeffs64, ((long long)b * ntiles + p) * 4);
     }
 }
 
 // SolveDepthToDepth with several active maps (Depth.cpp:1274-1376: every active map's sample
 // grid feeds one problem): the active tiles' sums added in tile order, one solve per panorama.
 __global__ void k_register_joint(const double* __restrict__ sums, const int* __restrict__ active,
-                                 int ntiles, int batch, int degree, float* __restrict__ coeffs,
-                                 double* __restrict__ coeffs64)
+                                 int ntiles, int batch, int degree, int solver,
+                                 float* __restrict__ coeffs, double* __restrict__ coeffs64)
 {
     const int b = blockIdx.x * blockDim.x + threadIdx.x;
     if (b >= batch) return;
@@ -396,7 +605,7 @@ __global__ void k_register_joint(const double* __restrict__ sums, const int* __r
         if (active[p])
             for (int k = 0; k < kRegSums; k++)
                 S[k] = S[k] + sums[((long long)b * ntiles + p) * kRegSums + k];
-    solve_store(S, degree, coeffs, coeffs64, (long long)b * 4);
+    solve_store(S, degree, solver, coeffs, coeffs64, (long long)b * 4);
 }
 
 // Depth2DepthTransform on all tiles (channel 0), in place.
@@ -549,22 +758,22 @@ void launch_quantize(hipStream_t s, const float* buf, long long bstride, int n, 
 void launch_register(hipStream_t s, const TileGeom* geom, const RegGrid* grids,
                      const GridCol* rcols, const GridRow* rrows, int ntiles, const float* emap,
                      int ew, int eh, int ec, long long estride, const float* tiles,
-                     long long tstride, int degree, float* coeffs, double* coeffs64, int batch,
-                     double* sums)
+                     long long tstride, int degree, int solver, float* coeffs, double* coeffs64,
+                     int batch, double* sums)
 {
     dim3 grid(ntiles, batch);
     hipLaunchKernelGGL(k_register, grid, dim3(kRegLanes), 0, s, geom, grids, rcols, rrows,
-                       ntiles, emap, ew, eh, ec, estride, tiles, tstride, degree, coeffs,
+                       ntiles, emap, ew, eh, ec, estride, tiles, tstride, degree, solver, coeffs,
                        coeffs64, sums);
 }
 
 int register_sums_per_tile() { return kRegSums; }
 
 void launch_register_joint(hipStream_t s, const double* sums, const int* active, int ntiles,
-                           int batch, int degree, float* coeffs, double* coeffs64)
+                           int batch, int degree, int solver, float* coeffs, double* coeffs64)
 {
     hipLaunchKernelGGL(k_register_joint, dim3((batch + 63) / 64), dim3(64), 0, s, sums, active,
-                       ntiles, batch, degree, coeffs, coeffs64);
+                       ntiles, batch, degree, solver, coeffs, coeffs64);
 }
 
 void launch_apply_cubic(hipStream_t s, const TileGeom* geom, int ntiles, long long tile_elems,

@@ -24,8 +24,9 @@ EXPORTS = [
     "pf_version", "pf_set_tiles", "pf_register", "pf_fuse", "pf_merge", "pf_warp_depth",
     "pf_warp_rgb", "pf_level_info", "pf_fuse_partial", "pf_fuse_seed", "pf_fuse_finish_level",
     "pf_probe_taps", "pf_profile_enable", "pf_profile_read", "pf_error_metrics",
-    "pf_depth_transform", "pf_register_joint",
+    "pf_depth_transform", "pf_register_joint", "pf_set_solver",
 ]
+SOLVERS = {"normal": 0, "lm": 1}  # PF_SOLVER_*; "lm" = the reference's Ceres LM (default)
 
 STAGES = ["warp", "register", "seed", "targets", "jacobi", "quantize", "metrics"]
 
@@ -83,6 +84,7 @@ def load():
     L.pf_register_joint.argtypes = [vp, vp, ip, ip, ip, vp, ip, fp, fp, ip, vp, vp, vp]
     L.pf_error_metrics.argtypes = [vp, vp, ip, ip, ip, vp, vp, ip, ip, ip, ip, fp, fp, ip, ip,
                                    vp]
+    L.pf_set_solver.argtypes = [vp, ip]
     L.pf_profile_enable.argtypes = [vp, ip]
     L.pf_profile_read.argtypes = [vp, C.POINTER(C.c_double), C.POINTER(C.c_double),
                                   C.POINTER(C.c_longlong)]
@@ -176,6 +178,10 @@ class Fuser:
         self.channels = channels
         self.tile_elems = int(sum(int(layout.tile_w[i]) * int(layout.tile_h[i])
                                   for i in range(n))) * channels
+
+    def set_solver(self, solver):
+        """Degree-3 registration solver: "lm" (the reference's Ceres LM, default) or "normal"."""
+        self._check(self.L.pf_set_solver(self.h, SOLVERS[solver]))
 
     def register(self, emap, tiles, zr, degree=3, apply=True, coeffs=None, coeffs64=None):
         ew, eh, ec = _emap_dims(emap)
