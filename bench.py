@@ -47,6 +47,9 @@ def parse():
     ap.add_argument("--prof-steps", type=int, default=2,
                     help="extra untimed steps with the per-stage hipEvent timers on (roofline)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--stand-in", action="store_true",
+                    help="test hook (tests/test_bench_dist.py): the launcher, seeding and timing "
+                         "path with a CPU stand-in step over gloo; no GPU is touched")
     return ap.parse_args()
 
 
@@ -204,6 +207,64 @@ def run_c5(args, rank, world, local, dev):
         dist.destroy_process_group()
 
 
+def rank_seeds(batch, rank):
+    """Seeds of the panoramas rank `rank` owns in the batch-sharded run (config C4): contiguous
+    blocks of `batch`, disjoint across ranks (pf_dist.panorama_block)."""
+    import pf_dist
+    return pf_dist.panorama_block(batch, rank)
+
+
+def timed_steps(step, sync, args, world, dist, device=None):
+    """W untimed warmup steps, then EXACTLY K steps bracketed by a barrier + device sync on both
+    sides; returns (elapsed seconds of this rank, elapsed MAX over ranks)."""
+    for _ in range(args.warmup):
+        step()
+    sync()
+    if world > 1:
+        dist.barrier()
+    sync()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    sync()
+    if world > 1:
+        dist.barrier()
+    mine = time.perf_counter() - t0
+    elapsed = mine
+    if world > 1:
+        import torch
+        t = torch.tensor([mine], dtype=torch.float64, device=device)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    return mine, elapsed
+
+
+def run_stand_in(args, rank, world):
+    """The batch-sharded launcher with a CPU stand-in step (gloo): each rank 'processes' its own
+    seed block, sleeping a rank-dependent time per step; rank 0 prints the bench line plus the
+    gathered per-rank seeds and times, so the test can check disjoint seeds, the MAX reduction and
+    global_batch = B x world."""
+    import torch.distributed as dist
+    B = args.batch
+    seeds = rank_seeds(B, rank)
+    step = lambda: time.sleep(0.01 * (rank + 1))  # noqa: E731
+    mine, elapsed = timed_steps(step, lambda: None, args, world, dist)
+    per_rank = [None] * world
+    if world > 1:
+        dist.all_gather_object(per_rank, {"rank": rank, "seeds": seeds, "elapsed": mine})
+    else:
+        per_rank = [{"rank": 0, "seeds": seeds, "elapsed": mine}]
+    if rank == 0:
+        print(json.dumps({"metric": METRIC, "value": B * world * args.steps / elapsed,
+                          "unit": "panoramas/s", "n_gpus": world, "steps": args.steps,
+                          "warmup": args.warmup, "ms_per_step": elapsed / args.steps * 1e3,
+                          "config": {"global_batch": B * world}, "stand_in": True,
+                          "elapsed": elapsed, "per_rank": per_rank}), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
 def main():
     args = parse()
     import numpy as np
@@ -217,6 +278,10 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.stand_in:
+        if world > 1:
+            dist.init_process_group("gloo")
+        return run_stand_in(args, rank, world)
     if world > 1:
         dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local}"))
     torch.cuda.set_device(local)
@@ -228,7 +293,7 @@ def main():
     lay = PL.config_layout("C2")
     zr = PL.ZENITH_RANGE
     B = args.batch
-    seeds = pf_synth.seeds_for(B, 20261015 + rank * B)
+    seeds = rank_seeds(B, rank)
     gt = pf_synth.scene_depth(seeds, out_w, out_w // 2, dev).contiguous()
     emap = pf_synth.baseline_emap(seeds, ew, ew // 2, dev).contiguous()
     resp = panofuse.make_responses(pf_synth.responses(seeds, lay.ntiles), dev)
@@ -243,20 +308,7 @@ def main():
         fz.warp_depth(gt, tiles, resp)
         fz.merge(emap, tiles, out, zr, coeffs=coeffs)
 
-    for _ in range(args.warmup):
-        step()
-    torch.cuda.synchronize()
-
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        step()
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    elapsed = time.perf_counter() - t0
+    _, elapsed = timed_steps(step, torch.cuda.synchronize, args, world, dist, dev)
     # Per-kernel roofline: the same steps again with the library's hipEvent stage timers on
     # (recorded on the stream the kernels run on).  With the timers on, the library runs each
     # batch unsplit (no half-batch stream overlap), so every stage's time is its own.
@@ -273,10 +325,6 @@ def main():
     prof["metrics"] = fz.profile_read()["metrics"]
     fz.profile(False)
     nprof = max(1, args.prof_steps)
-    if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
 
     total_panos = B * world * args.steps
     value = total_panos / elapsed

@@ -130,6 +130,29 @@ int pf_fuse_finish_level(pf_ctx* ctx, const float* lsum, const float* cnt, int o
                          int out_h, float zr0, float zr1, int level, float* buf,
                          uint16_t* out);
 
+/* ---- row-band sharding of one level's Jacobi over ranks (pf_dist.py) ----
+ * Every rank holds full-size level buffers but owns the rows [row0, row1) of the band [h0, h1].
+ * pf_fuse_normalize: the normalised targets of (summed) pf_fuse_partial grids.
+ * pf_fuse_border: the rows outside [h0, h1] (0 at level 0, else the nearest upsample of prev)
+ *   into both ping-pong buffers a and b, or into the u16 out on the last level.
+ * pf_fuse_band_plan: the sweep depths T[0..n) of the level's passes (returns n), a function of
+ *   (level, nbands) only, so every rank derives the same plan.
+ * pf_fuse_band_pass: one pass of depth T over rows [row0, row1): reads rows row0-T-1 .. row1+T
+ *   of src (src_mode 0), or of the upsample of prev (1) or the emap seed (2, level 0) for the
+ *   first pass; writes rows [row0, row1) of dst, or of the u16 out (when out != NULL: the last
+ *   pass of the last level).  Between passes the caller refreshes the T+1 halo rows on each side
+ *   from the neighbouring bands. */
+int pf_fuse_normalize(pf_ctx* ctx, const float* lsum, const float* cnt, int out_w, int out_h,
+                      float zr0, float zr1, int level, float* lnorm);
+int pf_fuse_border(pf_ctx* ctx, const float* prev, int out_w, int out_h, float zr0, float zr1,
+                   int level, float* a, float* b, uint16_t* out);
+int pf_fuse_band_plan(pf_ctx* ctx, int out_w, int out_h, float zr0, float zr1, int level,
+                      int nbands, int* T, int cap);
+int pf_fuse_band_pass(pf_ctx* ctx, const float* emap, int ew, int eh, int ec, const float* prev,
+                      const float* lnorm, int src_mode, const float* src, float* dst,
+                      uint16_t* out, int out_w, int out_h, float zr0, float zr1, int level, int T,
+                      int row0, int row1);
+
 /* ---- stage timing (hipEvents on the context stream; replaces the reference's timeGetTime
  * brackets around registration and fusion, Depth.cpp:792-808, 907-916) ----
  * While enabled, every entry point records an event pair around each stage it launches.

@@ -6,12 +6,15 @@
  *
  * Entry points and the reference interface each one replaces:
  *   EquirectangularMap::{Load, LoadPfm, ValueAtCoord, ValueAtXY, Avg}   Depth.h:9-59
- *   PerspectiveMap::{Load, SetWindow, Value, Depth2DepthTransform}     Depth.h:61-158
+ *   PerspectiveMap::{Load, SetWindow, Value, ValueAtXY, ToSphericalCoord, SphericalTo2D,
+ *                    Contain, Azimuth/ZenithMin/Max, Depth2DepthTransform} and the cached
+ *                    window members middle/hedge/vedge/corner0-3    Depth.h:61-158
  *   Metrics::{Save, Print}                                             Depth.h:161-250
  *   MergeDepthMaps                                                     Depth.h:286-289
  *   SolveDepthToDepth                                                  Depth.h:297-298
  *   SolveDepthAll                                                      Depth.h:306-307
  *   ErrorData / ErrorEmap                                              Depth.h:313-316
+ *   SphericalToWorld / WorldToSpherical                                Depth.h:326-329
  *   Save16BitPNG                                                       Depth.cpp:27-32
  *   g_zenith_range                                                     Depth.cpp:22
  *
@@ -20,8 +23,13 @@
  * Errors: false returns with a message on std::cout, as the reference prints its diagnostics.
  * Threading: one host thread per device (the facade keeps one pf_ctx per device).
  *
+ * The window geometry and projections (SetWindow, ToSphericalCoord, SphericalTo2D, Contain,
+ * SphericalToWorld, WorldToSpherical) are host fp32 code with the reference's Imath semantics
+ * and glibc calls (csrc/pf_geom.hpp), bit-identical to it; the per-pixel path runs on the GPU.
+ *
  * Not provided: progressive JPEG, SolveDisparityToDepth / SolveDepthToDepth2 /
- * SolveDepthBySmoothing (dead code in the reference's mode 0), ErrorCompare / ErrorLaplacian.
+ * SolveDepthBySmoothing (dead code in the reference's mode 0), ErrorCompare / ErrorLaplacian,
+ * the triangulation/subdivision members (vertices, faces, subd_*: never used on the path).
  */
 #pragma once
 
@@ -31,7 +39,8 @@
 
 #ifndef PF_DEPTH_NO_VEC
 /* Minimal stand-ins for the Imath vectors of ILMBase.h (Vec2f / Vec3f / Vec4f), indexable like
- * the reference uses them. */
+ * the reference uses them; Vec3f carries the Imath operations a caller of the window members
+ * uses (ImathVec.h: dot, cross, length with lengthTiny, normalize by division). */
 struct Vec2f {
     float x = 0, y = 0;
     Vec2f() = default;
@@ -39,14 +48,27 @@ struct Vec2f {
     Vec2f(float a, float b) : x(a), y(b) {}
     float& operator[](int i) { return (&x)[i]; }
     float operator[](int i) const { return (&x)[i]; }
+    float length() const;
 };
 struct Vec3f {
     float x = 0, y = 0, z = 0;
     Vec3f() = default;
+    explicit Vec3f(float a) : x(a), y(a), z(a) {}
     Vec3f(float a, float b, float c) : x(a), y(b), z(c) {}
     float& operator[](int i) { return (&x)[i]; }
     float operator[](int i) const { return (&x)[i]; }
+    Vec3f operator+(const Vec3f& v) const { return Vec3f(x + v.x, y + v.y, z + v.z); }
+    Vec3f operator-(const Vec3f& v) const { return Vec3f(x - v.x, y - v.y, z - v.z); }
+    Vec3f operator*(float s) const { return Vec3f(x * s, y * s, z * s); }
+    float dot(const Vec3f& v) const { return x * v.x + y * v.y + z * v.z; }
+    Vec3f cross(const Vec3f& v) const
+    {
+        return Vec3f(y * v.z - z * v.y, z * v.x - x * v.z, x * v.y - y * v.x);
+    }
+    float length() const;
+    const Vec3f& normalize();  /* in place, returns *this (Imath) */
 };
+inline Vec3f operator*(float s, const Vec3f& v) { return Vec3f(s * v.x, s * v.y, s * v.z); }
 struct Vec4f {
     float v[4] = {0, 0, 0, 0};
     Vec4f() = default;
@@ -87,8 +109,12 @@ class PerspectiveMap {
 public:
     int width = 0, height = 0, channels = 0;
     float* data = nullptr;
-    float az_left = 0, az_right = 0, zen_top = 0, zen_down = 0; /* SetWindow arguments */
-    Vec4f ranges;                                               /* valid {aL, aR, zU, zD} */
+    /* the FOVs of the viewing window (SetWindow arguments, Depth.h:70-73) */
+    float azimuth_left = 0, azimuth_right = 0, zenith_top = 0, zenith_down = 0;
+    Vec4f ranges; /* valid {azi_left, azi_right, zen_up, zen_down} (Depth.h:76) */
+    /* the cached quadrilateral window of SetWindow (Depth.h:87-93) */
+    Vec3f middle, hedge, vedge;
+    Vec3f corner0, corner1, corner2, corner3;
     bool window_set = false;
 
     PerspectiveMap() = default;
@@ -99,8 +125,16 @@ public:
     PerspectiveMap& operator=(const PerspectiveMap&) = delete;
 
     bool Load(std::string& filename);
-    void SetWindow(float azi_left, float azi_right, float zen_top, float zen_down);
+    void SetWindow(float AzimuthLeft, float AzimuthRight, float ZenithTop, float ZenithDown);
     float Value(float x, float y);
+    Vec2f ToSphericalCoord(float x, float y);       /* Depth.cpp:157-166 */
+    Vec2f SphericalTo2D(float azimuth, float zenith); /* Depth.cpp:168-182 */
+    bool Contain(float azimuth, float zenith);        /* Depth.cpp:184-207 */
+    float AzimuthMin() { return azimuth_left < azimuth_right ? azimuth_left : azimuth_right; }
+    float AzimuthMax() { return azimuth_left > azimuth_right ? azimuth_left : azimuth_right; }
+    float ZenithMin() { return zenith_top < zenith_down ? zenith_top : zenith_down; }
+    float ZenithMax() { return zenith_top > zenith_down ? zenith_top : zenith_down; }
+    float ValueAtXY(int x, int y);                    /* Depth.cpp:209-212 */
     void Depth2DepthTransform(Vec4f& abcd); /* runs on the GPU (pf_depth_transform) */
 };
 
@@ -137,6 +171,11 @@ bool ErrorEmap(EquirectangularMap& emap_gt, EquirectangularMap& emap_given, floa
                float& mae, float& mre, float& mse_log, float& delta1, float& delta2,
                float& delta3, int align_way, bool cap_depth,
                Vec2f* least_square_shift = nullptr, float* median_shift_factor = nullptr);
+
+/* spherical coord. (radians) to 3d position (Depth.cpp:2955-2958) */
+Vec3f SphericalToWorld(float azimuth, float zenith);
+/* 3d position to spherical coord.; p is normalized in place (Depth.cpp:2960-2971) */
+Vec2f WorldToSpherical(Vec3f& p);
 
 }  // namespace DepthNamespace
 

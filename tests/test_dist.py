@@ -123,3 +123,95 @@ def test_tile_sharded_fusion_gloo_world2():
     assert ("final", True) in res
     assert res.count(("targets", True)) == 2
     assert res.count(("max", 2.0)) == 2
+
+
+class OracleRowBackend(OracleBackend):
+    """CPU stand-in of pf_dist.HipRowShardBackend: each rank holds full-level planes (torch CPU
+    tensors) but only its band rows stay current; a band pass of depth T is T oracle sweeps of
+    the whole plane, of which only rows [row0, row1) are kept (they depend on rows row0-T-1 ..
+    row1+T only, the halo the orchestration refreshed)."""
+
+    def __init__(self, *args):
+        super().__init__(*args)
+        lv = self._lv(2)
+        self.out = torch.zeros(lv.w * lv.h, dtype=torch.int16)
+
+    def dims(self, level):
+        lv = self._lv(level)
+        return lv.w, lv.h, lv.h0, lv.h1
+
+    def plane(self, level):
+        lv = self._lv(level)
+        return torch.zeros(lv.w * lv.h, dtype=torch.float32)
+
+    def normalize(self, level, lsum, cnt):
+        lv = self._lv(level)
+        Ln = self.O.normalize(lsum.numpy(), cnt.numpy().astype(np.int32), lv)
+        return torch.from_numpy(np.ascontiguousarray(Ln).ravel().copy())
+
+    def plan(self, level, nbands):
+        it = self._lv(level).iters
+        return [10] * (it // 10) + ([it % 10] if it % 10 else [])
+
+    def _base(self, level, prev):
+        lv = self._lv(level)
+        if level == 0:
+            return self.O.seed_level0(self.emap, lv)
+        plv = self._lv(level - 1)
+        return self.O.upsample(prev.numpy().reshape(plv.h, plv.w), lv)
+
+    def border(self, level, prev, a, b):
+        base = torch.from_numpy(np.ascontiguousarray(self._base(level, prev)).ravel().copy())
+        if level == 2:
+            self.out.copy_(torch.from_numpy(self.O.quantize(base.numpy()).view(np.int16)))
+        else:
+            a.copy_(base)
+            b.copy_(base)
+
+    def band_pass(self, level, lnorm, src_mode, src, dst, T, row0, row1, last, prev):
+        lv = self._lv(level)
+        base = src.numpy().reshape(lv.h, lv.w) if src_mode == 0 else self._base(level, prev)
+        res = self.O.jacobi(base, lnorm.numpy().reshape(lv.h, lv.w), lv, T).ravel()
+        sl = slice(row0 * lv.w, row1 * lv.w)
+        if last:
+            self.out[sl] = torch.from_numpy(self.O.quantize(res[sl]).view(np.int16))
+        else:
+            dst[sl] = torch.from_numpy(res[sl].copy())
+
+
+def _row_worker(rank, world, port, q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        import pf_layouts as PL
+        import pf_synth
+        import pyoracle as O
+        lay = PL.config_layout("C1")
+        tiles, total = O.make_tiles(lay)
+        seeds = pf_synth.seeds_for(1, 4711)
+        emap = pf_synth.baseline_emap(seeds, 128, 64)[0].numpy()
+        data = np.random.RandomState(9).rand(total).astype(np.float32)
+        be = OracleRowBackend(O, PL, 512, emap, tiles, data)
+        pf_dist.fuse_row_sharded(be, 3, lay.ntiles, rank, world, pf_dist.TorchComm(dist))
+        ref, _ = O.solve_depth_all(emap, tiles, data, 512, PL.ZENITH_RANGE)
+        q.put((rank, bool(np.array_equal(be.out.numpy().view(np.uint16).reshape(256, 512), ref))))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_row_sharded_fusion_gloo(world):
+    """tiles and rows sharded, halo rows exchanged between passes -- every
+    rank ends with the u16 panorama of the unsharded oracle fusion, bit for bit."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_row_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(240)
+        assert p.exitcode == 0
+    res = sorted(q.get() for _ in range(world))
+    assert res == [(r, True) for r in range(world)]

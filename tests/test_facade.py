@@ -1,0 +1,133 @@
+"""The C++ drop-in boundary (include/pf_depth.h) called the way the reference's Main.cpp calls
+Depth.h: tests/cpp/facade_check.cpp is a compiled caller that includes pf_depth.h and links
+-lpanofuse_depth -lpanofuse.
+
+* geom (CPU): the cached window members of PerspectiveMap::SetWindow (middle, hedge, vedge,
+  corner0-3, Depth.cpp:120-155), ToSphericalCoord, SphericalTo2D, Contain, SphericalToWorld and
+  WorldToSpherical (Depth.cpp:157-207, 2955-2971) -- bit-exact against the oracle.
+* solve (GPU): MergeDepthMaps' calls in its order -- per tile SolveDepthToDepth with one active
+  map + Depth2DepthTransform (Depth.cpp:794-805), SolveDepthAll (:913) -- bit-exact against the
+  oracle on a C1 case, then SolveDepthToDepth with several active maps against the sample-wise
+  Ceres-LM restatement over the concatenated samples (relative 1e-5, tests/test_gpu_lm.py).
+"""
+import os
+import subprocess
+
+import numpy as np
+import pytest
+
+import pf_layouts as PL
+import pf_synth
+import pyoracle as O
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+PKG = os.path.join(ROOT, "wacv2023-high-resolution-depth-estimation-for-panoramas-through-"
+                         "perspective-map-registrations_amd")
+BIN = os.path.join(PKG, "bin", "pf_facade_check")
+ZR = PL.ZENITH_RANGE
+
+
+def _run(mode, blob, tmp_path):
+    if not os.path.exists(BIN):
+        pytest.fail(f"{BIN} not built (make -C {PKG})")
+    fi, fo = tmp_path / "in.bin", tmp_path / "out.bin"
+    fi.write_bytes(blob)
+    r = subprocess.run([BIN, mode, str(fi), str(fo)], capture_output=True, text=True,
+                       timeout=300)
+    assert r.returncode == 0, r.stdout + r.stderr
+    return np.fromfile(fo, dtype=np.uint8)
+
+
+def _layout_blob(lay):
+    rng = lay.capped_ranges()
+    parts = []
+    for i in range(lay.ntiles):
+        parts.append(np.asarray(lay.fovs[i], np.float32).tobytes())
+        parts.append(np.asarray(rng[i], np.float32).tobytes())
+    return b"".join(parts)
+
+
+@pytest.mark.parametrize("cfg", ["C1", "C2", "LERES"])
+def test_facade_geometry_bit_exact(cfg, tmp_path):
+    lay = PL.config_layout(cfg)
+    tiles, _ = O.make_tiles(lay)
+    rs = np.random.RandomState(7)
+    xy = rs.uniform(-0.1, 1.1, size=(64, 2)).astype(np.float32)
+    sp = np.stack([rs.uniform(0, 2 * np.pi, 96), rs.uniform(0.05, 3.09, 96)], 1).astype(np.float32)
+    blob = (np.int32(lay.ntiles).tobytes() + _layout_blob(lay) + np.int32(len(xy)).tobytes()
+            + xy.tobytes() + np.int32(len(sp)).tobytes() + sp.tobytes())
+    out = _run("geom", blob, tmp_path).view(np.float32)
+    per_tile = 21 + 2 * len(xy) + 3 * len(sp)
+    L = O.lib()
+    import ctypes as C
+    fp = C.POINTER(C.c_float)
+    for i in range(lay.ntiles):
+        o = out[i * per_tile:(i + 1) * per_tile]
+        t = tiles[i]
+        ref = np.concatenate([np.array(getattr(t, k), np.float32) for k in
+                              ("middle", "hedge", "vedge", "corner0", "corner1", "corner2",
+                               "corner3")])
+        assert np.array_equal(o[:21].view(np.uint32), ref.view(np.uint32)), f"tile {i} window"
+        got = o[21:21 + 2 * len(xy)].reshape(-1, 2)
+        for k, (x, y) in enumerate(xy):
+            r = np.zeros(2, np.float32)
+            L.pfo_to_spherical_coord(C.byref(t), float(x), float(y), r.ctypes.data_as(fp))
+            assert np.array_equal(got[k].view(np.uint32), r.view(np.uint32)), (i, k)
+        got = o[21 + 2 * len(xy):].reshape(-1, 3)
+        for k, (az, zen) in enumerate(sp):
+            r = np.zeros(2, np.float32)
+            L.pfo_sph_to_2d(C.byref(t), float(az), float(zen), r.ctypes.data_as(fp))
+            assert np.array_equal(got[k, :2].view(np.uint32), r.view(np.uint32)), (i, k)
+            inside = all(-1e-3 <= float(v) <= 1 + 1e-3 for v in r)
+            assert got[k, 2] == (1.0 if inside else 0.0)
+    rest = out[lay.ntiles * per_tile:].reshape(-1, 8)
+    for k, (az, zen) in enumerate(sp):
+        d = np.zeros(3, np.float32)
+        L.pfo_sph_to_world(float(az), float(zen), d.ctypes.data_as(fp))
+        assert np.array_equal(rest[k, :3].view(np.uint32), d.view(np.uint32))
+        q = (d * np.float32(3.5)).astype(np.float32)
+        s = np.zeros(2, np.float32)
+        L.pfo_world_to_sph(q.ctypes.data_as(fp), s.ctypes.data_as(fp))
+        assert np.array_equal(rest[k, 3:5].view(np.uint32), s.view(np.uint32))
+        assert abs(float(np.linalg.norm(rest[k, 5:8])) - 1.0) < 1e-6  # normalized in place
+
+
+@pytest.mark.gpu
+def test_facade_solvers_bit_exact(tmp_path):
+    lay = PL.config_layout("C1")
+    tiles, total = O.make_tiles(lay)
+    seeds = pf_synth.seeds_for(1, 31337)
+    emap = pf_synth.baseline_emap(seeds, 128, 64)[0].numpy()
+    gt = pf_synth.scene_depth(seeds, 512, 256)[0].numpy()
+    data = O.warp_depth(gt, tiles, total, O.responses(pf_synth.responses(seeds, lay.ntiles)))
+    act = np.array([1, 4], np.int32)
+    blob = (np.array([lay.ntiles, 256, 256], np.int32).tobytes() + _layout_blob(lay)
+            + np.array([128, 64], np.int32).tobytes() + emap.astype(np.float32).tobytes()
+            + data.astype(np.float32).tobytes() + np.int32(512).tobytes()
+            + np.array(ZR, np.float32).tobytes() + np.int32(len(act)).tobytes() + act.tobytes())
+    out = _run("solve", blob, tmp_path)
+    n = lay.ntiles
+    abcd = out[:16 * n].view(np.float32).reshape(n, 4)
+    off = 16 * n
+    tdata = out[off:off + 4 * total].view(np.float32)
+    off += 4 * total
+    u16 = out[off:off + 2 * 512 * 256].view(np.uint16).reshape(256, 512)
+    off += 2 * 512 * 256
+    joint = out[off:off + 16].view(np.float32)
+    # the oracle runs MergeDepthMaps' sequence on the same inputs (LM registration, Ceres-style)
+    ref_data = data.copy()
+    for p in range(n):
+        _, r_abcd, _ = O.register_tile(tiles[p], ref_data, emap, ZR, solver="lm")
+        assert np.array_equal(abcd[p], r_abcd), p
+        O.depth_to_depth(tiles[p], ref_data, r_abcd)
+    assert np.array_equal(tdata.view(np.uint32), ref_data.view(np.uint32))
+    ref_out, _ = O.solve_depth_all(emap, tiles, ref_data, 512, ZR)
+    assert int((u16 != ref_out).sum()) == 0
+    xs, ys = [], []
+    for p in act:
+        x, y, _, _ = O.reg_samples(tiles[p], ref_data, emap, ZR)
+        xs.append(x)
+        ys.append(y)
+    c, _ = O.lm_fit(np.concatenate(xs), np.concatenate(ys))
+    rel = np.abs(joint.astype(np.float64) - c) / np.maximum(np.abs(c), 1e-6)
+    assert rel.max() <= 1e-5, (joint, c)

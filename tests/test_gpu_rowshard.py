@@ -1,0 +1,123 @@
+"""Row-band sharded fusion on the GPU: pf_dist.fuse_row_sharded over the HIP band
+entry points (pf_fuse_band_plan / pf_fuse_band_pass / pf_fuse_border / pf_fuse_normalize).
+
+The ranks are simulated on one GPU: one thread and one panofuse context per rank, all on the
+same stream, with an in-process communicator standing in for RCCL (all-reduce, halo exchange,
+band broadcast).  The result of every rank must equal the one-GPU pf_fuse bit for bit, at C2
+(3 levels, 2 and 3 bands) and at the C5 layout (8192x4096, 4 levels, 4 bands, tiles sharded
+too).  The collectives themselves are covered over gloo in tests/test_dist.py.
+"""
+import threading
+
+import numpy as np
+import pytest
+
+torch = pytest.importorskip("torch")
+
+pytestmark = pytest.mark.gpu
+
+import panofuse  # noqa: E402
+import pf_dist  # noqa: E402
+import pf_layouts as PL  # noqa: E402
+import pf_synth  # noqa: E402
+
+ZR = PL.ZENITH_RANGE
+DEV = "cuda:0"
+
+
+class ThreadComm:
+    """In-process stand-in for pf_dist.TorchComm among `world` threads."""
+
+    def __init__(self, world):
+        self.world = world
+        self.bar = threading.Barrier(world, timeout=120)
+        self.box = {}
+
+    def rank(self, r):
+        outer = self
+
+        class RankComm:
+            def all_reduce_sum(self, t):
+                outer.box[("ar", r)] = t
+                outer.bar.wait()
+                if r == 0:
+                    acc = outer.box[("ar", 0)].clone()
+                    for k in range(1, outer.world):
+                        acc += outer.box[("ar", k)]
+                    outer.box["ar"] = acc
+                outer.bar.wait()
+                t.copy_(outer.box["ar"])
+                outer.bar.wait()
+
+            def exchange(self, sends, recvs):
+                for peer, t in sends:
+                    outer.box[("x", r, peer)] = t.clone()
+                outer.bar.wait()
+                for peer, t in recvs:
+                    t.copy_(outer.box[("x", peer, r)])
+                outer.bar.wait()
+
+            def broadcast(self, t, src):
+                if r == src:
+                    outer.box["bc"] = t.clone()
+                outer.bar.wait()
+                if r != src:
+                    t.copy_(outer.box["bc"])
+                outer.bar.wait()
+
+        return RankComm()
+
+
+def _run(cfg, world, seed):
+    lay = PL.config_layout(cfg)
+    out_w, ew = PL.CONFIGS["C5" if cfg == "C5" else "C2"]
+    seeds = pf_synth.seeds_for(1, seed)
+    gt = pf_synth.scene_depth(seeds, out_w, out_w // 2, DEV).contiguous()
+    emap = pf_synth.baseline_emap(seeds, ew, ew // 2, DEV).contiguous()
+    fz = panofuse.Fuser(0)
+    fz.set_tiles(lay)
+    tiles = torch.zeros((1, fz.tile_elems), dtype=torch.float32, device=DEV)
+    fz.warp_depth(gt, tiles, panofuse.make_responses(pf_synth.responses(seeds, lay.ntiles), DEV))
+    coeffs = torch.zeros((1, lay.ntiles, 4), dtype=torch.float32, device=DEV)
+    fz.register(emap, tiles, ZR, apply=False, coeffs=coeffs)
+    ref = torch.zeros((1, out_w // 2, out_w), dtype=torch.int16, device=DEV)
+    fz.fuse(emap, tiles, ref, ZR, coeffs=coeffs)
+    torch.cuda.synchronize()
+
+    comm = ThreadComm(world)
+    outs, errs = [None] * world, []
+
+    def rank_main(r):
+        try:
+            f = panofuse.Fuser(0)
+            f.set_tiles(lay)
+            out = torch.zeros(out_w * (out_w // 2), dtype=torch.int16, device=DEV)
+            be = pf_dist.HipRowShardBackend(f, emap, tiles, coeffs[0], out_w, ZR, out)
+            pf_dist.fuse_row_sharded(be, be.nlevels, lay.ntiles, r, world, comm.rank(r))
+            torch.cuda.synchronize()
+            outs[r] = out
+            f.close()
+        except BaseException as e:  # surfaced by the main thread
+            errs.append(e)
+            comm.bar.abort()
+
+    th = [threading.Thread(target=rank_main, args=(r,)) for r in range(world)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join(300)
+    assert not errs, errs
+    for r in range(world):
+        diff = (outs[r].view(out_w // 2, out_w) != ref[0]).sum(1)
+        rows = torch.nonzero(diff).flatten().tolist()
+        assert not rows, (f"rank {r}: {int(diff.sum())} pixels differ from the one-GPU fusion in "
+                          f"rows {rows[:20]} (bands {[pf_dist.band_rows(*panofuse.level_info(out_w, out_w // 2, ZR, 0)[2:4], q, world) for q in range(world)]})")
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_row_sharded_c2_equals_fuse(world):
+    _run("C2", world, 20261015 + 11)
+
+
+def test_row_sharded_c5_equals_fuse():
+    _run("C5", 4, 20261015 + 12)

@@ -6,6 +6,7 @@
 // and the separable trig tables of the fusion and registration grids, computed with glibc's
 // sincosf/tanf exactly as the reference calls them.  Everything per panorama runs on the GPU.
 #include "../../include/panofuse.h"
+#include "pf_geom.hpp"
 #include "pf_internal.hpp"
 
 #include <algorithm>
@@ -173,71 +174,21 @@ static int upload(pf_ctx* c, DevBuf& b, const std::vector<T>& v)
 }
 
 // ---------------------------------------------------------------------------------------------
-// Host geometry: Imath Vec3<float> semantics (ImathVec.h:1467-1700).
+// Host geometry: PerspectiveMap::SetWindow in Imath Vec3<float> semantics (pf_geom.hpp).
 namespace {
-struct V3 {
-    float x, y, z;
-};
-inline V3 add(V3 a, V3 b) { return {a.x + b.x, a.y + b.y, a.z + b.z}; }
-inline V3 sub(V3 a, V3 b) { return {a.x - b.x, a.y - b.y, a.z - b.z}; }
-inline V3 mul(V3 a, float s) { return {a.x * s, a.y * s, a.z * s}; }
-inline float dot(V3 a, V3 b) { return a.x * b.x + a.y * b.y + a.z * b.z; }
-inline V3 cross(V3 a, V3 b)
-{
-    return {a.y * b.z - a.z * b.y, a.z * b.x - a.x * b.z, a.x * b.y - a.y * b.x};
-}
-float length(V3 a)
-{
-    float l2 = dot(a, a);
-    if (l2 < 2.0f * FLT_MIN) {
-        float ax = a.x >= 0.0f ? a.x : -a.x, ay = a.y >= 0.0f ? a.y : -a.y,
-              az = a.z >= 0.0f ? a.z : -a.z;
-        float mx = ax;
-        if (mx < ay) mx = ay;
-        if (mx < az) mx = az;
-        if (mx == 0.0f) return 0.0f;
-        ax /= mx; ay /= mx; az /= mx;
-        return mx * sqrtf(ax * ax + ay * ay + az * az);
-    }
-    return sqrtf(l2);
-}
-V3 normalized(V3 a)
-{
-    float l = length(a);
-    if (l != 0.0f) { a.x /= l; a.y /= l; a.z /= l; }
-    return a;
-}
-V3 sph_to_world(float az, float zen)
-{  // Depth.cpp:2955-2958 (g++ emits sincosf for each sin/cos pair)
-    float sz, cz, sa, ca;
-    sincosf(zen, &sz, &cz);
-    sincosf(az, &sa, &ca);
-    return {sz * ca, sz * sa, cz};
-}
-
 TileGeom set_window(const pf_window& f, int w, int h, int ch)
 {  // PerspectiveMap::SetWindow, Depth.cpp:120-155
-    V3 middle = sph_to_world((f.az_left + f.az_right) / 2, (f.zen_top + f.zen_down) / 2);
-    V3 left = normalized(cross(V3{0, 0, 1}, middle));
-    V3 up = normalized(cross(left, middle));
-    float ta = tanf(fabsf(f.az_right - f.az_left) / 2);
-    float tz = tanf(fabsf(f.zen_top - f.zen_down) / 2);
-    V3 left_middle = add(middle, mul(left, ta));
-    V3 right_middle = sub(middle, mul(left, ta));
-    V3 up_middle = sub(middle, mul(up, tz));
-    V3 down_middle = add(middle, mul(up, tz));
-    V3 corner0 = add(add(middle, sub(left_middle, middle)), sub(up_middle, middle));
-    V3 hedge = sub(right_middle, left_middle);
-    V3 vedge = sub(down_middle, up_middle);
+    using namespace pfgeom;
+    const Window win = pfgeom::set_window(f.az_left, f.az_right, f.zen_top, f.zen_down);
     TileGeom g{};
-    g.middle[0] = middle.x; g.middle[1] = middle.y; g.middle[2] = middle.z;
-    g.hedge[0] = hedge.x; g.hedge[1] = hedge.y; g.hedge[2] = hedge.z;
-    g.vedge[0] = vedge.x; g.vedge[1] = vedge.y; g.vedge[2] = vedge.z;
-    g.corner0[0] = corner0.x; g.corner0[1] = corner0.y; g.corner0[2] = corner0.z;
-    V3 p0mp = {middle.x - 0.0f, middle.y - 0.0f, middle.z - 0.0f};  // (p0 - p), p = Vec3f(0)
-    g.mm = dot(p0mp, middle);
-    g.hl = length(hedge);
-    g.vl = length(vedge);
+    g.middle[0] = win.middle.x; g.middle[1] = win.middle.y; g.middle[2] = win.middle.z;
+    g.hedge[0] = win.hedge.x; g.hedge[1] = win.hedge.y; g.hedge[2] = win.hedge.z;
+    g.vedge[0] = win.vedge.x; g.vedge[1] = win.vedge.y; g.vedge[2] = win.vedge.z;
+    g.corner0[0] = win.corner0.x; g.corner0[1] = win.corner0.y; g.corner0[2] = win.corner0.z;
+    const V3 p0mp = {win.middle.x - 0.0f, win.middle.y - 0.0f, win.middle.z - 0.0f};  // p0 - p
+    g.mm = dot(p0mp, win.middle);
+    g.hl = length(win.hedge);
+    g.vl = length(win.vedge);
     g.w = w;
     g.h = h;
     g.c = ch;
@@ -550,10 +501,10 @@ static int prepare_registration(pf_ctx* c, float zr0, float zr1)
         float top = zr0 > r.zen_top ? zr0 : r.zen_top;      // MAX2 (:1301)
         float down = zr1 < r.zen_down ? zr1 : r.zen_down;   // MIN2 (:1302)
         rg.rows = (int)roundf(fabsf(down - top) / subd);
-        if (rg.cols <= 0 || rg.rows <= 0)
-            return fail(c, PF_EINVAL,
-                        "tile %d: registration grid %dx%d is empty (the reference divides by 0)",
-                        i, rg.cols, rg.rows);
+        // an empty grid (the reference divides by 0 there) is an error only for a tile that is
+        // solved (check_reg_grids); an inactive tile of a joint solve may have one
+        if (rg.cols < 0) rg.cols = 0;
+        if (rg.rows < 0) rg.rows = 0;
         rg.col_off = (int)rcols.size();
         rg.row_off = (int)rrows.size();
         for (int k = 0; k <= rg.cols; k++) {  // :1334
@@ -577,6 +528,21 @@ static int prepare_registration(pf_ctx* c, float zr0, float zr1)
     c->reg_valid = true;
     c->reg_zr0 = b0;
     c->reg_zr1 = b1;
+    return PF_OK;
+}
+
+// The tiles that will be solved must have a non-empty sample grid (Depth.cpp:1334-1335 divides
+// by cols and rows); active == nullptr means every tile.
+static int check_reg_grids(pf_ctx* c, const int* active)
+{
+    for (int i = 0; i < c->ntiles; i++) {
+        if (active && !active[i]) continue;
+        const RegGrid& rg = c->reg_h[i];
+        if (rg.cols <= 0 || rg.rows <= 0)
+            return fail(c, PF_EINVAL,
+                        "tile %d: registration grid %dx%d is empty (the reference divides by 0)",
+                        i, rg.cols, rg.rows);
+    }
     return PF_OK;
 }
 
@@ -696,6 +662,7 @@ struct JacobiTuning {
     int C = 2, Tmax = 10;  // PF_JC=0: per level, the cheaper of 2 and 4 by the cost model
     double step_overhead = 3.0, lone_cycles = 4.0;  // swept on MI355X (tools/jsweep.sh)
     double c4_eff = 23.0 / 26.0;  // packed C=4 issue per pixel-update relative to C=2
+    double pipe_overhead = 1.0;   // pipelined engine: barrier + exchange per step, update units
 };
 
 static JacobiTuning jacobi_tuning()
@@ -706,6 +673,7 @@ static JacobiTuning jacobi_tuning()
     if (const char* e = getenv("PF_JT")) t.Tmax = atoi(e);
     if (const char* e = getenv("PF_JOVH")) t.step_overhead = atof(e);
     if (const char* e = getenv("PF_JC1")) t.lone_cycles = atof(e);
+    if (const char* e = getenv("PF_JPOVH")) t.pipe_overhead = atof(e);
     if (t.Tmax < 1) t.Tmax = 1;
     return t;
 }
@@ -717,16 +685,20 @@ static JacobiTuning jacobi_tuning()
 // small levels a "one wave per slot" grid left the last round 20-80% empty.
 struct PassPlan {
     int T = 1, nchunks = 1;
+    int stages = 1;  // > 1: the pipelined engine (k_jpipe), T/stages levels per wave
     double cost = 0;
 };
 
 static PassPlan best_chunks(int T, int C, int band_rows, int w, int batch, int per_simd,
-                            int nsimd, double ovh, double c1, double c4_eff)
+                            int nsimd, double ovh, double c1, double c4_eff, int stages = 1)
 {
-    // VALU work of one step in update units: T*C updates, per-update issue of the C form
-    const double work = C == 4 ? T * 2.0 * c4_eff : (double)T;
+    // VALU work of one step of one wave in update units: T/stages levels of C updates, per-update
+    // issue of the C form
+    const double lv = (double)T / stages;
+    const double work = C == 4 ? lv * 2.0 * c4_eff : lv;
     PassPlan best;
     best.T = T;
+    best.stages = stages;
     best.cost = 1e300;
     const int Tp = (T + C - 1) / C * C;
     const long long per = (long long)((w + 64 * C - 2 * Tp - 1) / (64 * C - 2 * Tp)) * batch;
@@ -736,7 +708,7 @@ static PassPlan best_chunks(int T, int C, int band_rows, int w, int batch, int p
         if (n > 1 && (band_rows + rows - 1) / rows < n) continue;  // same as a smaller n
         // rounds of resident waves; in each, a SIMD holding W waves issues one VALU
         // instruction per 2 cycles shared among them, and a lone wave one per ~c1 cycles
-        const long long waves = per * n;
+        const long long waves = per * n * stages;
         double cyc = 0;
         for (long long left = waves; left > 0; left -= slots) {
             const long long in_round = left < slots ? left : slots;
@@ -755,17 +727,33 @@ static PassPlan best_chunks(int T, int C, int band_rows, int w, int batch, int p
 // Sweep depths for a level: a shortest-path split of `iters` into passes from the supported
 // menu (<= tcap), each with its best chunking.
 static std::vector<PassPlan> plan_level(pf_ctx* c, const LevelDims& L, int C, int tcap, int batch,
-                                        bool fast)
+                                        bool fast, int band_rows = 0)
 {
     static const JacobiTuning tune = jacobi_tuning();
     static const int menu[] = {10, 8, 5, 4, 2, 1};
-    const int band_rows = L.h1 - L.h0 + 1;
+    if (band_rows <= 0) band_rows = L.h1 - L.h0 + 1;
     PassPlan opt[11];
     for (int T : menu)
         if (T <= tcap && jstream_supported_T(T))
             opt[T] = best_chunks(T, C, band_rows, L.w, batch,
                                  jstream_waves_per_cu(C, T, fast) / 4, 4 * c->num_cu,
                                  tune.step_overhead, tune.lone_cycles, tune.c4_eff);
+    // the pipelined engine (2 waves per strip-chunk), packed form only; PF_JPIPE=0 disables it,
+    // PF_JPIPE=1 takes it wherever it exists, otherwise the cost model decides
+    static const char* pe = getenv("PF_JPIPE");
+    const int pmode = pe ? atoi(pe) : 2;
+    if (fast && C == 2 && pmode != 0)
+        for (int T : menu) {
+            if (T > tcap || T % 2 || !jpipe_supported(2, T / 2)) continue;
+            PassPlan pp = best_chunks(T, C, band_rows, L.w, batch,
+                                      jpipe_waves_per_cu(2, T / 2) / 4, 4 * c->num_cu,
+                                      tune.step_overhead + tune.pipe_overhead, tune.lone_cycles,
+                                      tune.c4_eff, 2);
+            if (pmode == 1 || pp.cost < opt[T].cost || !jstream_supported_T(T)) opt[T] = pp;
+        }
+    if (fast && C == 2 && pmode == 1)  // forced: the single-wave engine only where no pipe fits
+        for (int T : menu)
+            if (opt[T].stages == 1) opt[T].cost *= 1e6;
     std::vector<double> dp(L.iters + 1, 1e300);
     std::vector<int> choice(L.iters + 1, 1);
     dp[0] = 0;
@@ -780,6 +768,11 @@ static std::vector<PassPlan> plan_level(pf_ctx* c, const LevelDims& L, int C, in
         }
     std::vector<PassPlan> plan;
     for (int r = L.iters; r > 0; r -= choice[r]) plan.push_back(opt[choice[r]]);
+    // tuning runs: PF_JN<w> forces the row chunking of the level of width w
+    char key[32];
+    snprintf(key, sizeof(key), "PF_JN%d", L.w);
+    if (const char* e = getenv(key))
+        for (PassPlan& pp : plan) pp.nchunks = atoi(e) > 0 ? atoi(e) : pp.nchunks;
     return plan;
 }
 
@@ -793,6 +786,9 @@ static int jacobi_tcap(const LevelDims& L)
 {
     static const JacobiTuning tune = jacobi_tuning();
     int cap = tune.Tmax;
+    char key[32];  // tuning runs: PF_JT<w> caps the sweep depth of the level of width w
+    snprintf(key, sizeof(key), "PF_JT%d", L.w);
+    if (const char* e = getenv(key)) cap = atoi(e) > 0 ? atoi(e) : cap;
     if (L.h0 - 1 < cap) cap = L.h0 - 1;
     if (L.h - 2 - L.h1 < cap) cap = L.h - 2 - L.h1;
     while (cap >= 1) {
@@ -838,6 +834,8 @@ static float* run_jacobi(pf_ctx* c, const LevelDims& L, int first, const float* 
     P.out = out; P.ostride = ostride;
     P.w = L.w; P.h = L.h; P.h0 = L.h0; P.h1 = L.h1;
     P.hcol = hcol;
+    P.row_lo = L.h0;
+    P.row_hi = L.h1 + 1;
     const int band_rows = L.h1 - L.h0 + 1;
     float* src = (first == 0) ? a : nullptr;
     float* dst = (first == 0) ? b : a;
@@ -845,7 +843,8 @@ static float* run_jacobi(pf_ctx* c, const LevelDims& L, int first, const float* 
     if (show) {
         fprintf(stderr, "jacobi plan %dx%d band %d iters %d batch %d %s C%d:", L.w, L.h,
                 band_rows, L.iters, batch, fast ? "packed" : "general", C);
-        for (const PassPlan& pp : plan) fprintf(stderr, " T%d/n%d", pp.T, pp.nchunks);
+        for (const PassPlan& pp : plan)
+            fprintf(stderr, " T%d/n%d%s", pp.T, pp.nchunks, pp.stages > 1 ? "p" : "");
         fprintf(stderr, "\n");
     }
     int pass = 0;
@@ -860,7 +859,8 @@ static float* run_jacobi(pf_ctx* c, const LevelDims& L, int first, const float* 
         P.src = src;
         P.dst = dst;
         P.out_mode = (pass + 1 == (int)plan.size() && out) ? 1 : 0;
-        launch_jstream(c->stream, P, C, T, batch, fast);
+        if (pp.stages > 1) launch_jpipe(c->stream, P, pp.stages, T / pp.stages, batch);
+        else launch_jstream(c->stream, P, C, T, batch, fast);
         src = dst;
         dst = (dst == a) ? b : a;
         pass++;
@@ -1077,6 +1077,7 @@ int pf_register(pf_ctx* c, const float* emap, int ew, int eh, int ec, float* til
     if (!tiles) return fail(c, PF_EINVAL, "tiles is NULL");
     if (degree < 0 || degree > 3) return fail(c, PF_EINVAL, "degree %d not in [0,3]", degree);
     if ((rc = prepare_registration(c, zr0, zr1))) return rc;
+    if ((rc = check_reg_grids(c, nullptr))) return rc;
     float* cf = coeffs;
     if (!cf) {
         if ((rc = ensure(c, c->coeffs, sizeof(float) * 4 * c->ntiles * batch))) return rc;
@@ -1251,6 +1252,113 @@ int pf_fuse_finish_level(pf_ctx* c, const float* lsum, const float* cnt, int out
     return PF_OK;
 }
 
+// ---- row-band sharding of one level's sweeps (pf_dist.fuse_row_sharded) ----
+int pf_fuse_normalize(pf_ctx* c, const float* lsum, const float* cnt, int out_w, int out_h,
+                      float zr0, float zr1, int level, float* lnorm)
+{
+    int rc;
+    if ((rc = check_common(c, 1))) return rc;
+    if (!lsum || !cnt || !lnorm) return fail(c, PF_EINVAL, "NULL buffer");
+    if ((rc = prepare_levels(c, out_w, out_h, zr0, zr1))) return rc;
+    if (level < 0 || level >= c->lc.nlevels) return fail(c, PF_EINVAL, "bad level %d", level);
+    launch_normalize(c->stream, lsum, cnt, c->lc.dims[level], lnorm);
+    HIPCHK(c, hipGetLastError());
+    return PF_OK;
+}
+
+int pf_fuse_border(pf_ctx* c, const float* prev, int out_w, int out_h, float zr0, float zr1,
+                   int level, float* a, float* b, uint16_t* out)
+{
+    int rc;
+    if ((rc = check_common(c, 1))) return rc;
+    if ((rc = prepare_levels(c, out_w, out_h, zr0, zr1))) return rc;
+    const LevelCache& lc = c->lc;
+    if (level < 0 || level >= lc.nlevels) return fail(c, PF_EINVAL, "bad level %d", level);
+    if (level > 0 && !prev) return fail(c, PF_EINVAL, "level %d needs the previous level", level);
+    const bool last = level == lc.nlevels - 1;
+    if (last ? !out : (!a || !b)) return fail(c, PF_EINVAL, "NULL buffer");
+    const LevelDims& L = lc.dims[level];
+    const long long st = (long long)L.w * L.h;
+    const long long pst = level > 0 ? (long long)lc.dims[level - 1].w * lc.dims[level - 1].h : 0;
+    launch_border(c->stream, level == 0 ? nullptr : prev, pst, L, a, b, st, last ? out : nullptr,
+                  st, 1);
+    HIPCHK(c, hipGetLastError());
+    return PF_OK;
+}
+
+int pf_fuse_band_plan(pf_ctx* c, int out_w, int out_h, float zr0, float zr1, int level,
+                      int nbands, int* T, int cap)
+{
+    int rc;
+    if ((rc = check_common(c, 1))) return rc;
+    if (!T || cap < 1 || nbands < 1) return fail(c, PF_EINVAL, "pf_fuse_band_plan: bad arguments");
+    if ((rc = prepare_levels(c, out_w, out_h, zr0, zr1))) return rc;
+    const LevelCache& lc = c->lc;
+    if (level < 0 || level >= lc.nlevels) return fail(c, PF_EINVAL, "bad level %d", level);
+    const LevelDims& L = lc.dims[level];
+    if (jacobi_tcap(L) < 1)
+        return fail(c, PF_EINVAL, "level %d: the zenith band leaves no room for band passes", level);
+    const int band = L.h1 - L.h0 + 1;
+    // the sweep depths depend only on (level, nbands): every rank derives the same plan
+    std::vector<PassPlan> plan = plan_level(c, L, 2, jacobi_tcap(L), 1, lc.full[level],
+                                            (band + nbands - 1) / nbands);
+    if ((int)plan.size() > cap) return fail(c, PF_EINVAL, "plan of %zu passes > cap %d", plan.size(), cap);
+    for (size_t i = 0; i < plan.size(); i++) T[i] = plan[i].T;
+    return (int)plan.size();
+}
+
+int pf_fuse_band_pass(pf_ctx* c, const float* emap, int ew, int eh, int ec, const float* prev,
+                      const float* lnorm, int src_mode, const float* src, float* dst,
+                      uint16_t* out, int out_w, int out_h, float zr0, float zr1, int level, int T,
+                      int row0, int row1)
+{
+    int rc;
+    if ((rc = check_common(c, 1))) return rc;
+    if ((rc = prepare_levels(c, out_w, out_h, zr0, zr1))) return rc;
+    const LevelCache& lc = c->lc;
+    if (level < 0 || level >= lc.nlevels) return fail(c, PF_EINVAL, "bad level %d", level);
+    const LevelDims& L = lc.dims[level];
+    if (!lnorm || (!dst && !out)) return fail(c, PF_EINVAL, "NULL buffer");
+    if (src_mode < 0 || src_mode > 2) return fail(c, PF_EINVAL, "src_mode %d", src_mode);
+    if (src_mode == 0 && !src) return fail(c, PF_EINVAL, "src_mode 0 needs src");
+    if (src_mode == 1 && (level == 0 || !prev)) return fail(c, PF_EINVAL, "src_mode 1 needs prev");
+    if (src_mode == 2 && (level != 0 || (rc = check_emap(c, emap, ew, eh, ec))))
+        return rc ? rc : fail(c, PF_EINVAL, "src_mode 2 (seed) is level 0 only");
+    if (T < 1 || T > jacobi_tcap(L) || !jstream_supported_T(T))
+        return fail(c, PF_EINVAL, "pass depth %d not available at level %d", T, level);
+    if (row0 < L.h0 || row1 > L.h1 + 1 || row0 >= row1)
+        return fail(c, PF_EINVAL, "rows [%d,%d) outside the band [%d,%d]", row0, row1, L.h0, L.h1);
+    const bool fast = lc.full[level];
+    static const JacobiTuning tune = jacobi_tuning();
+    const int band = row1 - row0;
+    PassPlan pp = best_chunks(T, 2, band, L.w, 1, jstream_waves_per_cu(2, T, fast) / 4,
+                              4 * c->num_cu, tune.step_overhead, tune.lone_cycles, tune.c4_eff);
+    const long long st = (long long)L.w * L.h;
+    JacobiPass P{};
+    P.prev = prev; P.pstride = 0;
+    P.emap = emap; P.estride = 0; P.ew = ew; P.eh = eh; P.ec = ec;
+    P.cols = (const GridCol*)lc.cols[level].p; P.rows = (const GridRow*)lc.rows[level].p;
+    P.lnorm = lnorm; P.lstride = st;
+    P.sstride = st; P.dstride = st;
+    P.out = out; P.ostride = st;
+    P.w = L.w; P.h = L.h; P.h0 = L.h0; P.h1 = L.h1;
+    P.hcol = fast ? (const float*)lc.hcol[level].p : nullptr;
+    P.row_lo = row0;
+    P.row_hi = row1;
+    P.Tp = (T + 1) / 2 * 2;
+    P.V = 128 - 2 * P.Tp;
+    P.nstrips = (L.w + P.V - 1) / P.V;
+    P.rows_per_chunk = (band + pp.nchunks - 1) / pp.nchunks;
+    P.nchunks = (band + P.rows_per_chunk - 1) / P.rows_per_chunk;
+    P.src_mode = src_mode;
+    P.src = src;
+    P.dst = dst;
+    P.out_mode = out ? 1 : 0;
+    launch_jstream(c->stream, P, 2, T, 1, fast);
+    HIPCHK(c, hipGetLastError());
+    return PF_OK;
+}
+
 int pf_probe_taps(pf_ctx* c, int out_w, int out_h, float zr0, float zr1, int level,
                   int32_t* tap_index)
 {
@@ -1339,6 +1447,7 @@ int pf_register_joint(pf_ctx* c, const float* emap, int ew, int eh, int ec, cons
     int nact = 0;
     for (int v : act) nact += v != 0;
     if (nact == 0) return fail(c, PF_EINVAL, "pf_register_joint: no active tile");
+    if ((rc = check_reg_grids(c, act.data()))) return rc;
     if ((rc = upload(c, c->reg_active, act))) return rc;
     if ((rc = ensure(c, c->reg_sums,
                      sizeof(double) * register_sums_per_tile() * c->ntiles * batch)))
@@ -1351,7 +1460,8 @@ int pf_register_joint(pf_ctx* c, const float* emap, int ew, int eh, int ec, cons
     launch_register(c->stream, (const TileGeom*)c->geom.p, (const RegGrid*)c->reg.p,
                     (const GridCol*)c->rcols.p, (const GridRow*)c->rrows.p, c->ntiles, emap, ew,
                     eh, ec, (long long)ew * eh * ec, tiles, c->tile_elems, degree, c->solver,
-                    nullptr, nullptr, batch, (double*)c->reg_sums.p);
+                    nullptr, nullptr, batch, (double*)c->reg_sums.p,
+                    (const int*)c->reg_active.p);
     launch_register_joint(c->stream, (const double*)c->reg_sums.p, (const int*)c->reg_active.p,
                           c->ntiles, batch, degree, c->solver, cf, coeffs64);
     HIPCHK(c, hipGetLastError());

@@ -7,6 +7,7 @@
 // (registration, transform, fusion, quantisation, metrics) is a libpanofuse HIP kernel.
 #include "../../include/pf_depth.h"
 #include "../../include/panofuse.h"
+#include "pf_geom.hpp"
 #include "pf_image.hpp"
 
 #include <hip/hip_runtime.h>
@@ -25,6 +26,18 @@
 #include <mutex>
 
 Vec2f g_zenith_range((float)PF_D2R(26), (float)PF_D2R(154));  // Depth.cpp:22
+
+// Imath operations of the vector stand-ins (ImathVec.h:1145-1180, 1631-1700)
+float Vec2f::length() const { return pfgeom::length2(x, y); }
+float Vec3f::length() const { return pfgeom::length(pfgeom::V3{x, y, z}); }
+const Vec3f& Vec3f::normalize()
+{
+    const pfgeom::V3 n = pfgeom::normalized(pfgeom::V3{x, y, z});
+    x = n.x;
+    y = n.y;
+    z = n.z;
+    return *this;
+}
 
 namespace {
 
@@ -100,7 +113,7 @@ bool set_layout(pf_ctx* c, std::vector<DepthNamespace::PerspectiveMap*>& pm,
                       << std::endl;
             return false;
         }
-        fov[i] = pf_window{p.az_left, p.az_right, p.zen_top, p.zen_down};
+        fov[i] = pf_window{p.azimuth_left, p.azimuth_right, p.zenith_top, p.zenith_down};
         rng[i] = pf_window{p.ranges[0], p.ranges[1], p.ranges[2], p.ranges[3]};
         tw[i] = p.width;
         th[i] = p.height;
@@ -289,11 +302,18 @@ PerspectiveMap& PerspectiveMap::operator=(PerspectiveMap&& o) noexcept
         channels = o.channels;
         data = o.data;
         o.data = nullptr;
-        az_left = o.az_left;
-        az_right = o.az_right;
-        zen_top = o.zen_top;
-        zen_down = o.zen_down;
+        azimuth_left = o.azimuth_left;
+        azimuth_right = o.azimuth_right;
+        zenith_top = o.zenith_top;
+        zenith_down = o.zenith_down;
         ranges = o.ranges;
+        middle = o.middle;
+        hedge = o.hedge;
+        vedge = o.vedge;
+        corner0 = o.corner0;
+        corner1 = o.corner1;
+        corner2 = o.corner2;
+        corner3 = o.corner3;
         window_set = o.window_set;
     }
     return *this;
@@ -321,16 +341,65 @@ bool PerspectiveMap::Load(std::string& filename)
     return true;
 }
 
-// The window geometry (middle / hedge / vedge / corners, Depth.cpp:120-155) is computed by
-// pf_set_tiles, bit-identically, when the map is handed to the library.
+namespace {
+Vec3f vec(const pfgeom::V3& v) { return Vec3f(v.x, v.y, v.z); }
+pfgeom::V3 v3(const Vec3f& v) { return pfgeom::V3{v.x, v.y, v.z}; }
+pfgeom::Window window_of(const PerspectiveMap& p)
+{
+    pfgeom::Window w;
+    w.middle = v3(p.middle);
+    w.hedge = v3(p.hedge);
+    w.vedge = v3(p.vedge);
+    w.corner0 = v3(p.corner0);
+    w.corner1 = v3(p.corner1);
+    w.corner2 = v3(p.corner2);
+    w.corner3 = v3(p.corner3);
+    return w;
+}
+}  // namespace
+
+// The window geometry (Depth.cpp:120-155) on the host, bit-identical to the reference's (and to
+// pf_set_tiles, which recomputes it when the map is handed to the library).
 void PerspectiveMap::SetWindow(float aL, float aR, float zT, float zD)
 {
-    az_left = aL;
-    az_right = aR;
-    zen_top = zT;
-    zen_down = zD;
+    azimuth_left = aL;
+    azimuth_right = aR;
+    zenith_top = zT;
+    zenith_down = zD;
+    const pfgeom::Window w = pfgeom::set_window(aL, aR, zT, zD);
+    middle = vec(w.middle);
+    hedge = vec(w.hedge);
+    vedge = vec(w.vedge);
+    corner0 = vec(w.corner0);
+    corner1 = vec(w.corner1);
+    corner2 = vec(w.corner2);
+    corner3 = vec(w.corner3);
     window_set = true;
 }
+
+Vec2f PerspectiveMap::ToSphericalCoord(float x, float y)  // Depth.cpp:157-166
+{
+    float az, zen;
+    pfgeom::to_spherical_coord(window_of(*this), x, y, az, zen);
+    return Vec2f(az, zen);
+}
+
+Vec2f PerspectiveMap::SphericalTo2D(float azimuth, float zenith)  // Depth.cpp:168-182
+{
+    float x, y;
+    pfgeom::sph_to_2d(window_of(*this), azimuth, zenith, x, y);
+    return Vec2f(x, y);
+}
+
+bool PerspectiveMap::Contain(float azimuth, float zenith)  // Depth.cpp:184-207
+{
+    const Vec2f xy = SphericalTo2D(azimuth, zenith);
+    const float threshold = 1e-3f;
+    return xy.x >= 0 - threshold && xy.x <= 1 + threshold && xy.y >= 0 - threshold &&
+           xy.y <= 1 + threshold;
+}
+
+float PerspectiveMap::ValueAtXY(int x, int y) { return data[((size_t)y * width + x) * channels]; }
 
 float PerspectiveMap::Value(float x, float y)  // Depth.cpp:111-118
 {
@@ -352,6 +421,18 @@ void PerspectiveMap::Depth2DepthTransform(Vec4f& abcd)
         !pf_ok(c, pf_synchronize(c), "pf_synchronize"))
         return;
     hip_ok(hipMemcpy(data, d.p, n * sizeof(float), hipMemcpyDeviceToHost), "download");
+}
+
+// ---- free projection functions (Depth.cpp:2955-2971) ----
+Vec3f SphericalToWorld(float azimuth, float zenith) { return vec(pfgeom::sph_to_world(azimuth, zenith)); }
+
+Vec2f WorldToSpherical(Vec3f& p)
+{
+    pfgeom::V3 q = v3(p);
+    float az, zen;
+    pfgeom::world_to_sph(q, az, zen);
+    p = vec(q);
+    return Vec2f(az, zen);
 }
 
 // ---- Metrics (Depth.h:161-258) ----

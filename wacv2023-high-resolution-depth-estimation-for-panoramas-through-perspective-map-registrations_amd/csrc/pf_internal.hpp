@@ -151,6 +151,7 @@ struct JacobiPass {
     int out_mode;
     int w, h, h0, h1;
     int V, Tp, nstrips, nchunks, rows_per_chunk;
+    int row_lo, row_hi;  // rows stored by this pass: [row_lo, row_hi) within [h0, h1] (chunked)
     const float* hcol;  // packed form: per column 0.5 (covered) or 0 (un-windowed), w entries
 };
 
@@ -170,6 +171,9 @@ bool jstream_supported_T(int T);
 int jstream_waves_per_cu(int C, int T, bool fast);
 bool jstream_supported_C(int C, bool fast);
 void launch_jstream(hipStream_t s, const JacobiPass& P, int C, int T, int batch, bool fast);
+bool jpipe_supported(int S, int TS);
+int jpipe_waves_per_cu(int S, int TS);
+void launch_jpipe(hipStream_t s, const JacobiPass& P, int S, int TS, int batch);
 void launch_border(hipStream_t s, const float* prev, long long pstride, LevelDims L, float* a,
                    float* b, long long stride, uint16_t* out, long long ostride, int batch);
 void launch_seed0(hipStream_t s, const float* emap, int ew, int eh, int ec, long long estride,
@@ -197,7 +201,7 @@ void launch_register(hipStream_t s, const TileGeom* geom, const RegGrid* grids,
                      const GridCol* rcols, const GridRow* rrows, int ntiles, const float* emap,
                      int ew, int eh, int ec, long long estride, const float* tiles,
                      long long tstride, int degree, int solver, float* coeffs, double* coeffs64,
-                     int batch, double* sums = nullptr);
+                     int batch, double* sums = nullptr, const int* active = nullptr);
 int register_sums_per_tile();
 void launch_register_joint(hipStream_t s, const double* sums, const int* active, int ntiles,
                            int batch, int degree, int solver, float* coeffs, double* coeffs64);

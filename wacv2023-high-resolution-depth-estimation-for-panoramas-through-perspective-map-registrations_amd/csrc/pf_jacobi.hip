@@ -130,8 +130,11 @@ struct JLag {
     int w, xs0, vlo, vhi, r0, r1, h0, h1;
     int colbase;   // virtual column of lane 0 (wave-uniform)
     int lo;        // lane * C
-    int rlo, rhi;  // rows loads are clamped to (wave-uniform; the host guarantees every row a
-                   // valid output depends on lies inside, so clamping only touches halo rows)
+    int rlo, rhi;  // rows loads are clamped to: the band [h0, h1].  A band pixel never reads a
+                   // row outside it except as a neighbour of the un-windowed rows h0 / h1,
+                   // whose update ignores its neighbours -- in the packed form through a zero
+                   // factor, which needs the neighbours finite: the rows outside the band are
+                   // never stored by a pass, so on the last level they may hold anything
     const float *src, *prev, *emap, *lnorm;
     float* dst;
     uint16_t* out;
@@ -532,13 +535,13 @@ __global__ void __launch_bounds__(256, PF_JLAG_WAVES) k_jlag(JacobiPass P)
     S.h1 = P.h1;
     S.colbase = strip * P.V - P.Tp;
     S.lo = lane * C;
-    S.rlo = 1;
-    S.rhi = P.h - 2;
+    S.rlo = P.h0;
+    S.rhi = P.h1;
     S.xs0 = strip * P.V - P.Tp + lane * C;
     S.vlo = strip * P.V;
     S.vhi = min(S.vlo + P.V, P.w);
-    S.r0 = P.h0 + chunk * P.rows_per_chunk;
-    S.r1 = min(S.r0 + P.rows_per_chunk, P.h1 + 1);
+    S.r0 = P.row_lo + chunk * P.rows_per_chunk;
+    S.r1 = min(S.r0 + P.rows_per_chunk, P.row_hi);
     S.src = P.src + b * P.sstride;
     S.prev = P.prev + b * P.pstride;
     S.emap = P.emap + b * P.estride;
@@ -589,6 +592,300 @@ __global__ void __launch_bounds__(256, PF_JLAG_WAVES) k_jlag(JacobiPass P)
     const bool rows = (S.h0 >= wlo && S.h0 <= whi) || (S.h1 >= wlo && S.h1 <= whi);
     if (!FAST || rows) S.template run<true>(k0, kend, g0);
     else S.template run<false>(k0, kend, g0);
+}
+
+// ---------------------------------------------------------------------------------------------
+// Pipelined passes: the T = S*TS sweep levels of one strip-chunk are split over the S waves of a
+// workgroup.  Wave (stage) s owns levels s*TS+1 .. (s+1)*TS and runs the lagged stream of JLag
+// over them; the input of its first level is its predecessor's last level, whose new row the
+// predecessor leaves in a double-buffered LDS slot every step (one workgroup barrier per step).
+// Against JLag at the same T: S times the waves per strip-chunk at 1/S of the register rings, so
+// the small levels fill the chip with fewer row chunks (less vertical halo) and every level gets
+// more waves per SIMD to hide the load/LDS latency behind.  Same arithmetic, same order: every
+// pixel's value is bit-identical to JLag's (and the reference's).
+static constexpr int md(int a, int m) { return ((a % m) + m) % m; }
+
+template <int TS, int S, int SI, int SRC, bool OUT16>
+struct JPipe {
+    static constexpr int C = 2;
+    static constexpr int T = TS * S;
+    static constexpr int TB = SI * TS + 1, TE = TB + TS - 1;  // own levels
+    static constexpr int PF = PF_JLAG_PF, NB = PF_JLAG_PF + 1;
+    static constexpr int R = (2 * TS + 1 + 5) / 6 * 6;  // L ring rows (multiple of 6)
+    static constexpr int NG = R / 6;
+    static constexpr int G = PF_JPK_GROUP;
+    Row<C> H[TS][3];  // H[l][row % 3]: level TB-1+l (l = 0: the input level of this stage)
+    Row<C> In[NB];    // stage 0: level-0 input row r in In[r % NB]
+    Row<C> Lin[NB];   // L row r in Lin[r % NB], put into the LDS ring PF steps after its load
+    float* lring;     // this stage's ring: R rows of 64*C floats (row r in slot r % R)
+    const float* xin; // stage > 0: the predecessor's exchange slots [2][64*C]
+    float* xout;      // stage < S-1: this stage's exchange slots
+    int lane_c;
+    float hcol[C];
+    const JacobiPass* P;
+    int w, xs0, vlo, vhi, r0, r1, h0, h1, colbase, lo, rlo, rhi;
+    const float *src, *prev, *emap, *lnorm;
+    float* dst;
+    uint16_t* out;
+
+    __device__ __forceinline__ Row<C> load_row(const float* base_ptr, int k) const
+    {
+        Row<C> r;
+        int kc = k < rlo ? rlo : (k > rhi ? rhi : k);
+        const float2 q = *reinterpret_cast<const float2*>(base_ptr + ((long long)kc * w + colbase) + lo);
+        r.v[0] = q.x; r.v[1] = q.y;
+        return r;
+    }
+    __device__ __forceinline__ Row<C> load_input(int k) const
+    {  // as JLag::load_input
+        if constexpr (SRC == SRC_BUF) {
+            return load_row(src, k);
+        } else {
+            Row<C> r;
+            int xr = xs0, Y = k;
+            if (xr < 0) { xr += w; Y -= 1; }
+            else if (xr >= w) { xr -= w; Y += 1; }
+            float v0 = 0.0f, v1 = 0.0f;
+            if (Y >= 0 && Y < P->h) {
+                if constexpr (SRC == SRC_UPSAMPLE) {
+                    v0 = v1 = prev[(long long)(Y >> 1) * (w >> 1) + (xr >> 1)];
+                } else if (Y >= P->h0 && Y <= P->h1) {
+                    const float zen = P->rows[Y + 1].zen;
+                    v0 = emap[emap_index(P->cols[xr + 1].az, zen, P->ew, P->eh, P->ec)];
+                    v1 = emap[emap_index(P->cols[xr + 2].az, zen, P->ew, P->eh, P->ec)];
+                }
+            }
+            r.v[0] = v0;
+            r.v[1] = v1;
+            return r;
+        }
+    }
+    __device__ __forceinline__ void lds_put(float* p, Row<C> r) const
+    {  // L rows sanitised as they enter the ring (the packed form's H = 0 trick, JLag)
+        r.v[0] = __builtin_isfinite(r.v[0]) ? r.v[0] : 0.0f;
+        r.v[1] = __builtin_isfinite(r.v[1]) ? r.v[1] : 0.0f;
+        *reinterpret_cast<float2*>(p) = make_float2(r.v[0], r.v[1]);
+    }
+    __device__ __forceinline__ Row<C> lds_get(const float* p) const
+    {
+        Row<C> r;
+        const float2 q = *reinterpret_cast<const float2*>(p);
+        r.v[0] = q.x; r.v[1] = q.y;
+        return r;
+    }
+
+    // own levels T0 < t <= T1 (global indices) of step k (phase PH), packed form of JLag
+    template <int PH, int T0, int T1, bool ROWS>
+    __device__ __forceinline__ void sweep_group(const Row<C>* Lv, Row<C>* nw, int k) const
+    {
+        constexpr int NGR = T1 - T0;
+        const f2 q = {-0.25f, -0.25f};
+        const f2 reg = {(float)1e-4, (float)1e-4};
+        const f2 reg_ = {1 - (float)1e-4, 1 - (float)1e-4};
+        float Wl[NGR], Er[NGR];
+#pragma unroll
+        for (int g = 0; g < NGR; g++) {
+            const int t = T0 + 1 + g, l = t - TB;  // reads ring H[l] = level t-1
+            Wl[g] = dpp_from_left(H[l][md(PH - 2 * t, 3)].v[1]);
+            Er[g] = dpp_from_right(H[l][md(PH - 2 * t, 3)].v[0]);
+        }
+        f2 cur[NGR];
+#pragma unroll
+        for (int g = 0; g < NGR; g++) {
+            const int t = T0 + 1 + g, l = t - TB;
+            cur[g] = f2{Wl[g], H[l][md(PH - 2 * t, 3)].v[0]} + H[l][md(PH - 2 * t - 1, 3)].v;
+        }
+#pragma unroll
+        for (int g = 0; g < NGR; g++) {
+            const int t = T0 + 1 + g, l = t - TB;
+            cur[g] = __builtin_elementwise_fma(cur[g], q, H[l][md(PH - 2 * t, 3)].v);
+        }
+#pragma unroll
+        for (int g = 0; g < NGR; g++) {
+            const int t = T0 + 1 + g, l = t - TB;
+            cur[g] = __builtin_elementwise_fma(H[l][md(PH - 2 * t + 1, 3)].v, q, cur[g]);
+        }
+#pragma unroll
+        for (int g = 0; g < NGR; g++) {
+            const int t = T0 + 1 + g, l = t - TB;
+            cur[g] = __builtin_elementwise_fma(f2{H[l][md(PH - 2 * t, 3)].v[1], Er[g]}, q, cur[g]);
+        }
+#pragma unroll
+        for (int g = 0; g < NGR; g++) {
+            const int t = T0 + 1 + g, l = t - TB;
+            f2 hh = f2{hcol[0], hcol[1]};
+            if constexpr (ROWS) {
+                const int row = k - 2 * t;
+                const float hr = (row == h0 || row == h1) ? 0.0f : 1.0f;
+                hh = hh * hr;
+            }
+            cur[g] = __builtin_elementwise_fma(Lv[t - TB].v - cur[g], hh, H[l][md(PH - 2 * t, 3)].v);
+        }
+#pragma unroll
+        for (int g = 0; g < NGR; g++) {
+            const int t = T0 + 1 + g, l = t - TB;
+            nw[t - TB].v = pk_add_clamp01(cur[g] * reg_, H[l][md(PH - 2 * t, 3)].v * reg);
+        }
+    }
+    template <int PH, int T0, bool ROWS>
+    __device__ __forceinline__ void sweep(const Row<C>* Lv, Row<C>* nw, int k) const
+    {
+        constexpr int T1 = T0 + G < TE ? T0 + G : TE;
+        sweep_group<PH, T0, T1, ROWS>(Lv, nw, k);
+        if constexpr (T1 < TE) sweep<PH, T1, ROWS>(Lv, nw, k);
+    }
+
+    // step k = (group base) + PH, GB = group base mod R
+    template <int PH, bool ROWS, int GB>
+    __device__ __forceinline__ void step(int k)
+    {
+        // the input level's row k - 2TB + 1 joins ring H[0]
+        if constexpr (SI == 0) {
+            H[0][md(PH - 1, 3)] = In[md(PH - 1, NB)];
+        } else {
+            H[0][md(PH - 2 * TB + 1, 3)] = lds_get(xin + md(PH - 1, 2) * (64 * C) + lane_c);
+        }
+        // L row q = k - 2TB + 2 enters the ring; rows k - 2t (t = TB..TE) are read from it
+        constexpr int QO = -2 * TB + 2;
+        lds_put(lring + md(GB + PH + QO, R) * (64 * C) + lane_c, Lin[md(PH + QO, NB)]);
+        Row<C> Lv[TS];
+#pragma unroll
+        for (int t = TB; t <= TE; t++) Lv[t - TB] = lds_get(lring + md(GB + PH - 2 * t, R) * (64 * C) + lane_c);
+        Lin[md(PH + QO + PF, NB)] = load_row(lnorm, k + QO + PF);
+        if constexpr (SI == 0) In[md(PH + PF - 1, NB)] = load_input(k + PF - 1);
+        Row<C> nw[TS];
+        sweep<PH, TB - 1, ROWS>(Lv, nw, k);
+#pragma unroll
+        for (int t = TB; t < TE; t++) H[t - TB + 1][md(PH - 2 * t, 3)] = nw[t - TB];
+        if constexpr (SI < S - 1) {
+            *reinterpret_cast<float2*>(xout + md(PH, 2) * (64 * C) + lane_c) =
+                make_float2(nw[TS - 1].v[0], nw[TS - 1].v[1]);
+        } else {
+            const int j = k - 2 * T;  // final-level row finished this step
+            if (j >= r0 && j < r1 && xs0 >= vlo && xs0 < vhi) {
+                const long long rowb = (long long)j * w + colbase;
+                if constexpr (OUT16) {
+                    const uint32_t q0 = (uint32_t)(nw[TS - 1].v[0] * 65535.0f);
+                    const uint32_t q1 = (uint32_t)(nw[TS - 1].v[1] * 65535.0f);
+                    *reinterpret_cast<uint32_t*>(out + rowb + lo) = q0 | (q1 << 16);
+                } else {
+                    *reinterpret_cast<float2*>(dst + rowb + lo) =
+                        make_float2(nw[TS - 1].v[0], nw[TS - 1].v[1]);
+                }
+            }
+        }
+        __syncthreads();  // the exchange row of this step is visible to the next stage
+    }
+
+    template <bool ROWS, int GI>
+    __device__ __forceinline__ void group(int k)
+    {
+        step<0, ROWS, 6 * GI>(k);
+        step<1, ROWS, 6 * GI>(k + 1);
+        step<2, ROWS, 6 * GI>(k + 2);
+        step<3, ROWS, 6 * GI>(k + 3);
+        step<4, ROWS, 6 * GI>(k + 4);
+        step<5, ROWS, 6 * GI>(k + 5);
+    }
+    template <bool ROWS, int GI>
+    __device__ __forceinline__ bool groups_from(int& k, int kend)
+    {
+        group<ROWS, GI>(k);
+        k += 6;
+        if (k >= kend) return false;
+        if constexpr (GI + 1 < NG) return groups_from<ROWS, GI + 1>(k, kend);
+        else return true;
+    }
+    template <bool ROWS>
+    __device__ __forceinline__ void run(int k0, int kend, int g0)
+    {
+        int k = k0;
+        bool more = true;
+        static_assert(NG <= 4, "entry switch covers up to 4 groups");
+        if constexpr (NG > 3) { if (g0 == 3) more = groups_from<ROWS, (NG > 3 ? 3 : 0)>(k, kend); }
+        if constexpr (NG > 2) { if (more && g0 == 2) more = groups_from<ROWS, (NG > 2 ? 2 : 0)>(k, kend); }
+        if constexpr (NG > 1) { if (more && g0 == 1) more = groups_from<ROWS, (NG > 1 ? 1 : 0)>(k, kend); }
+        while (more) more = groups_from<ROWS, 0>(k, kend);
+    }
+};
+
+template <int TS, int S, int SI, int SRC, bool OUT16>
+__device__ __forceinline__ void jpipe_stage(const JacobiPass& P, int lane, int b, int strip,
+                                            int chunk, float* lring, float* xchg)
+{
+    using S_t = JPipe<TS, S, SI, SRC, OUT16>;
+    constexpr int T = S_t::T, C = 2;
+    S_t St;
+    St.P = &P;
+    St.w = P.w;
+    St.h0 = P.h0;
+    St.h1 = P.h1;
+    St.colbase = strip * P.V - P.Tp;
+    St.lo = lane * C;
+    St.lane_c = lane * C;
+    St.rlo = P.h0;  // as JLag::rlo
+    St.rhi = P.h1;
+    St.xs0 = strip * P.V - P.Tp + lane * C;
+    St.vlo = strip * P.V;
+    St.vhi = min(St.vlo + P.V, P.w);
+    St.r0 = P.row_lo + chunk * P.rows_per_chunk;
+    St.r1 = min(St.r0 + P.rows_per_chunk, P.row_hi);
+    St.src = P.src + b * P.sstride;
+    St.prev = P.prev + b * P.pstride;
+    St.emap = P.emap + b * P.estride;
+    St.lnorm = P.lnorm + b * P.lstride;
+    St.dst = P.dst + b * P.dstride;
+    St.out = P.out + b * P.ostride;
+    St.lring = lring + SI * (S_t::R * 64 * C);
+    St.xin = SI > 0 ? xchg + (SI - 1) * (2 * 64 * C) : nullptr;
+    St.xout = SI < S - 1 ? xchg + SI * (2 * 64 * C) : nullptr;
+    St.hcol[0] = St.hcol[1] = 0.0f;
+    if (St.xs0 >= 0 && St.xs0 < P.w) { St.hcol[0] = P.hcol[St.xs0]; St.hcol[1] = P.hcol[St.xs0 + 1]; }
+#pragma unroll
+    for (int l = 0; l < TS; l++)
+#pragma unroll
+        for (int q = 0; q < 3; q++) St.H[l][q].v = f2{0.0f, 0.0f};
+#pragma unroll
+    for (int q = 0; q < S_t::NB; q++) { St.In[q].v = f2{0.0f, 0.0f}; St.Lin[q].v = f2{0.0f, 0.0f}; }
+    const int kfirst = St.r0 - T - 1;
+    const int k0 = kfirst - md(kfirst, 6);
+    const int kend = St.r1 + 2 * T;
+    constexpr int QO = -2 * S_t::TB + 2;
+    if constexpr (SI == 0) {
+#pragma unroll
+        for (int r = 0; r + 1 < S_t::PF; r++) St.In[md(r, S_t::NB)] = St.load_input(k0 + r);
+    }
+#pragma unroll
+    for (int r = 0; r < S_t::PF; r++) St.Lin[md(QO + r, S_t::NB)] = St.load_row(St.lnorm, k0 + QO + r);
+    const int g0 = md(k0, S_t::R) / 6;
+    const int wlo = k0 - 2 * T, whi = kend + 3;
+    const bool rows = (St.h0 >= wlo && St.h0 <= whi) || (St.h1 >= wlo && St.h1 <= whi);
+    // rows is uniform over the workgroup (it depends on the chunk only), so every stage takes the
+    // same branch and runs the same number of steps (= barriers)
+    if (rows) St.template run<true>(k0, kend, g0);
+    else St.template run<false>(k0, kend, g0);
+}
+
+template <int TS, int S, int SRC, bool OUT16>
+__global__ void __launch_bounds__(64 * S) k_jpipe(JacobiPass P)
+{
+    constexpr int C = 2, R = JPipe<TS, S, 0, SRC, OUT16>::R;
+    const int lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int job = blockIdx.x;
+    if (job >= P.nstrips * P.nchunks) return;  // uniform over the workgroup
+    const int b = blockIdx.y;
+    const int strip = job % P.nstrips, chunk = job / P.nstrips;
+    __shared__ float lring[S * R * 64 * C];
+    __shared__ float xchg[(S > 1 ? S - 1 : 1) * 2 * 64 * C];
+    // the exchange slots are read one step before they are first written (those rows only
+    // feed halo cells); zero them so the stale cells are finite and deterministic
+    for (int i = threadIdx.x; i < (S > 1 ? S - 1 : 1) * 2 * 64 * C; i += 64 * S) xchg[i] = 0.0f;
+    __syncthreads();
+    if (wave == 0) jpipe_stage<TS, S, 0, SRC, OUT16>(P, lane, b, strip, chunk, lring, xchg);
+    if constexpr (S > 1) { if (wave == 1) jpipe_stage<TS, S, (S > 1 ? 1 : 0), SRC, OUT16>(P, lane, b, strip, chunk, lring, xchg); }
+    if constexpr (S > 2) { if (wave == 2) jpipe_stage<TS, S, (S > 2 ? 2 : 0), SRC, OUT16>(P, lane, b, strip, chunk, lring, xchg); }
+    if constexpr (S > 3) { if (wave == 3) jpipe_stage<TS, S, (S > 3 ? 3 : 0), SRC, OUT16>(P, lane, b, strip, chunk, lring, xchg); }
 }
 
 // Out-of-band rows of a level: 0 (level 0, Depth.cpp:1449-1452) or the nearest upsample of the
@@ -724,6 +1021,50 @@ void launch_jstream(hipStream_t s, const JacobiPass& P, int C, int T, int batch,
     }
     if (fast) launch_pass_c<2, true>(s, P, T, batch);
     else launch_pass_c<2, false>(s, P, T, batch);
+}
+
+// Pipelined passes (k_jpipe): T = S * TS.
+template <int TS, int S>
+static void launch_pipe_ts(hipStream_t s, const JacobiPass& P, int batch)
+{
+    dim3 grid((unsigned)(P.nstrips * P.nchunks), batch);
+    if (P.out_mode) {
+        if (P.src_mode == SRC_BUF) hipLaunchKernelGGL((k_jpipe<TS, S, SRC_BUF, true>), grid, dim3(64 * S), 0, s, P);
+        else if (P.src_mode == SRC_UPSAMPLE) hipLaunchKernelGGL((k_jpipe<TS, S, SRC_UPSAMPLE, true>), grid, dim3(64 * S), 0, s, P);
+        else hipLaunchKernelGGL((k_jpipe<TS, S, SRC_SEED, true>), grid, dim3(64 * S), 0, s, P);
+    } else {
+        if (P.src_mode == SRC_BUF) hipLaunchKernelGGL((k_jpipe<TS, S, SRC_BUF, false>), grid, dim3(64 * S), 0, s, P);
+        else if (P.src_mode == SRC_UPSAMPLE) hipLaunchKernelGGL((k_jpipe<TS, S, SRC_UPSAMPLE, false>), grid, dim3(64 * S), 0, s, P);
+        else hipLaunchKernelGGL((k_jpipe<TS, S, SRC_SEED, false>), grid, dim3(64 * S), 0, s, P);
+    }
+}
+
+// (S, TS) pairs the pipelined engine is built for; T = S * TS
+bool jpipe_supported(int S, int TS) { return S == 2 && (TS == 5 || TS == 4); }
+
+void launch_jpipe(hipStream_t s, const JacobiPass& P, int S, int TS, int batch)
+{
+    if (S == 2 && TS == 5) launch_pipe_ts<5, 2>(s, P, batch);
+    else if (S == 2 && TS == 4) launch_pipe_ts<4, 2>(s, P, batch);
+}
+
+template <int TS, int S>
+static int pipe_waves_per_cu_t()
+{
+    int nb = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(
+            &nb, reinterpret_cast<const void*>(k_jpipe<TS, S, SRC_BUF, false>), 64 * S, 0) != hipSuccess)
+        nb = 1;
+    return nb * S;
+}
+
+int jpipe_waves_per_cu(int S, int TS)
+{
+    static int cache[2] = {0, 0};
+    const int i = TS == 5 ? 0 : 1;
+    if (!cache[i]) cache[i] = TS == 5 ? pipe_waves_per_cu_t<5, 2>() : pipe_waves_per_cu_t<4, 2>();
+    (void)S;
+    return cache[i];
 }
 
 void launch_border(hipStream_t s, const float* prev, long long pstride, LevelDims L, float* a,

@@ -538,10 +538,12 @@ __global__ void __launch_bounds__(kRegLanes) k_register(
     const GridCol* __restrict__ rcols, const GridRow* __restrict__ rrows, int ntiles,
     const float* __restrict__ emap, int ew, int eh, int ec, long long estride,
     const float* __restrict__ tiles, long long tstride, int degree, int solver,
-    float* __restrict__ coeffs, double* __restrict__ coeffs64, double* __restrict__ sums)
+    float* __restrict__ coeffs, double* __restrict__ coeffs64, double* __restrict__ sums,
+    const int* __restrict__ active)
 {
     __shared__ double part[kRegSums][kRegLanes];
     const int p = blockIdx.x, b = blockIdx.y, l = threadIdx.x;
+    if (active && !active[p]) return;  // joint solve: an inactive tile is neither read nor solved
     const TileGeom g = geom[p];
     const RegGrid rg = grids[p];
     const float* tile = tiles + b * tstride + g.off;
@@ -759,12 +761,12 @@ void launch_register(hipStream_t s, const TileGeom* geom, const RegGrid* grids,
                      const GridCol* rcols, const GridRow* rrows, int ntiles, const float* emap,
                      int ew, int eh, int ec, long long estride, const float* tiles,
                      long long tstride, int degree, int solver, float* coeffs, double* coeffs64,
-                     int batch, double* sums)
+                     int batch, double* sums, const int* active)
 {
     dim3 grid(ntiles, batch);
     hipLaunchKernelGGL(k_register, grid, dim3(kRegLanes), 0, s, geom, grids, rcols, rrows,
                        ntiles, emap, ew, eh, ec, estride, tiles, tstride, degree, solver, coeffs,
-                       coeffs64, sums);
+                       coeffs64, sums, active);
 }
 
 int register_sums_per_tile() { return kRegSums; }

@@ -24,7 +24,8 @@ EXPORTS = [
     "pf_version", "pf_set_tiles", "pf_register", "pf_fuse", "pf_merge", "pf_warp_depth",
     "pf_warp_rgb", "pf_level_info", "pf_fuse_partial", "pf_fuse_seed", "pf_fuse_finish_level",
     "pf_probe_taps", "pf_profile_enable", "pf_profile_read", "pf_error_metrics",
-    "pf_depth_transform", "pf_register_joint", "pf_set_solver",
+    "pf_depth_transform", "pf_register_joint", "pf_set_solver", "pf_fuse_normalize",
+    "pf_fuse_border", "pf_fuse_band_plan", "pf_fuse_band_pass",
 ]
 SOLVERS = {"normal": 0, "lm": 1}  # PF_SOLVER_*; "lm" = the reference's Ceres LM (default)
 
@@ -85,6 +86,11 @@ def load():
     L.pf_error_metrics.argtypes = [vp, vp, ip, ip, ip, vp, vp, ip, ip, ip, ip, fp, fp, ip, ip,
                                    vp]
     L.pf_set_solver.argtypes = [vp, ip]
+    L.pf_fuse_normalize.argtypes = [vp, vp, vp, ip, ip, fp, fp, ip, vp]
+    L.pf_fuse_border.argtypes = [vp, vp, ip, ip, fp, fp, ip, vp, vp, vp]
+    L.pf_fuse_band_plan.argtypes = [vp, ip, ip, fp, fp, ip, ip, C.POINTER(C.c_int), ip]
+    L.pf_fuse_band_pass.argtypes = [vp, vp, ip, ip, ip, vp, vp, ip, vp, vp, vp, ip, ip, fp, fp,
+                                    ip, ip, ip, ip]
     L.pf_profile_enable.argtypes = [vp, ip]
     L.pf_profile_read.argtypes = [vp, C.POINTER(C.c_double), C.POINTER(C.c_double),
                                   C.POINTER(C.c_longlong)]
@@ -281,6 +287,32 @@ class Fuser:
         self._check(self.L.pf_fuse_finish_level(self.h, _ptr(lsum), _ptr(cnt), out_w,
                                                 out_w // 2, float(zr[0]), float(zr[1]), level,
                                                 _ptr(buf), _ptr(out)))
+
+    # ---- row-band sharding of a level's sweeps (pf_dist.fuse_row_sharded) ----
+    def fuse_normalize(self, lsum, cnt, out_w, zr, level, lnorm):
+        self._check(self.L.pf_fuse_normalize(self.h, _ptr(lsum), _ptr(cnt), out_w, out_w // 2,
+                                             float(zr[0]), float(zr[1]), level, _ptr(lnorm)))
+
+    def fuse_border(self, prev, out_w, zr, level, a=None, b=None, out=None):
+        self._check(self.L.pf_fuse_border(self.h, _ptr(prev), out_w, out_w // 2, float(zr[0]),
+                                          float(zr[1]), level, _ptr(a), _ptr(b), _ptr(out)))
+
+    def fuse_band_plan(self, out_w, zr, level, nbands):
+        """Sweep depths of the level's passes (identical on every rank for the same nbands)."""
+        T = (C.c_int * 256)()
+        n = self.L.pf_fuse_band_plan(self.h, out_w, out_w // 2, float(zr[0]), float(zr[1]),
+                                     level, nbands, T, 256)
+        if n < 0:
+            self._check(n)
+        return [T[i] for i in range(n)]
+
+    def fuse_band_pass(self, lnorm, src_mode, out_w, zr, level, T, row0, row1, src=None,
+                       dst=None, prev=None, emap=None, out=None):
+        ew, eh, ec = _emap_dims(emap) if emap is not None else (0, 0, 0)
+        self._check(self.L.pf_fuse_band_pass(self.h, _ptr(emap), ew, eh, ec, _ptr(prev),
+                                             _ptr(lnorm), int(src_mode), _ptr(src), _ptr(dst),
+                                             _ptr(out), out_w, out_w // 2, float(zr[0]),
+                                             float(zr[1]), level, int(T), int(row0), int(row1)))
 
     def profile(self, on=True):
         """Enable/disable per-stage hipEvent timing (resets the accumulators)."""

@@ -7,7 +7,9 @@
   grids are summed over ranks (RCCL reduce over xGMI; gloo in the CPU tests), and rank 0
   normalises and runs the damped Jacobi sweeps (`fuse_tile_sharded`).  With every pixel covered
   by at most two tiles (the reference's layouts) the reduced sums are exactly the single-GPU
-  sums: adding zeros is exact and a + b is commutative.
+  sums: adding zeros is exact and a + b is commutative.  With three or more the reduce order
+  (RCCL's, not the reference's tile order) could round differently, so rank 0 checks the reduced
+  coverage and refuses such a layout (`CoverageError`) instead of returning different bits.
 
 The reference has no distributed code; this replaces its single-process OpenMP tile loop
 (Depth.cpp:1492-1624).
@@ -62,6 +64,13 @@ class HipTileShardBackend:
         return buf
 
 
+class CoverageError(ValueError):
+    """A pixel is covered by more than two tiles: the tile-sharded sums are no longer exact."""
+
+
+MAX_SHARDED_COVER = 2
+
+
 def fuse_tile_sharded(backend, nlevels, ntiles, rank, world, dist=None, group=None):
     """Tile-sharded fusion of one panorama.
 
@@ -79,6 +88,170 @@ def fuse_tile_sharded(backend, nlevels, ntiles, rank, world, dist=None, group=No
             dist.reduce(lsum, dst=0, op=dist.ReduceOp.SUM, group=group)
             dist.reduce(cnt, dst=0, op=dist.ReduceOp.SUM, group=group)
         if rank == 0:
+            if world > 1:
+                cover = int(cnt.max().item())
+                if cover > MAX_SHARDED_COVER:
+                    raise CoverageError(
+                        f"level {level}: a pixel is covered by {cover} tiles; the tile-sharded "
+                        f"reduce is exact only up to {MAX_SHARDED_COVER} (run this layout on one "
+                        f"GPU)")
             buf = backend.seed(level, prev)
             prev = backend.finish(level, lsum, cnt, buf, level == nlevels - 1)
     return prev if rank == 0 else None
+
+
+# ---------------------------------------------------------------------------------------------
+# Row-band sharding of the sweeps: removes the Amdahl ceiling of
+# fuse_tile_sharded, whose Jacobi runs on rank 0 alone.  Every rank scatters its tiles' targets,
+# the grids are all-reduced, and each rank sweeps its own contiguous band of rows; before every
+# pass but a level's first, the T+1 rows nearest each band edge are exchanged with the
+# neighbouring ranks (a pass of depth T reads rows row0-T-1 .. row1+T).  Each band row is
+# computed exactly as in the one-GPU fusion (the kernels are the same; the band is just the row
+# range of the chunks), so the result is bit-identical.  After a level its bands are broadcast
+# so every rank holds the full buffer the next level upsamples; the u16 bands likewise.
+
+class TorchComm:
+    """The collectives fuse_row_sharded needs, over torch.distributed (RCCL on the GPU box,
+    gloo on CPU)."""
+
+    def __init__(self, dist, group=None):
+        self.dist, self.group = dist, group
+
+    def all_reduce_sum(self, t):
+        self.dist.all_reduce(t, op=self.dist.ReduceOp.SUM, group=self.group)
+
+    def exchange(self, sends, recvs):
+        """sends: [(peer, tensor)], recvs: [(peer, tensor)]; point-to-point, all at once."""
+        ops = [self.dist.P2POp(self.dist.isend, t, peer, group=self.group) for peer, t in sends]
+        ops += [self.dist.P2POp(self.dist.irecv, t, peer, group=self.group) for peer, t in recvs]
+        if ops:
+            for req in self.dist.batch_isend_irecv(ops):
+                req.wait()
+
+    def broadcast(self, t, src):
+        import torch
+        if t.dtype == torch.int16:  # the u16 result: as bytes (gloo has no 16-bit integers)
+            t = t.view(torch.uint8)
+        self.dist.broadcast(t, src=src, group=self.group)
+
+
+def band_rows(h0, h1, rank, world):
+    """[row0, row1) of rank's band of the level rows h0..h1."""
+    lo, hi = shard_range(h1 - h0 + 1, rank, world)
+    return h0 + lo, h0 + hi
+
+
+def fuse_row_sharded(backend, nlevels, ntiles, rank, world, comm=None):
+    """One panorama's fusion with tiles AND rows sharded over `world` ranks.
+
+    backend (one rank's device):
+      partial(level, t0, t1) -> (lsum, cnt)   the targets of tiles [t0, t1), full-level grids
+      dims(level) -> (w, h, h0, h1)
+      plane(level) -> a new full-level fp32 buffer (flat)
+      normalize(level, lsum, cnt) -> lnorm
+      plan(level, nbands) -> [T, ...]          identical on every rank
+      border(level, prev, a, b)               rows outside [h0, h1] (u16 `out` on the last level)
+      band_pass(level, lnorm, src_mode, src, dst, T, row0, row1, last, prev)
+                                               src_mode 0: src, 1: upsample prev, 2: emap seed
+      out                                      the u16 result plane (flat), filled on every rank
+    comm: TorchComm (or a stand-in with the same methods); None for world == 1.
+    Returns the final level's band-assembled buffer (None for the last level, whose result is
+    backend.out)."""
+    t0, t1 = shard_range(ntiles, rank, world)
+    prev = None
+    for level in range(nlevels):
+        last = level == nlevels - 1
+        lsum, cnt = backend.partial(level, t0, t1)
+        if world > 1:
+            comm.all_reduce_sum(lsum)
+            comm.all_reduce_sum(cnt)
+            cover = int(cnt.max().item())
+            if cover > MAX_SHARDED_COVER:
+                raise CoverageError(
+                    f"level {level}: a pixel is covered by {cover} tiles; the sharded reduce is "
+                    f"exact only up to {MAX_SHARDED_COVER} (run this layout on one GPU)")
+        lnorm = backend.normalize(level, lsum, cnt)
+        w, h, h0, h1 = backend.dims(level)
+        r0, r1 = band_rows(h0, h1, rank, world)
+        plan = backend.plan(level, world)
+        if world > 1 and (h1 - h0 + 1) // world < max(plan) + 1:
+            raise ValueError(f"level {level}: {h1 - h0 + 1} band rows over {world} ranks leave "
+                             f"bands thinner than the {max(plan) + 1}-row halo")
+        a, b = backend.plane(level), backend.plane(level)
+        backend.border(level, prev, a, b)
+        src, dst = None, a
+        for i, T in enumerate(plan):
+            if i > 0 and world > 1:
+                k = T + 1
+                sends, recvs = [], []
+                if rank > 0:
+                    lo = max(r0 - k, h0)
+                    sends.append((rank - 1, src[r0 * w:min(r0 + k, r1) * w]))
+                    recvs.append((rank - 1, src[lo * w:r0 * w]))
+                if rank < world - 1:
+                    hi = min(r1 + k, h1 + 1)
+                    sends.append((rank + 1, src[max(r1 - k, r0) * w:r1 * w]))
+                    recvs.append((rank + 1, src[r1 * w:hi * w]))
+                comm.exchange(sends, recvs)
+            mode = (2 if level == 0 else 1) if i == 0 else 0
+            fin = last and i == len(plan) - 1
+            backend.band_pass(level, lnorm, mode, src, dst, T, r0, r1, fin, prev)
+            src, dst = dst, (b if dst is a else a)
+        res = backend.out if last else src
+        if world > 1:
+            for r in range(world):
+                q0, q1 = band_rows(h0, h1, r, world)
+                comm.broadcast(res[q0 * w:q1 * w], r)
+        prev = None if last else res
+    return prev
+
+
+class HipRowShardBackend:
+    """GPU backend of `fuse_row_sharded` for one rank: the panofuse band entry points on a
+    panofuse.Fuser bound to this rank's GPU.  tiles: [1, tile_elems] of the full layout (only
+    [t0, t1) is read); coeffs: [ntiles, 4] or None; out: flat int16 [out_h * out_w]."""
+
+    def __init__(self, fuser, emap, tiles, coeffs, out_w, zr, out):
+        import panofuse
+        self.fz, self.emap, self.tiles, self.coeffs = fuser, emap, tiles, coeffs
+        self.out_w, self.zr, self.out = out_w, zr, out
+        n = panofuse.level_info(out_w, out_w // 2, zr, 0)[5]
+        self.levels = [panofuse.level_info(out_w, out_w // 2, zr, lv) for lv in range(n)]
+        self.nlevels = n
+
+    def dims(self, level):
+        w, h, h0, h1 = self.levels[level][:4]
+        return w, h, h0, h1
+
+    def plane(self, level):
+        import torch
+        w, h = self.levels[level][:2]
+        return torch.empty(h * w, dtype=torch.float32, device=self.tiles.device)
+
+    def partial(self, level, t0, t1):
+        lsum, cnt = self.plane(level), self.plane(level)
+        self.fz.fuse_partial(self.tiles, self.coeffs, t0, t1, self.out_w, self.zr, level,
+                             lsum, cnt)
+        return lsum, cnt
+
+    def normalize(self, level, lsum, cnt):
+        lnorm = self.plane(level)
+        self.fz.fuse_normalize(lsum, cnt, self.out_w, self.zr, level, lnorm)
+        return lnorm
+
+    def plan(self, level, nbands):
+        return self.fz.fuse_band_plan(self.out_w, self.zr, level, nbands)
+
+    def border(self, level, prev, a, b):
+        if level == self.nlevels - 1:
+            self.fz.fuse_border(prev, self.out_w, self.zr, level, out=self.out)
+        else:
+            self.fz.fuse_border(prev, self.out_w, self.zr, level, a=a, b=b)
+
+    def band_pass(self, level, lnorm, src_mode, src, dst, T, row0, row1, last, prev):
+        self.fz.fuse_band_pass(lnorm, src_mode, self.out_w, self.zr, level, T, row0, row1,
+                               src=src if src_mode == 0 else None,
+                               dst=None if last else dst,
+                               prev=prev if src_mode == 1 else None,
+                               emap=self.emap if src_mode == 2 else None,
+                               out=self.out if last else None)
