@@ -169,7 +169,7 @@ def run_c5(args, rank, world, local, dev):
             fs.register(emap, mine, zr, degree=3, apply=False, coeffs=coeffs[t0:t1][None])
         be = pf_dist.HipTileShardBackend(fz, emap, tiles, coeffs, out_w, zr, out)
         pf_dist.fuse_tile_sharded(be, nlevels, lay.ntiles, rank, world,
-                                  dist if world > 1 else None)
+                                  pf_dist.TorchComm(dist) if world > 1 else None)
 
     for _ in range(args.warmup):
         step()

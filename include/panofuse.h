@@ -129,12 +129,26 @@ int pf_fuse_seed(pf_ctx* ctx, const float* emap, int ew, int eh, int ec, const f
 int pf_fuse_finish_level(pf_ctx* ctx, const float* lsum, const float* cnt, int out_w,
                          int out_h, float zr0, float zr1, int level, float* buf,
                          uint16_t* out);
+/* Exactness of the summed grids.  Per pixel the reference adds the covering tiles' Laplacians
+ * one at a time (Depth.cpp:1609-1617); summing per-rank partials reproduces that for pixels
+ * covered by at most two tiles, not for the few covered by three or more (sector corners on
+ * shared band rows: 7 pixels per level in the C5 layout).  pf_fuse_multicover lists their
+ * (pixel, tile) pairs (count in *npairs; contrib == NULL: count only) and writes contrib[i] =
+ * the contribution of pair i's tile if it lies in [t0, t1), else 0; summing contrib over ranks
+ * (exact: one non-zero per pair) and pf_fuse_multicover_patch then rewrites those pixels of
+ * the summed lsum in the reference's single-thread order (tiles ascending). */
+int pf_fuse_multicover(pf_ctx* ctx, const float* tiles, const float* coeffs, int t0, int t1,
+                       int out_w, int out_h, float zr0, float zr1, int level, float* contrib,
+                       int* npairs);
+int pf_fuse_multicover_patch(pf_ctx* ctx, int out_w, int out_h, float zr0, float zr1, int level,
+                             const float* contrib, float* lsum);
 
 /* ---- row-band sharding of one level's Jacobi over ranks (pf_dist.py) ----
  * Every rank holds full-size level buffers but owns the rows [row0, row1) of the band [h0, h1].
  * pf_fuse_normalize: the normalised targets of (summed) pf_fuse_partial grids.
  * pf_fuse_border: the rows outside [h0, h1] (0 at level 0, else the nearest upsample of prev)
- *   into both ping-pong buffers a and b, or into the u16 out on the last level.
+ *   into both ping-pong buffers a and b, or into the u16 out on the last level (and then, if
+ *   a / b are given, their rows h0-1 and h1+1, which the passes' halo lanes read).
  * pf_fuse_band_plan: the sweep depths T[0..n) of the level's passes (returns n), a function of
  *   (level, nbands) only, so every rank derives the same plan.
  * pf_fuse_band_pass: one pass of depth T over rows [row0, row1): reads rows row0-T-1 .. row1+T

@@ -191,8 +191,9 @@ int pf_create_depth_panoramas(const std::string& rgb_folder, const std::string& 
                               int nshards = 1);
 /* The RGB tile export of mode 0 (Main.cpp:399-430 + SaveCubeMap :242-326): every panorama of
  * rgb_folder (8/16-bit PNG, PGM/PPM) warped on the GPU (pf_warp_rgb) into the 15 LeReS tiles
- * of 1024 x round(1024/aspect) px, written as <tile_dir>/<raw>.<a0>_<a1>_<z0>_<z1>.png (rows
- * top-first, like the reference's flipped JPEG write; PNG instead of JPEG q=100). */
+ * of 1024 x round(1024/aspect) px, written as <tile_dir>/<raw>.<a0>_<a1>_<z0>_<z1>.jpg (rows
+ * top-first, like the reference's flipped write; baseline JPEG at quality 100, 4:4:4, as the
+ * reference's stbi_write_jpg call ends up, Main.cpp:319-320). */
 int pf_export_rgb_tiles(const std::string& rgb_folder, const std::string& tile_dir);
 /* The active LeReS layout (Main.cpp:788-843): 15 FOVs and ranges. */
 void pf_leres_layout(std::vector<Vec4f>& fovs, std::vector<Vec4f>& ranges);
@@ -204,4 +205,7 @@ void pf_leres_layout(std::vector<Vec4f>& fovs, std::vector<Vec4f>& ranges);
 extern "C" int pfd_load_map(const char* fn, int is_emap, float* out, long long cap, int* w,
                             int* h, int* c);
 extern "C" int pfd_save_png16(const char* fn, const uint16_t* data, int w, int h);
+/* the tile writer of the RGB export: baseline JPEG, 4:4:4, stb/IJG quality scaling (>= 100:
+ * every quantiser 1), 8-bit gray (c = 1) or RGB (c = 3) rows top-first */
+extern "C" int pfd_save_jpeg(const char* fn, const uint8_t* px, int w, int h, int c, int quality);
 extern "C" void pfd_leres_layout(float* fovs, float* ranges);

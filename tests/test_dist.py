@@ -59,6 +59,11 @@ class OracleBackend:
             n = np.zeros((lv.h, lv.w), np.int32)
         return torch.from_numpy(Ls.copy()), torch.from_numpy(n.astype(np.float32))
 
+    def multicover_count(self, level):
+        # the C1 layout covers every pixel at most twice (tests/test_oracle.py); the GPU backend
+        # handles 3+ (tests/test_gpu_rowshard.py at the C5 layout)
+        return 0
+
     def seed(self, level, prev):
         lv = self._lv(level)
         if level == 0:
@@ -85,7 +90,7 @@ def _worker(rank, world, port, q):
         emap = pf_synth.baseline_emap(seeds, 128, 64)[0].numpy()
         data = np.random.RandomState(2).rand(total).astype(np.float32)
         be = OracleBackend(O, PL, 512, emap, tiles, data)
-        final = pf_dist.fuse_tile_sharded(be, 3, lay.ntiles, rank, world, dist)
+        final = pf_dist.fuse_tile_sharded(be, 3, lay.ntiles, rank, world, pf_dist.TorchComm(dist))
         # every rank also checks the reduced level-2 targets against the single-rank sums
         lv = be._lv(2)
         ls, n = be.partial(2, *pf_dist.shard_range(lay.ntiles, rank, world))

@@ -158,8 +158,11 @@ def _png8_write_rgb(path, a):
 
 def test_export_rgb_tiles(tmp_path):
     """`panofuse_main export`: the tile render of mode 0 (SaveCubeMap, Main.cpp:242-326) for
-    the LeReS layout at 1024 x 988 px, against the oracle's restatement of the GL camera within
-    1 LSB (the a18 bar of test_gpu_parity.py); OpenGL rasterisation parity is unpinned."""
+    the LeReS layout at 1024 x 988 px, written as JPEG at quality 100 / 4:4:4 (Main.cpp:320)
+    and decoded here by libjpeg (PIL), against the oracle's restatement of the GL camera: the
+    warp's 1 LSB bar (test_gpu_parity.py) plus the JPEG round trip's (tests/test_io.py), i.e.
+    within 4 levels, mean under 0.5.  OpenGL rasterisation parity is unpinned."""
+    Image = pytest.importorskip("PIL.Image")
     (tmp_path / "rgb").mkdir()
     h, w = 512, 1024
     rs = np.random.RandomState(9)
@@ -176,12 +179,15 @@ def test_export_rgb_tiles(tmp_path):
     off = 0
     for t in range(lay.ntiles):
         f = [_cround(float(v) / MYPI * 180.0) for v in lay.fovs[t]]
-        got = _png8_read(tmp_path / "tiles" / f"room7.{f[0]}_{f[1]}_{f[2]}_{f[3]}.png")
+        fn = tmp_path / "tiles" / f"room7.{f[0]}_{f[1]}_{f[2]}_{f[3]}.jpg"
+        im = Image.open(fn)
+        assert im.format == "JPEG" and im.mode == "RGB"
+        got = np.asarray(im)
         assert got.shape == (988, 1024, 3)
         n = 988 * 1024 * 3
         d = np.abs(got.reshape(-1).astype(np.int32) - ref[off:off + n].astype(np.int32))
         off += n
-        assert d.max() <= 1 and (d > 0).mean() < 1e-3, (t, d.max(), (d > 0).mean())
+        assert d.max() <= 4 and d.mean() < 0.5, (t, d.max(), d.mean())
 
 
 def test_mode0_cli_jpeg_inputs(tmp_path):

@@ -153,11 +153,20 @@ def test_c5_tile_sharded_pipeline_equals_fuse(fuser):
     be = pf_dist.HipTileShardBackend(fz, emap, tiles, coeffs[0], out_w, ZR, out)
 
     class SumBackend:
+        """Rank 0's view of the 8-rank reduce: partials summed over the simulated ranks, then the
+        pixels covered by 3+ tiles (7 per level at this layout) re-added in tile order from the
+        per-rank contributions, as fuse_tile_sharded does at world > 1."""
         def partial(self, level, t0, t1):
             acc = None
+            contrib = None
             for r in range(world):
-                l, n = be.partial(level, *pf_dist.shard_range(lay.ntiles, r, world))
+                q0, q1 = pf_dist.shard_range(lay.ntiles, r, world)
+                l, n = be.partial(level, q0, q1)
                 acc = (l, n) if acc is None else (acc[0] + l, acc[1] + n)
+                c = be.multicover(level, q0, q1)
+                contrib = c if contrib is None else contrib + c
+            assert be.multicover_count(level) == 4 * 7  # 7 pixels x 4 tiles (tests/test_oracle.py)
+            be.multicover_patch(level, contrib, acc[0])
             return acc
 
         seed, finish = be.seed, be.finish

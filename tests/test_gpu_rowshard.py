@@ -5,7 +5,9 @@ The ranks are simulated on one GPU: one thread and one panofuse context per rank
 same stream, with an in-process communicator standing in for RCCL (all-reduce, halo exchange,
 band broadcast).  The result of every rank must equal the one-GPU pf_fuse bit for bit, at C2
 (3 levels, 2 and 3 bands) and at the C5 layout (8192x4096, 4 levels, 4 bands, tiles sharded
-too).  The collectives themselves are covered over gloo in tests/test_dist.py.
+too, including the pixels covered by four tiles), and likewise the tiles-only flow
+(fuse_tile_sharded, 8 ranks).  The collectives themselves are covered over gloo in
+tests/test_dist.py.
 """
 import threading
 
@@ -49,6 +51,9 @@ class ThreadComm:
                 t.copy_(outer.box["ar"])
                 outer.bar.wait()
 
+            def reduce_sum(self, t, dst):
+                self.all_reduce_sum(t)
+
             def exchange(self, sends, recvs):
                 for peer, t in sends:
                     outer.box[("x", r, peer)] = t.clone()
@@ -68,7 +73,7 @@ class ThreadComm:
         return RankComm()
 
 
-def _run(cfg, world, seed):
+def _run(cfg, world, seed, flow="rows"):
     lay = PL.config_layout(cfg)
     out_w, ew = PL.CONFIGS["C5" if cfg == "C5" else "C2"]
     seeds = pf_synth.seeds_for(1, seed)
@@ -92,8 +97,14 @@ def _run(cfg, world, seed):
             f = panofuse.Fuser(0)
             f.set_tiles(lay)
             out = torch.zeros(out_w * (out_w // 2), dtype=torch.int16, device=DEV)
-            be = pf_dist.HipRowShardBackend(f, emap, tiles, coeffs[0], out_w, ZR, out)
-            pf_dist.fuse_row_sharded(be, be.nlevels, lay.ntiles, r, world, comm.rank(r))
+            if flow == "rows":
+                be = pf_dist.HipRowShardBackend(f, emap, tiles, coeffs[0], out_w, ZR, out)
+                pf_dist.fuse_row_sharded(be, be.nlevels, lay.ntiles, r, world, comm.rank(r))
+            else:  # tiles only: rank 0 sweeps
+                be = pf_dist.HipTileShardBackend(f, emap, tiles, coeffs[0], out_w, ZR,
+                                                 out.view(out_w // 2, out_w))
+                nlev = panofuse.level_info(out_w, out_w // 2, ZR, 0)[5]
+                pf_dist.fuse_tile_sharded(be, nlev, lay.ntiles, r, world, comm.rank(r))
             torch.cuda.synchronize()
             outs[r] = out
             f.close()
@@ -107,7 +118,7 @@ def _run(cfg, world, seed):
     for t in th:
         t.join(300)
     assert not errs, errs
-    for r in range(world):
+    for r in range(world if flow == "rows" else 1):
         diff = (outs[r].view(out_w // 2, out_w) != ref[0]).sum(1)
         rows = torch.nonzero(diff).flatten().tolist()
         assert not rows, (f"rank {r}: {int(diff.sum())} pixels differ from the one-GPU fusion in "
@@ -121,3 +132,9 @@ def test_row_sharded_c2_equals_fuse(world):
 
 def test_row_sharded_c5_equals_fuse():
     _run("C5", 4, 20261015 + 12)
+
+
+def test_tile_sharded_c5_threads_equals_fuse():
+    """fuse_tile_sharded at world 8 (reduce to rank 0, the 7 pixels per level covered by four
+    tiles re-added in tile order): rank 0's u16 == the one-GPU fusion."""
+    _run("C5", 8, 20261015 + 13, flow="tiles")

@@ -28,6 +28,8 @@ def lib():
     L.pfd_load_map.argtypes = [C.c_char_p, C.c_int, fp, C.c_longlong, ip, ip, ip]
     L.pfd_save_png16.argtypes = [C.c_char_p, C.POINTER(C.c_uint16), C.c_int, C.c_int]
     L.pfd_leres_layout.argtypes = [fp, fp]
+    L.pfd_save_jpeg.argtypes = [C.c_char_p, C.POINTER(C.c_uint8), C.c_int, C.c_int, C.c_int,
+                                C.c_int]
     return L
 
 
@@ -279,3 +281,48 @@ def test_image_decoders_fuzz_sanitized(tmp_path):
 def subprocess_run(cmd, timeout=300):
     import subprocess
     return subprocess.run(cmd, capture_output=True, text=True, timeout=timeout)
+
+
+@pytest.mark.parametrize("mode,quality", [("RGB", 3072), ("L", 100), ("RGB", 95)])
+def test_jpeg_writer_roundtrip(lib, tmp_path, mode, quality):
+    """The tile writer of the RGB export (pfd_save_jpeg; the reference's stbi_write_jpg at
+    quality width*3, clamped to 100, 4:4:4, Main.cpp:320, stb_image_write.h:1448-1451): a
+    baseline JFIF file that libjpeg (PIL) reads as 4:4:4 with all-one quantisers at quality
+    >= 100.  Bar: decoded by libjpeg and by the in-tree decoder, the error against the input is
+    no worse than libjpeg's own encoder at the same quality and sampling (max + 1 level, mean
+    x 1.15); odd sizes exercise the edge blocks."""
+    import io
+    Image = pytest.importorskip("PIL.Image")
+    rng = np.random.default_rng(3)
+    h, w = 67, 93
+    yy, xx = np.mgrid[0:h, 0:w]
+    base = np.sin(xx / 7.0) * 70 + np.cos(yy / 5.0) * 40 + 128
+    if mode == "L":
+        a = np.clip(base + rng.normal(0, 3, (h, w)), 0, 255).astype(np.uint8)
+        c = 1
+    else:
+        a = np.clip(np.stack([base, 255 - base, (xx * 3 + yy) % 256], -1) +
+                    rng.normal(0, 3, (h, w, 3)), 0, 255).astype(np.uint8)
+        c = 3
+    fn = tmp_path / "w.jpg"
+    arr = np.ascontiguousarray(a)
+    assert lib.pfd_save_jpeg(str(fn).encode(), arr.ctypes.data_as(C.POINTER(C.c_uint8)), w, h,
+                             c, quality) == 0
+    im = Image.open(fn)
+    assert im.format == "JPEG" and im.size == (w, h) and im.mode == mode
+    if quality >= 100:
+        assert all(v == 1 for t in im.quantization.values() for v in t)
+    if c == 3:
+        assert im.layer[0][1:3] == (1, 1) and im.layer[1][1:3] == (1, 1)  # 4:4:4
+    buf = io.BytesIO()  # libjpeg's own encoder at the same settings, the yardstick
+    Image.fromarray(a, mode).save(buf, "JPEG", quality=min(quality, 100), subsampling=0)
+    buf.seek(0)
+    e = np.abs(np.asarray(Image.open(buf)).astype(np.int32) - a.astype(np.int32))
+    d = np.abs(np.asarray(im).astype(np.int32) - a.astype(np.int32))
+    assert d.max() <= e.max() + 1 and d.mean() <= 1.15 * e.mean() + 0.02, (d.max(), d.mean(),
+                                                                            e.max(), e.mean())
+    got = _load(lib, fn, 0)
+    got = np.rint(got * 255.0).astype(np.int32).reshape(a.shape)
+    d = np.abs(got - a.astype(np.int32))
+    assert d.max() <= e.max() + 1 and d.mean() <= 1.15 * e.mean() + 0.02, (d.max(), d.mean(),
+                                                                            e.max(), e.mean())

@@ -232,3 +232,23 @@ def test_golden_large_regression():
     assert np.array_equal(abcd, g["W4096_abcd"])
     assert np.array_equal(out.ravel()[::int(g["stride"])], g["W4096_out_sub"])
     assert hashlib.sha256(out.tobytes()).digest() == g["W4096_out_sha256"].tobytes()
+
+
+def test_layout_coverage_counts():
+    """Per-pixel tile coverage of the BASELINE layouts (the sharded fusion's exactness argument,
+    pf_dist.py): at most 2 for C1, C2 and LeReS at every level; the C5 layout has exactly 7
+    pixels per level covered by 4 tiles (column w/2, where the float-rounded 180-degree sector
+    edges round to the same column, on the shared rows of two zenith bands)."""
+    for cfg, out_w in (("C1", 512), ("C2", 2048), ("LERES", 2048), ("C5", 8192)):
+        lay = PL.config_layout(cfg)
+        tiles, total = O.make_tiles(lay)
+        data = np.zeros(total, np.float32)
+        for level in range(O.num_levels(out_w)):
+            lv = O.level_dims(out_w, out_w // 2, ZR, level)
+            _, n, _, _ = O.targets(tiles, data, lv)
+            many = np.argwhere(n > 2)
+            if cfg != "C5":
+                assert n.max() <= 2, (cfg, level)
+            else:
+                assert n.max() == 4 and len(many) == 7, (level, len(many))
+                assert set(many[:, 1].tolist()) == {lv.w // 2}

@@ -34,6 +34,10 @@ struct LevelCache {
     int nlevels = 0;
     LevelDims dims[4];
     DevBuf box[4], cols[4], rows[4], tapbox[4], tapmap[4], hcol[4];
+    // (pixel, tile) pairs of the pixels covered by three or more tiles, sorted by pixel then
+    // tile (the sharded fusion recomputes their sums in tile order: pf_fuse_multicover)
+    DevBuf mcpairs[4];
+    int nmc[4] = {0, 0, 0, 0};
     std::vector<TileBox> box_h[4];
     // separable-coverage certificate of each level: a band pixel is covered iff it lies in rows
     // h0+1..h1-1 and in a column of a fixed set that excludes column 0.  Enables the packed
@@ -290,6 +294,7 @@ void pf_destroy(pf_ctx* c)
         release(c->lc.tapbox[l]);
         release(c->lc.tapmap[l]);
         release(c->lc.hcol[l]);
+        release(c->lc.mcpairs[l]);
     }
 
     for (auto& s : c->spans) {
@@ -584,6 +589,22 @@ static int prepare_levels(pf_ctx* c, int out_w, int out_h, float zr0, float zr1)
                                     X, Y, PF_MAX_COVER);
         }
         lc.box_h[l] = boxes;
+        {
+            std::vector<int2> mc;
+            for (size_t o = 0; o < cover.size(); o++) {
+                if (cover[o] <= 2) continue;
+                const int Y = (int)(o / L.w), X = (int)(o % L.w);
+                for (int p = 0; p < c->ntiles; p++) {
+                    const TileBox& b = boxes[p];
+                    const bool in = Y >= b.y0 && Y <= b.y1 &&
+                                    (b.xs > 0 ? (X >= b.x0 && X < b.x1) : (X <= b.x0 && X > b.x1));
+                    if (in) mc.push_back(make_int2((int)o, p));
+                }
+            }
+            lc.nmc[l] = (int)mc.size();
+            int rc2;
+            if ((rc2 = upload(c, lc.mcpairs[l], mc))) return rc2;
+        }
         std::vector<float> hcol(L.w, 0.0f);
         bool full = L.h0 + 1 < L.h1;
         for (int X = 0; X < L.w && full; X++)
@@ -1266,6 +1287,43 @@ int pf_fuse_normalize(pf_ctx* c, const float* lsum, const float* cnt, int out_w,
     return PF_OK;
 }
 
+int pf_fuse_multicover(pf_ctx* c, const float* tiles, const float* coeffs, int t0, int t1,
+                       int out_w, int out_h, float zr0, float zr1, int level, float* contrib,
+                       int* npairs)
+{
+    int rc;
+    if ((rc = check_common(c, 1))) return rc;
+    if ((rc = prepare_levels(c, out_w, out_h, zr0, zr1))) return rc;
+    const LevelCache& lc = c->lc;
+    if (level < 0 || level >= lc.nlevels) return fail(c, PF_EINVAL, "bad level %d", level);
+    if (npairs) *npairs = lc.nmc[level];
+    if (!contrib || lc.nmc[level] == 0) return PF_OK;
+    if (!tiles) return fail(c, PF_EINVAL, "NULL tiles");
+    if (t0 < 0 || t1 > c->ntiles || t0 > t1)
+        return fail(c, PF_EINVAL, "tile range [%d,%d) outside [0,%d)", t0, t1, c->ntiles);
+    launch_multicover(c->stream, (const TileGeom*)c->geom.p, (const int2*)lc.mcpairs[level].p,
+                      lc.nmc[level], t0, t1, (const GridCol*)lc.cols[level].p,
+                      (const GridRow*)lc.rows[level].p, tiles, coeffs, lc.dims[level], contrib);
+    HIPCHK(c, hipGetLastError());
+    return PF_OK;
+}
+
+int pf_fuse_multicover_patch(pf_ctx* c, int out_w, int out_h, float zr0, float zr1, int level,
+                             const float* contrib, float* lsum)
+{
+    int rc;
+    if ((rc = check_common(c, 1))) return rc;
+    if ((rc = prepare_levels(c, out_w, out_h, zr0, zr1))) return rc;
+    const LevelCache& lc = c->lc;
+    if (level < 0 || level >= lc.nlevels) return fail(c, PF_EINVAL, "bad level %d", level);
+    if (lc.nmc[level] == 0) return PF_OK;
+    if (!contrib || !lsum) return fail(c, PF_EINVAL, "NULL buffer");
+    launch_multicover_patch(c->stream, (const int2*)lc.mcpairs[level].p, lc.nmc[level], contrib,
+                            lsum);
+    HIPCHK(c, hipGetLastError());
+    return PF_OK;
+}
+
 int pf_fuse_border(pf_ctx* c, const float* prev, int out_w, int out_h, float zr0, float zr1,
                    int level, float* a, float* b, uint16_t* out)
 {
@@ -1281,7 +1339,7 @@ int pf_fuse_border(pf_ctx* c, const float* prev, int out_w, int out_h, float zr0
     const long long st = (long long)L.w * L.h;
     const long long pst = level > 0 ? (long long)lc.dims[level - 1].w * lc.dims[level - 1].h : 0;
     launch_border(c->stream, level == 0 ? nullptr : prev, pst, L, a, b, st, last ? out : nullptr,
-                  st, 1);
+                  st, 1);  // last level: a / b (if given) get the rows h0-1 and h1+1
     HIPCHK(c, hipGetLastError());
     return PF_OK;
 }

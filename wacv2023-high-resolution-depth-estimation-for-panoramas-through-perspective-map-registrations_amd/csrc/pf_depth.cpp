@@ -864,13 +864,15 @@ int pf_export_rgb_tiles(const std::string& rgb_folder, const std::string& tile_d
         size_t off = 0;
         for (int i = 0; i < n; ++i) {
             char name[512];
-            std::snprintf(name, sizeof(name), "%s.%d_%d_%d_%d.png", rawname.c_str(),
+            std::snprintf(name, sizeof(name), "%s.%d_%d_%d_%d.jpg", rawname.c_str(),
                           (int)std::round(fovs[i][0] / PF_MYPI_D * 180.0),
                           (int)std::round(fovs[i][1] / PF_MYPI_D * 180.0),
                           (int)std::round(fovs[i][2] / PF_MYPI_D * 180.0),
                           (int)std::round(fovs[i][3] / PF_MYPI_D * 180.0));
-            if (!pfio::save_png8((fs::path(tile_dir) / name).string(), tiles.data() + off, tw[i],
-                                 th[i], 3, err)) {
+            // stbi_write_jpg(filename, w, h, 3, data, w * 3): the reference passes the row stride
+            // as the quality, which stb clamps to 100 (no chroma subsampling), Main.cpp:319-320
+            if (!pfio::save_jpeg((fs::path(tile_dir) / name).string(), tiles.data() + off, tw[i],
+                                 th[i], 3, tw[i] * 3, err)) {
                 std::cout << "[SaveCubeMap] " << err << std::endl;
                 return 1;
             }
@@ -897,6 +899,16 @@ extern "C" int pfd_load_map(const char* fn, int is_emap, float* out, long long c
     *c = C;
     const long long n = (long long)W * H * C;
     if (out && cap >= n) std::memcpy(out, is_emap ? e.data : p.data, sizeof(float) * n);
+    return 0;
+}
+
+extern "C" int pfd_save_jpeg(const char* fn, const uint8_t* px, int w, int h, int c, int quality)
+{
+    std::string err;
+    if (!pfio::save_jpeg(fn, px, w, h, c, quality, err)) {
+        std::cout << "[pfd_save_jpeg] " << err << std::endl;
+        return -1;
+    }
     return 0;
 }
 

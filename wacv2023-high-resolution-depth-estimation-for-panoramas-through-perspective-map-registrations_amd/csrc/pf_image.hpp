@@ -35,5 +35,12 @@ bool save_png16(const std::string& fn, const uint16_t* data, int w, int h, std::
 bool decode_jpeg(const std::vector<uint8_t>& f, Image& out, std::string& err);
 bool save_png8(const std::string& fn, const uint8_t* data, int w, int h, int c,
                std::string& err);
+// Baseline JPEG writer (pf_jpeg.cpp): 8-bit gray (c = 1) or RGB (c = 3), 4:4:4, the stb/IJG
+// quality scaling of the Annex K tables (quality 100: every quantiser 1), as stbi_write_jpg is
+// called by the reference's tile export (Main.cpp:320).
+bool encode_jpeg(const uint8_t* px, int w, int h, int c, int quality, std::vector<uint8_t>& out,
+                 std::string& err);
+bool save_jpeg(const std::string& fn, const uint8_t* px, int w, int h, int c, int quality,
+               std::string& err);
 
 }  // namespace pfio

@@ -191,6 +191,11 @@ void launch_targets_partial(hipStream_t s, const TileGeom* geom, const TileBox* 
                             float* cnt);
 void launch_normalize(hipStream_t s, const float* lsum, const float* cnt, LevelDims L,
                       float* lnorm);
+void launch_multicover(hipStream_t s, const TileGeom* geom, const int2* pairs, int npairs,
+                       int t0, int t1, const GridCol* cols, const GridRow* rows,
+                       const float* tiles, const float* coeffs, LevelDims L, float* contrib);
+void launch_multicover_patch(hipStream_t s, const int2* pairs, int npairs, const float* contrib,
+                             float* lsum);
 void launch_probe_taps(hipStream_t s, const TileGeom* geom, const TileBox* box, int ntiles,
                        const GridCol* cols, const GridRow* rows, LevelDims L, int32_t* out);
 void launch_jacobi(hipStream_t s, float* buf_a, float* buf_b, const float* lnorm,

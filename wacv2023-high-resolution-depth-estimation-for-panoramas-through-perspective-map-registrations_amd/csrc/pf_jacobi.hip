@@ -133,8 +133,8 @@ struct JLag {
     int rlo, rhi;  // rows loads are clamped to: the band [h0, h1].  A band pixel never reads a
                    // row outside it except as a neighbour of the un-windowed rows h0 / h1,
                    // whose update ignores its neighbours -- in the packed form through a zero
-                   // factor, which needs the neighbours finite: the rows outside the band are
-                   // never stored by a pass, so on the last level they may hold anything
+                   // factor, which needs the neighbours finite.  A halo lane's virtual columns
+                   // past a row end still reach rows h0-1 / h1+1, which k_border keeps finite
     const float *src, *prev, *emap, *lnorm;
     float* dst;
     uint16_t* out;
@@ -890,7 +890,7 @@ __global__ void __launch_bounds__(64 * S) k_jpipe(JacobiPass P)
 
 // Out-of-band rows of a level: 0 (level 0, Depth.cpp:1449-1452) or the nearest upsample of the
 // previous level (Depth.cpp:1467-1485); stored to both ping-pong buffers, or quantised into the
-// u16 output on the last level.
+// u16 output on the last level (where the ping-pong buffers get only the rows h0-1 and h1+1).
 __global__ void __launch_bounds__(256) k_border(const float* __restrict__ prev, long long pstride,
                                                 LevelDims L, float* __restrict__ a,
                                                 float* __restrict__ bb, long long stride,
@@ -910,6 +910,13 @@ __global__ void __launch_bounds__(256) k_border(const float* __restrict__ prev, 
         if (q < 0) q = 0;
         if (q > 1) q = 1;
         out[b * ostride + o] = (uint16_t)(q * 65535.0f);
+        // the rows next to the band: a pass's loads clamp rows to [h0, h1], but a halo lane's
+        // virtual columns past either row end still reach rows h0-1 / h1+1 (the neighbours of
+        // the un-windowed rows, whose zero factor needs them finite; JLag::rlo)
+        if (a && (y == L.h0 - 1 || y == L.h1 + 1)) {
+            a[b * stride + o] = v;
+            bb[b * stride + o] = v;
+        }
     } else {
         a[b * stride + o] = v;
         bb[b * stride + o] = v;

@@ -12,6 +12,7 @@
 #include "pf_image.hpp"
 
 #include <cmath>
+#include <cstdio>
 #include <cstring>
 
 namespace pfio {
@@ -374,6 +375,248 @@ bool decode_jpeg(const std::vector<uint8_t>& f, Image& out, std::string& err)
         out.px8[3 * i + 2] = clamp8((int)std::lround(Y + 1.772 * cb));
     }
     return true;
+}
+
+
+// ---------------------------------------------------------------------------------------------
+// Baseline JPEG encoder for the RGB tile export: the reference writes each
+// rendered tile with stbi_write_jpg(..., quality = width*3) (Main.cpp:320), which stb clamps to
+// 100 with no chroma subsampling (stb_image_write.h:1448-1451).  Written here from T.81: JFIF
+// APP0, the Annex K example quantisation tables scaled by the stb/IJG quality rule (all ones at
+// 100), 4:4:4 sampling, the Annex K.3 Huffman tables, full-precision DCT (double) with the
+// quantised coefficients rounded half away from zero.  The bytes are not stb's (its float AAN
+// DCT rounds differently); decoded samples agree with the input to a level or two.
+namespace {
+
+const uint8_t kLumQ[64] = {16, 11, 10, 16, 24,  40,  51,  61,  12, 12, 14, 19, 26,  58,  60,  55,
+                           14, 13, 16, 24, 40,  57,  69,  56,  14, 17, 22, 29, 51,  87,  80,  62,
+                           18, 22, 37, 56, 68,  109, 103, 77,  24, 35, 55, 64, 81,  104, 113, 92,
+                           49, 64, 78, 87, 103, 121, 120, 101, 72, 92, 95, 98, 112, 100, 103, 99};
+const uint8_t kChrQ[64] = {17, 18, 24, 47, 99, 99, 99, 99, 18, 21, 26, 66, 99, 99, 99, 99,
+                           24, 26, 56, 99, 99, 99, 99, 99, 47, 66, 99, 99, 99, 99, 99, 99,
+                           99, 99, 99, 99, 99, 99, 99, 99, 99, 99, 99, 99, 99, 99, 99, 99,
+                           99, 99, 99, 99, 99, 99, 99, 99, 99, 99, 99, 99, 99, 99, 99, 99};
+// Annex K.3: {bits[1..16], values}
+const uint8_t kDcLumBits[16] = {0, 1, 5, 1, 1, 1, 1, 1, 1, 0, 0, 0, 0, 0, 0, 0};
+const uint8_t kDcLumVal[12] = {0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11};
+const uint8_t kDcChrBits[16] = {0, 3, 1, 1, 1, 1, 1, 1, 1, 1, 1, 0, 0, 0, 0, 0};
+const uint8_t kDcChrVal[12] = {0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11};
+const uint8_t kAcLumBits[16] = {0, 2, 1, 3, 3, 2, 4, 3, 5, 5, 4, 4, 0, 0, 1, 0x7d};
+const uint8_t kAcLumVal[162] = {
+    0x01, 0x02, 0x03, 0x00, 0x04, 0x11, 0x05, 0x12, 0x21, 0x31, 0x41, 0x06, 0x13, 0x51, 0x61,
+    0x07, 0x22, 0x71, 0x14, 0x32, 0x81, 0x91, 0xa1, 0x08, 0x23, 0x42, 0xb1, 0xc1, 0x15, 0x52,
+    0xd1, 0xf0, 0x24, 0x33, 0x62, 0x72, 0x82, 0x09, 0x0a, 0x16, 0x17, 0x18, 0x19, 0x1a, 0x25,
+    0x26, 0x27, 0x28, 0x29, 0x2a, 0x34, 0x35, 0x36, 0x37, 0x38, 0x39, 0x3a, 0x43, 0x44, 0x45,
+    0x46, 0x47, 0x48, 0x49, 0x4a, 0x53, 0x54, 0x55, 0x56, 0x57, 0x58, 0x59, 0x5a, 0x63, 0x64,
+    0x65, 0x66, 0x67, 0x68, 0x69, 0x6a, 0x73, 0x74, 0x75, 0x76, 0x77, 0x78, 0x79, 0x7a, 0x83,
+    0x84, 0x85, 0x86, 0x87, 0x88, 0x89, 0x8a, 0x92, 0x93, 0x94, 0x95, 0x96, 0x97, 0x98, 0x99,
+    0x9a, 0xa2, 0xa3, 0xa4, 0xa5, 0xa6, 0xa7, 0xa8, 0xa9, 0xaa, 0xb2, 0xb3, 0xb4, 0xb5, 0xb6,
+    0xb7, 0xb8, 0xb9, 0xba, 0xc2, 0xc3, 0xc4, 0xc5, 0xc6, 0xc7, 0xc8, 0xc9, 0xca, 0xd2, 0xd3,
+    0xd4, 0xd5, 0xd6, 0xd7, 0xd8, 0xd9, 0xda, 0xe1, 0xe2, 0xe3, 0xe4, 0xe5, 0xe6, 0xe7, 0xe8,
+    0xe9, 0xea, 0xf1, 0xf2, 0xf3, 0xf4, 0xf5, 0xf6, 0xf7, 0xf8, 0xf9, 0xfa};
+const uint8_t kAcChrBits[16] = {0, 2, 1, 2, 4, 4, 3, 4, 7, 5, 4, 4, 0, 1, 2, 0x77};
+const uint8_t kAcChrVal[162] = {
+    0x00, 0x01, 0x02, 0x03, 0x11, 0x04, 0x05, 0x21, 0x31, 0x06, 0x12, 0x41, 0x51, 0x07, 0x61,
+    0x71, 0x13, 0x22, 0x32, 0x81, 0x08, 0x14, 0x42, 0x91, 0xa1, 0xb1, 0xc1, 0x09, 0x23, 0x33,
+    0x52, 0xf0, 0x15, 0x62, 0x72, 0xd1, 0x0a, 0x16, 0x24, 0x34, 0xe1, 0x25, 0xf1, 0x17, 0x18,
+    0x19, 0x1a, 0x26, 0x27, 0x28, 0x29, 0x2a, 0x35, 0x36, 0x37, 0x38, 0x39, 0x3a, 0x43, 0x44,
+    0x45, 0x46, 0x47, 0x48, 0x49, 0x4a, 0x53, 0x54, 0x55, 0x56, 0x57, 0x58, 0x59, 0x5a, 0x63,
+    0x64, 0x65, 0x66, 0x67, 0x68, 0x69, 0x6a, 0x73, 0x74, 0x75, 0x76, 0x77, 0x78, 0x79, 0x7a,
+    0x82, 0x83, 0x84, 0x85, 0x86, 0x87, 0x88, 0x89, 0x8a, 0x92, 0x93, 0x94, 0x95, 0x96, 0x97,
+    0x98, 0x99, 0x9a, 0xa2, 0xa3, 0xa4, 0xa5, 0xa6, 0xa7, 0xa8, 0xa9, 0xaa, 0xb2, 0xb3, 0xb4,
+    0xb5, 0xb6, 0xb7, 0xb8, 0xb9, 0xba, 0xc2, 0xc3, 0xc4, 0xc5, 0xc6, 0xc7, 0xc8, 0xc9, 0xca,
+    0xd2, 0xd3, 0xd4, 0xd5, 0xd6, 0xd7, 0xd8, 0xd9, 0xda, 0xe2, 0xe3, 0xe4, 0xe5, 0xe6, 0xe7,
+    0xe8, 0xe9, 0xea, 0xf2, 0xf3, 0xf4, 0xf5, 0xf6, 0xf7, 0xf8, 0xf9, 0xfa};
+
+struct Code {
+    uint16_t code[256];
+    uint8_t len[256];
+};
+
+Code make_codes(const uint8_t* bits, const uint8_t* vals)
+{  // canonical Huffman codes (T.81 Annex C)
+    Code c{};
+    int k = 0, code = 0;
+    for (int l = 1; l <= 16; l++) {
+        for (int i = 0; i < bits[l - 1]; i++, k++) {
+            c.code[vals[k]] = (uint16_t)code++;
+            c.len[vals[k]] = (uint8_t)l;
+        }
+        code <<= 1;
+    }
+    return c;
+}
+
+struct BitOut {
+    std::vector<uint8_t>& o;
+    uint32_t acc = 0;
+    int n = 0;
+    explicit BitOut(std::vector<uint8_t>& out) : o(out) {}
+    void put(uint32_t v, int k)
+    {
+        acc = (acc << k) | (v & ((1u << k) - 1));
+        n += k;
+        while (n >= 8) {
+            const uint8_t b = (uint8_t)(acc >> (n - 8));
+            o.push_back(b);
+            if (b == 0xFF) o.push_back(0);  // byte stuffing
+            n -= 8;
+        }
+    }
+    void flush()
+    {
+        if (n > 0) put(0x7F, 8 - n);  // pad with 1 bits
+    }
+};
+
+void put16(std::vector<uint8_t>& o, int v)
+{
+    o.push_back((uint8_t)(v >> 8));
+    o.push_back((uint8_t)v);
+}
+
+void encode_block(BitOut& bo, const double* px, const uint8_t* q, int& pred, const Code& dc,
+                  const Code& ac)
+{
+    static double cosv[8][8];
+    static bool init = false;
+    if (!init) {
+        for (int u = 0; u < 8; u++)
+            for (int x = 0; x < 8; x++) cosv[u][x] = std::cos((2 * x + 1) * u * M_PI / 16.0);
+        init = true;
+    }
+    int zz[64];
+    for (int v = 0; v < 8; v++)
+        for (int u = 0; u < 8; u++) {
+            double s = 0;
+            for (int y = 0; y < 8; y++)
+                for (int x = 0; x < 8; x++) s += px[y * 8 + x] * cosv[u][x] * cosv[v][y];
+            const double cu = u ? 1.0 : M_SQRT1_2, cv = v ? 1.0 : M_SQRT1_2;
+            const double f = 0.25 * cu * cv * s / q[v * 8 + u];
+            zz[v * 8 + u] = (int)(f < 0 ? f - 0.5 : f + 0.5);
+        }
+    auto mag = [](int v, int& nb) {
+        int a = v < 0 ? -v : v;
+        nb = 0;
+        while (a) { nb++; a >>= 1; }
+        return v < 0 ? v + (1 << nb) - 1 : v;
+    };
+    int nb;
+    const int diff = zz[0] - pred;
+    pred = zz[0];
+    const int dv = mag(diff, nb);
+    bo.put(dc.code[nb], dc.len[nb]);
+    if (nb) bo.put((uint32_t)dv, nb);
+    int run = 0;
+    for (int k = 1; k < 64; k++) {
+        const int v = zz[kZig[k]];
+        if (v == 0) { run++; continue; }
+        while (run > 15) { bo.put(ac.code[0xF0], ac.len[0xF0]); run -= 16; }
+        const int av = mag(v, nb);
+        const int sym = (run << 4) | nb;
+        bo.put(ac.code[sym], ac.len[sym]);
+        bo.put((uint32_t)av, nb);
+        run = 0;
+    }
+    if (run) bo.put(ac.code[0], ac.len[0]);  // EOB
+}
+
+}  // namespace
+
+bool encode_jpeg(const uint8_t* px, int w, int h, int c, int quality, std::vector<uint8_t>& o,
+                 std::string& err)
+{
+    if (!px || w < 1 || h < 1 || w > 65535 || h > 65535 || (c != 1 && c != 3)) {
+        err = "encode_jpeg: bad image";
+        return false;
+    }
+    // quality scaling of the Annex K tables, as stb / IJG (stb_image_write.h:1448-1458)
+    int qs = quality ? quality : 90;
+    qs = qs < 1 ? 1 : (qs > 100 ? 100 : qs);
+    qs = qs < 50 ? 5000 / qs : 200 - qs * 2;
+    uint8_t ql[64], qc[64];  // natural (row-major) order
+    for (int i = 0; i < 64; i++) {
+        const int a = (kLumQ[i] * qs + 50) / 100, b = (kChrQ[i] * qs + 50) / 100;
+        ql[i] = (uint8_t)(a < 1 ? 1 : (a > 255 ? 255 : a));
+        qc[i] = (uint8_t)(b < 1 ? 1 : (b > 255 ? 255 : b));
+    }
+    o.clear();
+    const uint8_t soi_app0[] = {0xFF, 0xD8, 0xFF, 0xE0, 0, 16, 'J', 'F', 'I', 'F', 0, 1, 1, 0,
+                                0, 1, 0, 1, 0, 0};
+    o.insert(o.end(), soi_app0, soi_app0 + sizeof(soi_app0));
+    const int ntab = c == 3 ? 2 : 1;  // DQT (zig-zag order)
+    o.push_back(0xFF); o.push_back(0xDB); put16(o, 2 + 65 * ntab);
+    for (int t = 0; t < ntab; t++) {
+        o.push_back((uint8_t)t);
+        for (int k = 0; k < 64; k++) o.push_back(t ? qc[kZig[k]] : ql[kZig[k]]);
+    }
+    o.push_back(0xFF); o.push_back(0xC0); put16(o, 8 + 3 * c);  // SOF0, 4:4:4
+    o.push_back(8); put16(o, h); put16(o, w); o.push_back((uint8_t)c);
+    for (int k = 0; k < c; k++) {
+        o.push_back((uint8_t)(k + 1)); o.push_back(0x11); o.push_back(k ? 1 : 0);
+    }
+    auto dht = [&](int cls_id, const uint8_t* bits, const uint8_t* vals) {
+        int n = 0;
+        for (int i = 0; i < 16; i++) n += bits[i];
+        o.push_back(0xFF); o.push_back(0xC4); put16(o, 2 + 17 + n);
+        o.push_back((uint8_t)cls_id);
+        o.insert(o.end(), bits, bits + 16);
+        o.insert(o.end(), vals, vals + n);
+    };
+    dht(0x00, kDcLumBits, kDcLumVal);
+    dht(0x10, kAcLumBits, kAcLumVal);
+    if (c == 3) {
+        dht(0x01, kDcChrBits, kDcChrVal);
+        dht(0x11, kAcChrBits, kAcChrVal);
+    }
+    o.push_back(0xFF); o.push_back(0xDA); put16(o, 6 + 2 * c); o.push_back((uint8_t)c);
+    for (int k = 0; k < c; k++) { o.push_back((uint8_t)(k + 1)); o.push_back(k ? 0x11 : 0x00); }
+    o.push_back(0); o.push_back(63); o.push_back(0);
+    const Code dcl = make_codes(kDcLumBits, kDcLumVal), acl = make_codes(kAcLumBits, kAcLumVal);
+    const Code dcc = make_codes(kDcChrBits, kDcChrVal), acc = make_codes(kAcChrBits, kAcChrVal);
+    BitOut bo(o);
+    int pred[3] = {0, 0, 0};
+    double blk[3][64];
+    for (int by = 0; by < h; by += 8)
+        for (int bx = 0; bx < w; bx += 8) {
+            for (int y = 0; y < 8; y++)
+                for (int x = 0; x < 8; x++) {  // edge blocks repeat the last row / column
+                    const int sy = by + y < h ? by + y : h - 1, sx = bx + x < w ? bx + x : w - 1;
+                    const uint8_t* p = px + ((size_t)sy * w + sx) * c;
+                    if (c == 1) {
+                        blk[0][y * 8 + x] = p[0] - 128.0;
+                    } else {  // JFIF YCbCr, level shifted
+                        const double r = p[0], g = p[1], b = p[2];
+                        blk[0][y * 8 + x] = 0.299 * r + 0.587 * g + 0.114 * b - 128.0;
+                        blk[1][y * 8 + x] = -0.168735892 * r - 0.331264108 * g + 0.5 * b;
+                        blk[2][y * 8 + x] = 0.5 * r - 0.418687589 * g - 0.081312411 * b;
+                    }
+                }
+            encode_block(bo, blk[0], ql, pred[0], dcl, acl);
+            if (c == 3) {
+                encode_block(bo, blk[1], qc, pred[1], dcc, acc);
+                encode_block(bo, blk[2], qc, pred[2], dcc, acc);
+            }
+        }
+    bo.flush();
+    o.push_back(0xFF); o.push_back(0xD9);
+    return true;
+}
+
+bool save_jpeg(const std::string& fn, const uint8_t* px, int w, int h, int c, int quality,
+               std::string& err)
+{
+    std::vector<uint8_t> o;
+    if (!encode_jpeg(px, w, h, c, quality, o, err)) return false;
+    FILE* f = std::fopen(fn.c_str(), "wb");
+    if (!f) {
+        err = "cannot write " + fn;
+        return false;
+    }
+    const bool ok = std::fwrite(o.data(), 1, o.size(), f) == o.size();
+    std::fclose(f);
+    if (!ok) err = "short write to " + fn;
+    return ok;
 }
 
 }  // namespace pfio

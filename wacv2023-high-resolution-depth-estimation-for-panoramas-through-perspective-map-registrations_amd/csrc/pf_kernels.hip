@@ -610,6 +610,45 @@ __global__ void k_register_joint(const double* __restrict__ sums, const int* __r
     solve_store(S, degree, solver, coeffs, coeffs64, (long long)b * 4);
 }
 
+// Pixels covered by three or more tiles (pf_fuse_multicover, sharded fusion): the contribution
+// of tile p to pixel o for every listed (o, p) pair with p in [t0, t1), 0 for the others.
+__global__ void __launch_bounds__(kBlock) k_multicover_contrib(
+    const TileGeom* __restrict__ geom, const int2* __restrict__ pairs, int npairs, int t0, int t1,
+    const GridCol* __restrict__ cols, const GridRow* __restrict__ rows,
+    const float* __restrict__ tiles, const float* __restrict__ coeffs, LevelDims L,
+    float* __restrict__ contrib)
+{
+    const int i = blockIdx.x * kBlock + threadIdx.x;
+    if (i >= npairs) return;
+    const int o = pairs[i].x, p = pairs[i].y;
+    float v = 0.0f;
+    if (p >= t0 && p < t1) {
+        const int Y = o / L.w, X = o - Y * L.w;
+        const TileGeom& g = geom[p];
+        float4 abcd = make_float4(0, 0, 0, 0);
+        const bool xf = coeffs != nullptr;
+        if (xf) abcd = *reinterpret_cast<const float4*>(coeffs + (long long)p * 4);
+        v = target_one(g, tiles + g.off, cols, rows, X, Y, xf, abcd);
+    }
+    contrib[i] = v;
+}
+
+// The window sums of those pixels in the reference's single-thread order (tiles ascending, from
+// 0, one rounding per tile), overwriting the rank-summed values; pairs are sorted by pixel, then
+// tile.  One thread: a handful of pixels per level.
+__global__ void k_multicover_patch(const int2* __restrict__ pairs, int npairs,
+                                   const float* __restrict__ contrib, float* __restrict__ lsum)
+{
+    if (blockIdx.x != 0 || threadIdx.x != 0) return;
+    int i = 0;
+    while (i < npairs) {
+        const int o = pairs[i].x;
+        float acc = 0.0f;
+        for (; i < npairs && pairs[i].x == o; i++) acc += contrib[i];
+        lsum[o] = acc;
+    }
+}
+
 // Depth2DepthTransform on all tiles (channel 0), in place.
 __global__ void __launch_bounds__(kBlock) k_apply_cubic(const TileGeom* __restrict__ geom,
                                                         int ntiles, float* __restrict__ tiles,
@@ -718,6 +757,22 @@ void launch_targets_partial(hipStream_t s, const TileGeom* geom, const TileBox* 
     dim3 grid(nblocks((long long)L.w * (L.h1 - L.h0 + 1)));
     hipLaunchKernelGGL(k_targets_partial, grid, dim3(kBlock), 0, s, geom, box, t0, t1, cols,
                        rows, tiles, coeffs, L, lsum, cnt);
+}
+
+void launch_multicover(hipStream_t s, const TileGeom* geom, const int2* pairs, int npairs,
+                       int t0, int t1, const GridCol* cols, const GridRow* rows,
+                       const float* tiles, const float* coeffs, LevelDims L, float* contrib)
+{
+    if (npairs <= 0) return;
+    hipLaunchKernelGGL(k_multicover_contrib, dim3(nblocks(npairs)), dim3(kBlock), 0, s, geom, pairs,
+                       npairs, t0, t1, cols, rows, tiles, coeffs, L, contrib);
+}
+
+void launch_multicover_patch(hipStream_t s, const int2* pairs, int npairs, const float* contrib,
+                             float* lsum)
+{
+    if (npairs <= 0) return;
+    hipLaunchKernelGGL(k_multicover_patch, dim3(1), dim3(64), 0, s, pairs, npairs, contrib, lsum);
 }
 
 void launch_normalize(hipStream_t s, const float* lsum, const float* cnt, LevelDims L,

@@ -25,7 +25,8 @@ EXPORTS = [
     "pf_warp_rgb", "pf_level_info", "pf_fuse_partial", "pf_fuse_seed", "pf_fuse_finish_level",
     "pf_probe_taps", "pf_profile_enable", "pf_profile_read", "pf_error_metrics",
     "pf_depth_transform", "pf_register_joint", "pf_set_solver", "pf_fuse_normalize",
-    "pf_fuse_border", "pf_fuse_band_plan", "pf_fuse_band_pass",
+    "pf_fuse_border", "pf_fuse_band_plan", "pf_fuse_band_pass", "pf_fuse_multicover",
+    "pf_fuse_multicover_patch",
 ]
 SOLVERS = {"normal": 0, "lm": 1}  # PF_SOLVER_*; "lm" = the reference's Ceres LM (default)
 
@@ -87,6 +88,9 @@ def load():
                                    vp]
     L.pf_set_solver.argtypes = [vp, ip]
     L.pf_fuse_normalize.argtypes = [vp, vp, vp, ip, ip, fp, fp, ip, vp]
+    L.pf_fuse_multicover.argtypes = [vp, vp, vp, ip, ip, ip, ip, fp, fp, ip, vp,
+                                     C.POINTER(C.c_int)]
+    L.pf_fuse_multicover_patch.argtypes = [vp, ip, ip, fp, fp, ip, vp, vp]
     L.pf_fuse_border.argtypes = [vp, vp, ip, ip, fp, fp, ip, vp, vp, vp]
     L.pf_fuse_band_plan.argtypes = [vp, ip, ip, fp, fp, ip, ip, C.POINTER(C.c_int), ip]
     L.pf_fuse_band_pass.argtypes = [vp, vp, ip, ip, ip, vp, vp, ip, vp, vp, vp, ip, ip, fp, fp,
@@ -287,6 +291,24 @@ class Fuser:
         self._check(self.L.pf_fuse_finish_level(self.h, _ptr(lsum), _ptr(cnt), out_w,
                                                 out_w // 2, float(zr[0]), float(zr[1]), level,
                                                 _ptr(buf), _ptr(out)))
+
+    def multicover_count(self, out_w, zr, level):
+        n = C.c_int(0)
+        self._check(self.L.pf_fuse_multicover(self.h, None, None, 0, 0, out_w, out_w // 2,
+                                              float(zr[0]), float(zr[1]), level, None,
+                                              C.byref(n)))
+        return n.value
+
+    def multicover(self, tiles, coeffs, t0, t1, out_w, zr, level, contrib):
+        n = C.c_int(0)
+        self._check(self.L.pf_fuse_multicover(self.h, _ptr(tiles), _ptr(coeffs), t0, t1, out_w,
+                                              out_w // 2, float(zr[0]), float(zr[1]), level,
+                                              _ptr(contrib), C.byref(n)))
+
+    def multicover_patch(self, out_w, zr, level, contrib, lsum):
+        self._check(self.L.pf_fuse_multicover_patch(self.h, out_w, out_w // 2, float(zr[0]),
+                                                    float(zr[1]), level, _ptr(contrib),
+                                                    _ptr(lsum)))
 
     # ---- row-band sharding of a level's sweeps (pf_dist.fuse_row_sharded) ----
     def fuse_normalize(self, lsum, cnt, out_w, zr, level, lnorm):

@@ -5,11 +5,15 @@
 * Tile sharding of one huge panorama (config C5): per fusion level every rank scatters the
   Laplacian targets of its contiguous share of the tiles into full-level (sum L, n) grids, the
   grids are summed over ranks (RCCL reduce over xGMI; gloo in the CPU tests), and rank 0
-  normalises and runs the damped Jacobi sweeps (`fuse_tile_sharded`).  With every pixel covered
-  by at most two tiles (the reference's layouts) the reduced sums are exactly the single-GPU
-  sums: adding zeros is exact and a + b is commutative.  With three or more the reduce order
-  (RCCL's, not the reference's tile order) could round differently, so rank 0 checks the reduced
-  coverage and refuses such a layout (`CoverageError`) instead of returning different bits.
+  normalises and runs the damped Jacobi sweeps (`fuse_tile_sharded`).  The reference adds the
+  covering tiles' Laplacians to a pixel one at a time (Depth.cpp:1609-1617); a sum of per-rank
+  partials is that same value for pixels covered by at most two tiles (adding zeros is exact,
+  a + b commutes), not always for the few covered by three or more (sector corners on shared
+  band rows: 7 pixels per level in the C5 layout).  Those pixels are recomputed exactly: every
+  rank contributes its tiles' terms of their (pixel, tile) pairs, the terms are summed over
+  ranks (one non-zero per pair: exact), and the pixels are re-added in tile order
+  (`_exact_multicover`, pf_fuse_multicover).  The result is bit-identical to one GPU's.
+* Row-band sharding of the sweeps as well (`fuse_row_sharded`, below).
 
 The reference has no distributed code; this replaces its single-process OpenMP tile loop
 (Depth.cpp:1492-1624).
@@ -52,6 +56,19 @@ class HipTileShardBackend:
                              lsum, cnt)
         return lsum, cnt
 
+    def multicover_count(self, level):
+        return self.fz.multicover_count(self.out_w, self.zr, level)
+
+    def multicover(self, level, t0, t1):
+        import torch
+        c = torch.zeros(max(1, self.multicover_count(level)), dtype=torch.float32,
+                        device=self.tiles.device)
+        self.fz.multicover(self.tiles, self.coeffs, t0, t1, self.out_w, self.zr, level, c)
+        return c
+
+    def multicover_patch(self, level, contrib, lsum):
+        self.fz.multicover_patch(self.out_w, self.zr, level, contrib, lsum)
+
     def seed(self, level, prev):
         buf = self._plane(level)
         self.fz.fuse_seed(self.emap if level == 0 else None, prev, self.out_w, self.zr, level,
@@ -64,37 +81,31 @@ class HipTileShardBackend:
         return buf
 
 
-class CoverageError(ValueError):
-    """A pixel is covered by more than two tiles: the tile-sharded sums are no longer exact."""
-
-
-MAX_SHARDED_COVER = 2
-
-
-def fuse_tile_sharded(backend, nlevels, ntiles, rank, world, dist=None, group=None):
+def fuse_tile_sharded(backend, nlevels, ntiles, rank, world, comm=None):
     """Tile-sharded fusion of one panorama.
 
     backend: object with
       partial(level, t0, t1) -> (lsum, cnt) tensors of the level (zeros outside the band),
+      multicover_count(level) / multicover(level, t0, t1) / multicover_patch(level, contrib,
+        lsum) -> the exact fix-up of pixels covered by three or more tiles,
       seed(level, prev) -> buf tensor (level 0 from the baseline, else upsampled prev),
       finish(level, lsum, cnt, buf, last) -> buf after the sweeps (u16 written when last).
+    comm: TorchComm (reduce to rank 0) or a stand-in; None for world == 1.
     Returns rank 0's final level buffer (None on other ranks).
     """
     t0, t1 = shard_range(ntiles, rank, world)
     prev = None
     for level in range(nlevels):
         lsum, cnt = backend.partial(level, t0, t1)
-        if dist is not None and world > 1:
-            dist.reduce(lsum, dst=0, op=dist.ReduceOp.SUM, group=group)
-            dist.reduce(cnt, dst=0, op=dist.ReduceOp.SUM, group=group)
+        if world > 1:
+            comm.reduce_sum(lsum, 0)
+            comm.reduce_sum(cnt, 0)
+            if backend.multicover_count(level):
+                contrib = backend.multicover(level, t0, t1)
+                comm.all_reduce_sum(contrib)
+                if rank == 0:
+                    backend.multicover_patch(level, contrib, lsum)
         if rank == 0:
-            if world > 1:
-                cover = int(cnt.max().item())
-                if cover > MAX_SHARDED_COVER:
-                    raise CoverageError(
-                        f"level {level}: a pixel is covered by {cover} tiles; the tile-sharded "
-                        f"reduce is exact only up to {MAX_SHARDED_COVER} (run this layout on one "
-                        f"GPU)")
             buf = backend.seed(level, prev)
             prev = backend.finish(level, lsum, cnt, buf, level == nlevels - 1)
     return prev if rank == 0 else None
@@ -119,6 +130,9 @@ class TorchComm:
 
     def all_reduce_sum(self, t):
         self.dist.all_reduce(t, op=self.dist.ReduceOp.SUM, group=self.group)
+
+    def reduce_sum(self, t, dst):
+        self.dist.reduce(t, dst=dst, op=self.dist.ReduceOp.SUM, group=self.group)
 
     def exchange(self, sends, recvs):
         """sends: [(peer, tensor)], recvs: [(peer, tensor)]; point-to-point, all at once."""
@@ -146,6 +160,7 @@ def fuse_row_sharded(backend, nlevels, ntiles, rank, world, comm=None):
 
     backend (one rank's device):
       partial(level, t0, t1) -> (lsum, cnt)   the targets of tiles [t0, t1), full-level grids
+      multicover_count / multicover / multicover_patch   as fuse_tile_sharded
       dims(level) -> (w, h, h0, h1)
       plane(level) -> a new full-level fp32 buffer (flat)
       normalize(level, lsum, cnt) -> lnorm
@@ -165,11 +180,10 @@ def fuse_row_sharded(backend, nlevels, ntiles, rank, world, comm=None):
         if world > 1:
             comm.all_reduce_sum(lsum)
             comm.all_reduce_sum(cnt)
-            cover = int(cnt.max().item())
-            if cover > MAX_SHARDED_COVER:
-                raise CoverageError(
-                    f"level {level}: a pixel is covered by {cover} tiles; the sharded reduce is "
-                    f"exact only up to {MAX_SHARDED_COVER} (run this layout on one GPU)")
+            if backend.multicover_count(level):  # exact sums where 3+ tiles meet
+                contrib = backend.multicover(level, t0, t1)
+                comm.all_reduce_sum(contrib)
+                backend.multicover_patch(level, contrib, lsum)
         lnorm = backend.normalize(level, lsum, cnt)
         w, h, h0, h1 = backend.dims(level)
         r0, r1 = band_rows(h0, h1, rank, world)
@@ -234,6 +248,10 @@ class HipRowShardBackend:
                              lsum, cnt)
         return lsum, cnt
 
+    multicover_count = HipTileShardBackend.multicover_count
+    multicover = HipTileShardBackend.multicover
+    multicover_patch = HipTileShardBackend.multicover_patch
+
     def normalize(self, level, lsum, cnt):
         lnorm = self.plane(level)
         self.fz.fuse_normalize(lsum, cnt, self.out_w, self.zr, level, lnorm)
@@ -244,7 +262,7 @@ class HipRowShardBackend:
 
     def border(self, level, prev, a, b):
         if level == self.nlevels - 1:
-            self.fz.fuse_border(prev, self.out_w, self.zr, level, out=self.out)
+            self.fz.fuse_border(prev, self.out_w, self.zr, level, a=a, b=b, out=self.out)
         else:
             self.fz.fuse_border(prev, self.out_w, self.zr, level, a=a, b=b)
 
