@@ -42,6 +42,9 @@
 #ifndef PF_JPK_GROUP
 #define PF_JPK_GROUP 3  // levels per stage-wise group of the packed form (VGPR bound: 3 waves/SIMD)
 #endif
+#ifndef PF_JGATE
+#define PF_JGATE 0  // skip the sweep levels a step does not need (JLag::sweep_packed)
+#endif
 #ifndef PF_JLAG_PF
 #define PF_JLAG_PF 2  // steps of lead for the input and L row loads (1 or 2)
 #endif
@@ -112,6 +115,23 @@ __device__ __forceinline__ f2 pk_add_clamp01(f2 a, f2 b)
     return r;
 }
 
+// a plain v_add_f32: keeps the backend from widening a lone add of two vector halves into a
+// packed op plus a move
+__device__ __forceinline__ float add_scalar(float a, float b)
+{
+    float r;
+    asm("v_add_f32 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+    return r;
+}
+// fma(a, b, c) as a plain v_fma_f32 (same reason: two scalar FMAs on the halves of a pair would
+// otherwise become a packed FMA after a pair assembly)
+__device__ __forceinline__ float fma_scalar(float a, float b, float c)
+{
+    float r;
+    asm("v_fma_f32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+    return r;
+}
+
 template <int C, int T, int SRC, bool OUT16, bool FAST>
 struct JLag {
     static_assert(C % 2 == 0, "column pairs: vector stores and the wrap logic assume even C");
@@ -126,8 +146,10 @@ struct JLag {
     float* lring;     // this wave's ring: R rows of 64*C floats
     int lane_c;       // lane * C (LDS column offset)
     float hcol[C];  // FAST: H of the lane's columns: 0.5 (covered column) or 0
+    float vq;       // -1/4 in a VGPR (the folded-DPP FMA takes its second operand from a VGPR)
     const JacobiPass* P;
     int w, xs0, vlo, vhi, r0, r1, h0, h1;
+    int kr0, kr1;  // r0 - T and r1 + T: the gating windows of sweep_packed
     int colbase;   // virtual column of lane 0 (wave-uniform)
     int lo;        // lane * C
     int rlo, rhi;  // rows loads are clamped to: the band [h0, h1].  A band pixel never reads a
@@ -348,8 +370,8 @@ struct JLag {
                 hm0 = hm0 * hr;
                 hm1 = hm1 * hr;
             }
-            lo[g] = __builtin_elementwise_fma(Lv[t - 1].v.lo - lo[g], hm0, c.lo);
-            hi[g] = __builtin_elementwise_fma(Lv[t - 1].v.hi - hi[g], hm1, c.hi);
+            lo[g] = __builtin_elementwise_fma(Lv[g].v.lo - lo[g], hm0, c.lo);
+            hi[g] = __builtin_elementwise_fma(Lv[g].v.hi - hi[g], hm1, c.hi);
         }
 #pragma unroll
         for (int g = 0; g < G; g++) {
@@ -361,8 +383,13 @@ struct JLag {
         }
     }
 
-    // FAST form (C == 2): the same update on the lane's column pair with packed ops, stage-wise
-    // over groups of PF_JPK_GROUP levels (bounds the live temporaries, i.e. the VGPR count).
+    // FAST form (C == 2): the same update on the lane's column pair, stage-wise over groups of
+    // PF_JPK_GROUP levels (bounds the live temporaries, i.e. the VGPR count).  The terms that
+    // cross lanes are scalar ops: W + N of column 0 is one v_add_f32_dpp (the DPP move folded
+    // into the add) and the E terms are two scalar FMAs, the rest packed.  Measured issue costs
+    // on MI355X (tools/ubench/dpp_rate.hip, >= 2 waves/SIMD): v_pk_* 4.7 cycles, v_add/v_fma 2.8,
+    // any DPP op 4.4 -- so per level and column pair 7 packed + 1 folded DPP + 1 DPP move +
+    // 3 scalar (~50 cycles) against 9 packed + 2 DPP moves + 2 pair assemblies (~57).
     template <int PH, int T0, int T1, bool ROWS>
     __device__ __forceinline__ void sweep_packed_group(const Row<C>* Lv, Row<C>* nw, int k) const
     {
@@ -370,19 +397,14 @@ struct JLag {
         const f2 q = {-0.25f, -0.25f};
         const f2 reg = {(float)1e-4, (float)1e-4};
         const f2 reg_ = {1 - (float)1e-4, 1 - (float)1e-4};
-        float Wl[G], Er[G];
-#pragma unroll
-        for (int g = 0; g < G; g++) {
-            constexpr int t0 = T0 + 1;
-            Wl[g] = dpp_from_left(H[t0 + g - 1][slot(PH, 2 * (t0 + g))].v[1]);
-            Er[g] = dpp_from_right(H[t0 + g - 1][slot(PH, 2 * (t0 + g))].v[0]);
-        }
         f2 cur[G];
         // Lcur = (((W*q + N*q) + b) + S*q) + E*q, q = -1/4, as in sweep_general
 #pragma unroll
         for (int g = 0; g < G; g++) {
             const int t = T0 + 1 + g;
-            cur[g] = f2{Wl[g], H[t - 1][slot(PH, 2 * t)].v[0]} + H[t - 1][slot(PH, 2 * t + 1)].v;
+            const f2 c = H[t - 1][slot(PH, 2 * t)].v, n = H[t - 1][slot(PH, 2 * t + 1)].v;
+            cur[g].x = dpp_from_left(c.y) + n.x;  // folds into v_add_f32_dpp
+            cur[g].y = add_scalar(c.x, n.y);
         }
 #pragma unroll
         for (int g = 0; g < G; g++) {
@@ -397,7 +419,9 @@ struct JLag {
 #pragma unroll
         for (int g = 0; g < G; g++) {
             const int t = T0 + 1 + g;
-            cur[g] = __builtin_elementwise_fma(f2{H[t - 1][slot(PH, 2 * t)].v[1], Er[g]}, q, cur[g]);
+            const f2 c = H[t - 1][slot(PH, 2 * t)].v;
+            cur[g].x = fma_scalar(c.y, vq, cur[g].x);
+            cur[g].y = __builtin_fmaf(dpp_from_right(c.x), vq, cur[g].y);
         }
 #pragma unroll
         for (int g = 0; g < G; g++) {
@@ -410,7 +434,7 @@ struct JLag {
                 const float hr = (row == h0 || row == h1) ? 0.0f : 1.0f;
                 hh = hh * hr;
             }
-            cur[g] = __builtin_elementwise_fma(Lv[t - 1].v - cur[g], hh, H[t - 1][slot(PH, 2 * t)].v);
+            cur[g] = __builtin_elementwise_fma(Lv[g].v - cur[g], hh, H[t - 1][slot(PH, 2 * t)].v);
         }
 #pragma unroll
         for (int g = 0; g < G; g++) {
@@ -418,13 +442,30 @@ struct JLag {
             nw[t - 1].v = pk_add_clamp01(cur[g] * reg_, H[t - 1][slot(PH, 2 * t)].v * reg);
         }
     }
-    template <int PH, int T0, bool ROWS>
-    __device__ __forceinline__ void sweep_packed(const Row<C>* Lv, Row<C>* nw, int k) const
+    // Fill/drain gating.  Level t is only needed for rows [r0 - (T-t), r1 + (T-t)) of the chunk,
+    // i.e. at steps k in [r0 - T + 3t, r1 + T + t); outside that window its row is never read by
+    // a needed update (stencil closure), so a group of levels whose windows all miss step k is
+    // skipped with one wave-uniform branch -- its ring slots then hold stale rows, read only by
+    // unneeded updates.  At the default depths this drops 10-30% of the issued updates (the
+    // lagged start fills T levels over 3T steps, the drain empties them over T).
+    template <int PH, int GB, int T0, bool ROWS>
+    __device__ __forceinline__ void sweep_packed(Row<C>* nw, int k) const
     {
         constexpr int T1 = T0 + PF_JPK_GROUP < T ? T0 + PF_JPK_GROUP : T;
-        if constexpr (C == 4) sweep_packed_group4<PH, T0, T1, ROWS>(Lv, nw, k);
-        else sweep_packed_group<PH, T0, T1, ROWS>(Lv, nw, k);
-        if constexpr (T1 < T) sweep_packed<PH, T1, ROWS>(Lv, nw, k);
+        // the groups run from the deepest level down: level t+1 reads the oldest row of level
+        // t's ring before level t overwrites it, so the new row can take that row's registers
+        // (all reads of a step are rows of earlier steps, so the order is free)
+        if constexpr (T1 < T) sweep_packed<PH, GB, T1, ROWS>(nw, k);
+#if PF_JGATE
+        if (k - kr0 >= 3 * (T0 + 1) && k - kr1 < T1)
+#endif
+        {
+            Row<C> Lv[T1 - T0];
+#pragma unroll
+            for (int t = T0 + 1; t <= T1; t++) Lv[t - 1 - T0] = lds_get(lslot_t<GB, PH>(t));
+            if constexpr (C == 4) sweep_packed_group4<PH, T0, T1, ROWS>(Lv, nw, k);
+            else sweep_packed_group<PH, T0, T1, ROWS>(Lv, nw, k);
+        }
     }
 
     // Step k = (group base) + PH; GB = group base mod R.
@@ -435,15 +476,7 @@ struct JLag {
         H[0][slot(PH, 1)] = In[(PH + NB - 1) % NB];
         // L row k (landed in Lin last step) goes to its ring slot; fetch L row k+PF.  The slot
         // is reused by row k+R > k, after every level has read row k (last read at k + 2T).
-        Row<C> Lv[T];
-#if PF_JDBG_NOLDS  // profiling only (wrong results): no LDS ring
-#pragma unroll
-        for (int t = 1; t <= T; t++) Lv[t - 1] = Lin[(PH + t) % NB];
-#else
         lds_put(lslot<GB, PH>(), Lin[PH % NB]);
-#pragma unroll
-        for (int t = 1; t <= T; t++) Lv[t - 1] = lds_get(lslot_t<GB, PH>(t));
-#endif
 #if PF_JDBG_NOGLOBAL  // profiling only (wrong results): no global loads in the loop
         Lin[(PH + PF) % NB] = H[T - 1][slot(PH, 1)];
         In[(PH + PF - 1) % NB] = H[T - 2][slot(PH, 2)];
@@ -453,8 +486,14 @@ struct JLag {
         In[(PH + PF - 1) % NB] = load_input(k + PF - 1);
 #endif
         Row<C> nw[T];
-        if constexpr (FAST) sweep_packed<PH, 0, ROWS>(Lv, nw, k);
-        else sweep_general<PH>(Lv, nw);
+        if constexpr (FAST) {
+            sweep_packed<PH, GB, 0, ROWS>(nw, k);
+        } else {
+            Row<C> Lv[T];
+#pragma unroll
+            for (int t = 1; t <= T; t++) Lv[t - 1] = lds_get(lslot_t<GB, PH>(t));
+            sweep_general<PH>(Lv, nw);
+        }
 #pragma unroll
         for (int t = 1; t < T; t++) H[t][slot(PH, 2 * t)] = nw[t - 1];
         const int j = k - 2 * T;  // final-level row finished this step
@@ -535,6 +574,8 @@ __global__ void __launch_bounds__(256, PF_JLAG_WAVES) k_jlag(JacobiPass P)
     S.h1 = P.h1;
     S.colbase = strip * P.V - P.Tp;
     S.lo = lane * C;
+    S.vq = -0.25f;
+    asm volatile("" : "+v"(S.vq));
     S.rlo = P.h0;
     S.rhi = P.h1;
     S.xs0 = strip * P.V - P.Tp + lane * C;
@@ -542,6 +583,8 @@ __global__ void __launch_bounds__(256, PF_JLAG_WAVES) k_jlag(JacobiPass P)
     S.vhi = min(S.vlo + P.V, P.w);
     S.r0 = P.row_lo + chunk * P.rows_per_chunk;
     S.r1 = min(S.r0 + P.rows_per_chunk, P.row_hi);
+    S.kr0 = S.r0 - T;
+    S.kr1 = S.r1 + T;
     S.src = P.src + b * P.sstride;
     S.prev = P.prev + b * P.pstride;
     S.emap = P.emap + b * P.estride;
@@ -622,6 +665,7 @@ struct JPipe {
     float* xout;      // stage < S-1: this stage's exchange slots
     int lane_c;
     float hcol[C];
+    float vq;  // -1/4 in a VGPR, as JLag::vq
     const JacobiPass* P;
     int w, xs0, vlo, vhi, r0, r1, h0, h1, colbase, lo, rlo, rhi;
     const float *src, *prev, *emap, *lnorm;
@@ -682,18 +726,13 @@ struct JPipe {
         const f2 q = {-0.25f, -0.25f};
         const f2 reg = {(float)1e-4, (float)1e-4};
         const f2 reg_ = {1 - (float)1e-4, 1 - (float)1e-4};
-        float Wl[NGR], Er[NGR];
-#pragma unroll
-        for (int g = 0; g < NGR; g++) {
-            const int t = T0 + 1 + g, l = t - TB;  // reads ring H[l] = level t-1
-            Wl[g] = dpp_from_left(H[l][md(PH - 2 * t, 3)].v[1]);
-            Er[g] = dpp_from_right(H[l][md(PH - 2 * t, 3)].v[0]);
-        }
         f2 cur[NGR];
 #pragma unroll
         for (int g = 0; g < NGR; g++) {
-            const int t = T0 + 1 + g, l = t - TB;
-            cur[g] = f2{Wl[g], H[l][md(PH - 2 * t, 3)].v[0]} + H[l][md(PH - 2 * t - 1, 3)].v;
+            const int t = T0 + 1 + g, l = t - TB;  // reads ring H[l] = level t-1
+            const f2 c = H[l][md(PH - 2 * t, 3)].v, n = H[l][md(PH - 2 * t - 1, 3)].v;
+            cur[g].x = dpp_from_left(c.y) + n.x;
+            cur[g].y = add_scalar(c.x, n.y);
         }
 #pragma unroll
         for (int g = 0; g < NGR; g++) {
@@ -708,7 +747,9 @@ struct JPipe {
 #pragma unroll
         for (int g = 0; g < NGR; g++) {
             const int t = T0 + 1 + g, l = t - TB;
-            cur[g] = __builtin_elementwise_fma(f2{H[l][md(PH - 2 * t, 3)].v[1], Er[g]}, q, cur[g]);
+            const f2 c = H[l][md(PH - 2 * t, 3)].v;
+            cur[g].x = fma_scalar(c.y, vq, cur[g].x);
+            cur[g].y = __builtin_fmaf(dpp_from_right(c.x), vq, cur[g].y);
         }
 #pragma unroll
         for (int g = 0; g < NGR; g++) {
@@ -823,6 +864,8 @@ __device__ __forceinline__ void jpipe_stage(const JacobiPass& P, int lane, int b
     St.colbase = strip * P.V - P.Tp;
     St.lo = lane * C;
     St.lane_c = lane * C;
+    St.vq = -0.25f;
+    asm volatile("" : "+v"(St.vq));
     St.rlo = P.h0;  // as JLag::rlo
     St.rhi = P.h1;
     St.xs0 = strip * P.V - P.Tp + lane * C;
@@ -888,6 +931,7 @@ __global__ void __launch_bounds__(64 * S) k_jpipe(JacobiPass P)
     if constexpr (S > 3) { if (wave == 3) jpipe_stage<TS, S, (S > 3 ? 3 : 0), SRC, OUT16>(P, lane, b, strip, chunk, lring, xchg); }
 }
 
+#if !defined(PF_JPART) || PF_JPART == 0
 // Out-of-band rows of a level: 0 (level 0, Depth.cpp:1449-1452) or the nearest upsample of the
 // previous level (Depth.cpp:1467-1485); stored to both ping-pong buffers, or quantised into the
 // u16 output on the last level (where the ping-pong buffers get only the rows h0-1 and h1+1).
@@ -923,7 +967,21 @@ __global__ void __launch_bounds__(256) k_border(const float* __restrict__ prev, 
     }
 }
 
+#endif
+
 // ---------------------------------------------------------------------------------------------
+// The lagged passes of one sweep depth T are built in their own translation unit (the Makefile
+// compiles this file once per T with -DPF_JPART=T, and once with PF_JPART=0 for the rest), so the
+// 70-odd k_jlag instantiations compile in parallel.
+#define PF_JCAT2(a, b) a##b
+#define PF_JCAT(a, b) PF_JCAT2(a, b)
+#define PF_JDECL(T)                                                                            \
+    void PF_JCAT(jlag_launch_t, T)(hipStream_t s, const JacobiPass& P, int C, int batch,      \
+                                   bool fast);                                               \
+    int PF_JCAT(jlag_waves_t, T)(int C, bool fast);
+PF_JDECL(1) PF_JDECL(2) PF_JDECL(4) PF_JDECL(5) PF_JDECL(8) PF_JDECL(10)
+
+#if defined(PF_JPART) && PF_JPART > 0
 template <int C, int T, int SRC, bool OUT16, bool FAST>
 static void launch_pass_cts(hipStream_t s, const JacobiPass& P, int batch)
 {
@@ -946,21 +1004,6 @@ static void launch_pass_ct(hipStream_t s, const JacobiPass& P, int batch)
     }
 }
 
-template <int C, bool FAST>
-static void launch_pass_c(hipStream_t s, const JacobiPass& P, int T, int batch)
-{
-    switch (T) {
-        case 1: launch_pass_ct<C, 1, FAST>(s, P, batch); break;
-        case 2: launch_pass_ct<C, 2, FAST>(s, P, batch); break;
-        case 4: launch_pass_ct<C, 4, FAST>(s, P, batch); break;
-        case 5: launch_pass_ct<C, 5, FAST>(s, P, batch); break;
-        case 8: launch_pass_ct<C, 8, FAST>(s, P, batch); break;
-        default: launch_pass_ct<C, 10, FAST>(s, P, batch); break;
-    }
-}
-
-bool jstream_supported_T(int T) { return T == 1 || T == 2 || T == 4 || T == 5 || T == 8 || T == 10; }
-
 template <int C, int T, bool FAST>
 static int waves_per_cu_t()
 {
@@ -971,16 +1014,51 @@ static int waves_per_cu_t()
     return nb * 4;
 }
 
-template <int C, bool FAST>
-static int waves_per_cu_c(int T)
+// C == 4: packed form in PF_JACOBI_C4P builds, general form in PF_JACOBI_C4 builds (both off by
+// default: measured slower than C == 2 on MI355X, see DESIGN.md; they double the build time).
+void PF_JCAT(jlag_launch_t, PF_JPART)(hipStream_t s, const JacobiPass& P, int C, int batch, bool fast)
+{
+    constexpr int T = PF_JPART;
+    if (C == 4) {
+#if PF_JACOBI_C4
+        if (!fast) { launch_pass_ct<4, T, false>(s, P, batch); return; }
+#endif
+#if PF_JACOBI_C4P
+        if (fast) { launch_pass_ct<4, T, true>(s, P, batch); return; }
+#endif
+        return;  // unreachable: the host checks jstream_supported_C first
+    }
+    if (fast) launch_pass_ct<2, T, true>(s, P, batch);
+    else launch_pass_ct<2, T, false>(s, P, batch);
+}
+
+int PF_JCAT(jlag_waves_t, PF_JPART)(int C, bool fast)
+{
+    constexpr int T = PF_JPART;
+    if (C == 4) {
+#if PF_JACOBI_C4
+        if (!fast) return waves_per_cu_t<4, T, false>();
+#endif
+#if PF_JACOBI_C4P
+        if (fast) return waves_per_cu_t<4, T, true>();
+#endif
+        return 4;
+    }
+    return fast ? waves_per_cu_t<2, T, true>() : waves_per_cu_t<2, T, false>();
+}
+#else  // PF_JPART == 0: dispatch, the pipelined engine, the border kernel
+
+bool jstream_supported_T(int T) { return T == 1 || T == 2 || T == 4 || T == 5 || T == 8 || T == 10; }
+
+static int waves_per_cu_c(int C, int T, bool fast)
 {
     switch (T) {
-        case 1: return waves_per_cu_t<C, 1, FAST>();
-        case 2: return waves_per_cu_t<C, 2, FAST>();
-        case 4: return waves_per_cu_t<C, 4, FAST>();
-        case 5: return waves_per_cu_t<C, 5, FAST>();
-        case 8: return waves_per_cu_t<C, 8, FAST>();
-        default: return waves_per_cu_t<C, 10, FAST>();
+        case 1: return jlag_waves_t1(C, fast);
+        case 2: return jlag_waves_t2(C, fast);
+        case 4: return jlag_waves_t4(C, fast);
+        case 5: return jlag_waves_t5(C, fast);
+        case 8: return jlag_waves_t8(C, fast);
+        default: return jlag_waves_t10(C, fast);
     }
 }
 
@@ -988,26 +1066,12 @@ static int waves_per_cu_c(int T)
 int jstream_waves_per_cu(int C, int T, bool fast)
 {
     static int cache[2][2][11] = {{{0}}};
-    if (T < 1 || T > 10) return 4;
+    if (T < 1 || T > 10 || !jstream_supported_T(T)) return 4;
     int& c = cache[C == 4 ? 1 : 0][fast ? 1 : 0][T];
-    if (!c) {
-        if (C == 4) {
-#if PF_JACOBI_C4
-            if (!fast) c = waves_per_cu_c<4, false>(T);
-#endif
-#if PF_JACOBI_C4P
-            if (fast) c = waves_per_cu_c<4, true>(T);
-#endif
-            if (!c) c = 4;
-        } else {
-            c = fast ? waves_per_cu_c<2, true>(T) : waves_per_cu_c<2, false>(T);
-        }
-    }
+    if (!c) c = waves_per_cu_c(C == 4 ? 4 : 2, T, fast);
     return c;
 }
 
-// C == 4: packed form in PF_JACOBI_C4P builds, general form in PF_JACOBI_C4 builds (both off by
-// default: measured slower than C == 2 on MI355X, see DESIGN.md; they double the build time).
 bool jstream_supported_C(int C, bool fast)
 {
     if (C == 2) return true;
@@ -1017,17 +1081,14 @@ bool jstream_supported_C(int C, bool fast)
 
 void launch_jstream(hipStream_t s, const JacobiPass& P, int C, int T, int batch, bool fast)
 {
-    if (C == 4) {
-#if PF_JACOBI_C4
-        if (!fast) { launch_pass_c<4, false>(s, P, T, batch); return; }
-#endif
-#if PF_JACOBI_C4P
-        if (fast) { launch_pass_c<4, true>(s, P, T, batch); return; }
-#endif
-        return;  // unreachable: the host checks jstream_supported_C first
+    switch (T) {
+        case 1: jlag_launch_t1(s, P, C, batch, fast); break;
+        case 2: jlag_launch_t2(s, P, C, batch, fast); break;
+        case 4: jlag_launch_t4(s, P, C, batch, fast); break;
+        case 5: jlag_launch_t5(s, P, C, batch, fast); break;
+        case 8: jlag_launch_t8(s, P, C, batch, fast); break;
+        default: jlag_launch_t10(s, P, C, batch, fast); break;
     }
-    if (fast) launch_pass_c<2, true>(s, P, T, batch);
-    else launch_pass_c<2, false>(s, P, T, batch);
 }
 
 // Pipelined passes (k_jpipe): T = S * TS.
@@ -1083,5 +1144,7 @@ void launch_border(hipStream_t s, const float* prev, long long pstride, LevelDim
     hipLaunchKernelGGL(k_border, grid, dim3(256), 0, s, prev, pstride, L, a, b, stride, out,
                        ostride);
 }
+
+#endif  // PF_JPART
 
 }  // namespace pf
