@@ -40,6 +40,10 @@ def parse():
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--batch", type=int, default=64, help="panoramas per GPU per step")
+    ap.add_argument("--c5-shard", choices=("rows", "tiles"), default="rows",
+                    help="c5 mode: rows = tiles AND sweep row bands sharded over the ranks "
+                         "(pf_dist.fuse_row_sharded, halo exchange per pass); tiles = tiles "
+                         "sharded, every sweep on rank 0 (pf_dist.fuse_tile_sharded)")
     ap.add_argument("--mode", choices=("batch", "c5"), default="batch",
                     help="batch: configs C3/C4 (the headline metric); c5: one 8192x4096 "
                          "panorama, tiles sharded over the ranks")
@@ -129,7 +133,9 @@ def run_c5(args, rank, world, local, dev):
     """BASELINE config C5: one 8192x4096 panorama, 80 tiles of 1024^2 sharded over the ranks.
     Each rank warps and registers its own tiles (a sub-layout context writing into its slice of
     the full tile block), scatters their targets per level (pf_fuse_partial); the (sum L, n) grids
-    are reduced to rank 0 over RCCL, which normalises and sweeps (pf_dist.fuse_tile_sharded).
+    are all-reduced over RCCL and every rank sweeps its row band with halo exchange per pass
+    (--c5-shard rows, pf_dist.fuse_row_sharded), or rank 0 sweeps the whole level (--c5-shard
+    tiles, pf_dist.fuse_tile_sharded).
     One step = one panorama end to end; value = panoramas/s of the whole job."""
     import torch
     import torch.distributed as dist
@@ -167,9 +173,13 @@ def run_c5(args, rank, world, local, dev):
             mine = tiles[:, off0:off1]
             fs.warp_depth(gt, mine, resp)
             fs.register(emap, mine, zr, degree=3, apply=False, coeffs=coeffs[t0:t1][None])
-        be = pf_dist.HipTileShardBackend(fz, emap, tiles, coeffs, out_w, zr, out)
-        pf_dist.fuse_tile_sharded(be, nlevels, lay.ntiles, rank, world,
-                                  pf_dist.TorchComm(dist) if world > 1 else None)
+        comm = pf_dist.TorchComm(dist) if world > 1 else None
+        if args.c5_shard == "rows":
+            be = pf_dist.HipRowShardBackend(fz, emap, tiles, coeffs, out_w, zr, out.view(-1))
+            pf_dist.fuse_row_sharded(be, nlevels, lay.ntiles, rank, world, comm)
+        else:
+            be = pf_dist.HipTileShardBackend(fz, emap, tiles, coeffs, out_w, zr, out)
+            pf_dist.fuse_tile_sharded(be, nlevels, lay.ntiles, rank, world, comm)
 
     for _ in range(args.warmup):
         step()
@@ -199,8 +209,10 @@ def run_c5(args, rank, world, local, dev):
             "data": "synthetic (box-room scene, synthetic depth-net response)",
             "config": {"workload": "C5: one 8192x4096 panorama, 80 tiles of 1024x1024 (10x8), "
                                    "2048x1024 baseline; tiles sharded over ranks, per-level "
-                                   "(sum L, n) reduce to rank 0 (RCCL), Jacobi on rank 0",
-                       "parallelism": f"tile-sharded x{world}"},
+                                   + ("(sum L, n) all-reduce (RCCL), row-band Jacobi per rank "
+                                      "with halo exchange per pass" if args.c5_shard == "rows"
+                                      else "(sum L, n) reduce to rank 0 (RCCL), Jacobi on rank 0"),
+                       "parallelism": f"{'row-band' if args.c5_shard == 'rows' else 'tile'}-sharded x{world}"},
             "nonzero_px": nz}), flush=True)
     if world > 1:
         dist.barrier()

@@ -43,6 +43,9 @@ struct LevelCache {
     // h0+1..h1-1 and in a column of a fixed set that excludes column 0.  Enables the packed
     // Jacobi form (pf_jacobi.hip), with hcol[l][X] = 0.5 on covered columns, 0 elsewhere.
     bool full[4] = {false, false, false, false};
+    // tap-grid points of each level (one tile texel gathered per point): the targets stage's
+    // algorithmic read count
+    long long taps[4] = {0, 0, 0, 0};
 };
 
 }  // namespace
@@ -646,6 +649,7 @@ static int prepare_levels(pf_ctx* c, int out_w, int out_h, float zr0, float zr1)
         }
         if ((rc = upload(c, lc.tapbox[l], tbs))) return rc;
         if ((rc = ensure(c, lc.tapmap[l], sizeof(int32_t) * (moff + 1)))) return rc;
+        lc.taps[l] = moff;
         launch_tapmap(c->stream, (const TileGeom*)c->geom.p, (const TapBox*)lc.tapbox[l].p,
                       c->ntiles, maxpts, (const GridCol*)lc.cols[l].p,
                       (const GridRow*)lc.rows[l].p, (int32_t*)lc.tapmap[l].p);
@@ -997,7 +1001,9 @@ static int fuse_range(pf_ctx* c, const float* emap, int ew, int eh, int ec, cons
         if (side && l > 0) {
             HIPCHK(c, hipStreamWaitEvent(c->stream, c->ev_tgt[l], 0));
         } else {
-            StageTimer t(c, PF_STAGE_TARGETS, B * (4.0 * band + 4.0 * (double)c->tile_elems), 1);
+            // algorithmic bytes: one 4-B tile texel per tap-grid point (k_targets_patch gathers
+            // each once; coarse levels touch a fraction of the tiles) + the 4-B L plane write
+            StageTimer t(c, PF_STAGE_TARGETS, B * (4.0 * band + 4.0 * (double)lc.taps[l]), 1);
             targets(l, c->stream);
         }
         float* res = nullptr;
