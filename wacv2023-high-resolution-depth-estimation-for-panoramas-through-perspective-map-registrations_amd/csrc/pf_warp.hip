@@ -41,6 +41,16 @@ static constexpr int kSlots = kCap / kWB;               // staging loads per thr
 #define PF_WARP_BATCH 16
 #endif
 static constexpr int kNB = PF_WARP_BATCH;               // panoramas per block
+// Wider memory operations, measured on MI355X at C3 (tools/warp_probe.py, round 2) and not kept:
+// 16-B staging loads of quad-aligned boxes 0.596 ms, a thread's pixels in one row with 16-B
+// stores 0.600 ms, both 0.637 ms, against 0.586 ms for 4-B loads and stores -- the kernel is not
+// bound by its memory instruction count.
+#ifndef PF_WARP_V4
+#define PF_WARP_V4 0     // quad-aligned footprint boxes staged with 16-B loads (pw % 4 == 0)
+#endif
+#ifndef PF_WARP_ROWPX
+#define PF_WARP_ROWPX 0  // a thread's pixels consecutive in one row: one 16-B store per panorama
+#endif
 
 __device__ __forceinline__ void world_to_sph(float p0, float p1, float p2, float& az,
                                              float& zen)
@@ -114,8 +124,14 @@ __global__ void __launch_bounds__(kWB) k_warp_coords(const TileGeom* __restrict_
 
 __device__ __forceinline__ int patch_pixel(const WarpPatch& P, const TileGeom& g, int t, int k,
                                            int& i)
-{  // thread t, slot k -> tile pixel index i; returns 0 outside the tile
+{  // thread t, slot k -> tile pixel index i; returns 0 outside the tile.  A thread owns kPx
+   // consecutive pixels of one patch row (one 16-B store per panorama), a wave 8 whole rows.
+    static_assert(kPx == 4 && kPatch == 32, "4 pixels per thread, 8 threads per patch row");
+#if PF_WARP_ROWPX
+    const int X = P.X0 + 4 * (t & 7) + k, Y = P.Y0 + (t >> 3);
+#else  // a wave covers 2 rows per slot, slots 8 rows apart
     const int X = P.X0 + (t & (kPatch - 1)), Y = P.Y0 + t / kPatch + k * (kWB / kPatch);
+#endif
     i = Y * g.w + X;
     return X < g.w && Y < g.h;
 }
@@ -155,9 +171,15 @@ __global__ void __launch_bounds__(kWB) k_patch_box(const TileGeom* __restrict__ 
     if (t == 0) {
         int gx0 = ref + red[0];
         gx0 = gx0 < 0 ? gx0 + pw : (gx0 >= pw ? gx0 - pw : gx0);
+        int bw = red[1] - red[0] + 2;
+        if (PF_WARP_V4 && (pw & 3) == 0) {  // 16-B staging loads: origin and width in quads
+            const int a = gx0 & 3;
+            gx0 -= a;
+            bw = (bw + a + 3) & ~3;
+        }
         P.gx0 = gx0;
         P.gy0 = red[2];
-        P.bw = red[1] - red[0] + 2;
+        P.bw = bw;
         P.bh = red[3] - red[2] + 2;
         P.wide = (P.bw * P.bh > kCap || P.bw > pw / 2) ? 1 : 0;
         patches[blockIdx.x] = P;
@@ -263,46 +285,60 @@ struct WarpLanes {  // one thread's kPx pixels, all panorama-invariant
     uint32_t hp[kPx];   // mix32(pixel index): the per-pixel half of the noise hash
     f2 wx[kPx], wy[kPx];  // (1-fx, fx), (1-fy, fy)
     bool ok[kPx];
+    bool full;  // the kPx pixels are inside the tile and contiguous (one channel): 16-B store
 };
 
-// LDS-staged interpolation of kNB panoramas for a box of at most NS*256 floats.  The box is
-// double-buffered with the two parities interleaved (element e of parity PA at box[2e + PA]), so
-// a pixel's c00/c01 (and c10/c11) are one ds_read2_b32 with immediate offsets in both parities.
-// Every staging load is issued unconditionally (slots past the box reload a valid element,
-// panoramas past the chunk reload the last one), so the loads for panorama q+2 go out before
-// panorama q is interpolated and the wait for panorama q+1's loads -- an in-order vmcnt -- never
-// covers them.
-template <int NS, bool RESP>
+// LDS-staged interpolation of kNB panoramas for a box of at most NS*256 staging units (floats,
+// or with V4 column quads: 16-B loads of a box whose origin and width are whole quads, which
+// k_patch_box guarantees when pw % 4 == 0).  The box is double-buffered with the two parities
+// interleaved (element e of parity PA at box[2e + PA]), so a pixel's c00/c01 (and c10/c11) are
+// one ds_read2_b32 with immediate offsets in both parities.  Every staging load is issued
+// unconditionally (slots past the box reload a valid unit, panoramas past the chunk reload the
+// last one), so the loads for panorama q+2 go out before panorama q is interpolated and the wait
+// for panorama q+1's loads -- an in-order vmcnt -- never covers them.  A thread's four pixels
+// are consecutive in one tile row: one 16-B store per panorama when they are all inside.
+typedef uint32_t u4v __attribute__((ext_vector_type(4)));
+template <int NS, bool RESP, bool V4>
 __device__ __forceinline__ void warp_staged(float* box, const RespK* rk, const WarpPatch& P,
                                             int t, const WarpLanes& W,
                                             const float* __restrict__ pano, int pw, int ph,
                                             long long pstride, float* __restrict__ tiles,
                                             long long tstride, int bbeg, int nb)
 {
-    const int bw2 = 2 * P.bw, area = P.bw * P.bh;
-    uint32_t goff[NS];  // element e = t + 256*s of the bw x bh box -> panorama offset
+    constexpr int U = V4 ? 4 : 1;  // floats per staging unit
+    const int bw2 = 2 * P.bw, bwu = P.bw / U, units = bwu * P.bh;
+    uint32_t goff[NS];  // unit e = t + 256*s of the box -> panorama byte offset
 #pragma unroll
     for (int s = 0; s < NS; s++) {
         int e = t + s * kWB;
-        e = e < area ? e : area - 1;
-        const int r = e / P.bw, c = e - r * P.bw;
+        e = e < units ? e : units - 1;
+        const int r = e / bwu, c = (e - r * bwu) * U;
         int row = P.gy0 + r;
         row = row < ph ? row : ph - 1;
         int col = P.gx0 + c;
         col = col < pw ? col : col - pw;
         goff[s] = (uint32_t)(row * pw + col) * 4u;
     }
-    float stg[2][NS];
+    float stg[2][NS][U];
     const uint32_t pbytes = (uint32_t)(pstride * 4);
-    auto fetch = [&](float* dst, int q) {
+    auto fetch = [&](float (*dst)[U], int q) {
         const auto pr = rsrc(pano + (long long)(bbeg + (q < nb ? q : nb - 1)) * pstride, pbytes);
 #pragma unroll
-        for (int s = 0; s < NS; s++)
-            dst[s] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(pr, (int)goff[s], 0, 0));
-    };
-    auto put = [&](int pa, const float* src) {
+        for (int s = 0; s < NS; s++) {
+            if constexpr (V4) {
+                const u4v v = __builtin_amdgcn_raw_buffer_load_b128(pr, (int)goff[s], 0, 0);
 #pragma unroll
-        for (int s = 0; s < NS; s++) box[2 * (t + s * kWB) + pa] = src[s];
+                for (int j = 0; j < 4; j++) dst[s][j] = __uint_as_float(v[j]);
+            } else {
+                dst[s][0] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(pr, (int)goff[s], 0, 0));
+            }
+        }
+    };
+    auto put = [&](int pa, const float (*src)[U]) {
+#pragma unroll
+        for (int s = 0; s < NS; s++)
+#pragma unroll
+            for (int j = 0; j < U; j++) box[2 * ((t + s * kWB) * U + j) + pa] = src[s][j];
     };
     auto iter = [&](auto parity, int q) {
         constexpr int PA = decltype(parity)::value;
@@ -318,6 +354,7 @@ __device__ __forceinline__ void warp_staged(float* box, const RespK* rk, const W
             be = f2{r.beta, r.beta}; si = f2{r.sigma, r.sigma};
             key = r.key;
         }
+        float out[kPx];
 #pragma unroll
         for (int k = 0; k < kPx; k += 2) {
             f2 v;
@@ -336,9 +373,17 @@ __device__ __forceinline__ void warp_staged(float* box, const RespK* rk, const W
                 tt = tt + be;
                 v = pk_add_clamp01(tt, si * nz);
             }
+            out[k] = v[0];
+            out[k + 1] = v[1];
+        }
+        if (W.full) {
+            const u4v o = {__float_as_uint(out[0]), __float_as_uint(out[1]),
+                           __float_as_uint(out[2]), __float_as_uint(out[3])};
+            __builtin_amdgcn_raw_buffer_store_b128(o, orr, (int)W.oo[0], 0, 0);
+        } else {
 #pragma unroll
-            for (int j = 0; j < 2; j++)
-                __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v[j]), orr, (int)W.oo[k + j],
+            for (int k = 0; k < kPx; k++)
+                __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(out[k]), orr, (int)W.oo[k],
                                                       0, 0);
         }
         put(1 - PA, stg[1 - PA]);  // panorama q+1 (a duplicate past the chunk: unread)
@@ -354,17 +399,17 @@ __device__ __forceinline__ void warp_staged(float* box, const RespK* rk, const W
     }
 }
 
-template <int NS>
+template <int NS, bool V4>
 __device__ __forceinline__ void warp_staged_sel(bool resp, float* box, const RespK* rk,
                                                 const WarpPatch& P, int t, const WarpLanes& W,
                                                 const float* pano, int pw, int ph,
                                                 long long pstride, float* tiles,
                                                 long long tstride, int bbeg, int nb)
 {
-    if (resp) warp_staged<NS, true>(box, rk, P, t, W, pano, pw, ph, pstride, tiles, tstride,
+    if (resp) warp_staged<NS, true, V4>(box, rk, P, t, W, pano, pw, ph, pstride, tiles, tstride,
+                                        bbeg, nb);
+    else warp_staged<NS, false, V4>(box, rk, P, t, W, pano, pw, ph, pstride, tiles, tstride,
                                     bbeg, nb);
-    else warp_staged<NS, false>(box, rk, P, t, W, pano, pw, ph, pstride, tiles, tstride, bbeg,
-                                nb);
 }
 
 __global__ void __launch_bounds__(kWB) k_warp_depth(const TileGeom* __restrict__ geom,
@@ -433,17 +478,29 @@ __global__ void __launch_bounds__(kWB) k_warp_depth(const TileGeom* __restrict__
         return;
     }
 
+    W.full = PF_WARP_ROWPX && W.ok[0] && W.ok[kPx - 1] && g.c == 1;
 #pragma unroll
     for (int k = 0; k < kPx; k++) W.la[k] *= 2;  // parity-interleaved box
     __shared__ RespK rk[kNB];  // published by the first barrier inside warp_staged
     if (t < nb) rk[t] = resp_key(resp, bbeg + t, ntiles, P.tile);
-    const int ns = (P.bw * P.bh + kWB - 1) / kWB;  // uniform: staging loads per thread
-    if (ns <= 4) warp_staged_sel<4>(resp != nullptr, box, rk, P, t, W, pano, pw, ph, pstride,
-                                    tiles, tstride, bbeg, nb);
-    else if (ns <= 8) warp_staged_sel<8>(resp != nullptr, box, rk, P, t, W, pano, pw, ph,
-                                         pstride, tiles, tstride, bbeg, nb);
-    else warp_staged_sel<kSlots>(resp != nullptr, box, rk, P, t, W, pano, pw, ph, pstride,
-                                 tiles, tstride, bbeg, nb);
+    const bool rs = resp != nullptr;
+    if (PF_WARP_V4 && (pw & 3) == 0) {  // quad-aligned boxes (k_patch_box): 16-B staging loads
+        const int nq = (P.bw * P.bh / 4 + kWB - 1) / kWB;  // uniform: loads per thread
+        if (nq <= 1) warp_staged_sel<1, true>(rs, box, rk, P, t, W, pano, pw, ph, pstride, tiles,
+                                              tstride, bbeg, nb);
+        else if (nq <= 2) warp_staged_sel<2, true>(rs, box, rk, P, t, W, pano, pw, ph, pstride,
+                                                   tiles, tstride, bbeg, nb);
+        else warp_staged_sel<kSlots / 4, true>(rs, box, rk, P, t, W, pano, pw, ph, pstride,
+                                               tiles, tstride, bbeg, nb);
+    } else {
+        const int ns = (P.bw * P.bh + kWB - 1) / kWB;  // uniform: staging loads per thread
+        if (ns <= 4) warp_staged_sel<4, false>(rs, box, rk, P, t, W, pano, pw, ph, pstride,
+                                               tiles, tstride, bbeg, nb);
+        else if (ns <= 8) warp_staged_sel<8, false>(rs, box, rk, P, t, W, pano, pw, ph, pstride,
+                                                    tiles, tstride, bbeg, nb);
+        else warp_staged_sel<kSlots, false>(rs, box, rk, P, t, W, pano, pw, ph, pstride, tiles,
+                                            tstride, bbeg, nb);
+    }
 }
 
 // ---------------------------------------------------------------------------------------------
