@@ -563,6 +563,8 @@ static int prepare_levels(pf_ctx* c, int out_w, int out_h, float zr0, float zr1)
     if (lc.out_w == out_w && lc.out_h == out_h && lc.zr0 == b0 && lc.zr1 == b1) return PF_OK;
     if (out_w < 8 || out_h < 8)
         return fail(c, PF_EINVAL, "output %dx%d too small", out_w, out_h);
+    if ((long long)out_w * out_h >= (1LL << 31))  // per-panorama pixel indices are 32-bit
+        return fail(c, PF_EINVAL, "output %dx%d too large", out_w, out_h);
     int nl = out_w >= 4096 ? 4 : 3;
     for (int l = 0; l < nl; l++) {
         LevelDims L = level_dims(out_w, out_h, zr0, zr1, l);

@@ -940,15 +940,18 @@ __global__ void __launch_bounds__(256) k_border(const float* __restrict__ prev, 
                                                 float* __restrict__ bb, long long stride,
                                                 uint16_t* __restrict__ out, long long ostride)
 {
-    const long long top = (long long)L.h0 * L.w;
-    const long long bot = (long long)(L.h - 1 - L.h1) * L.w;
-    long long i = (long long)blockIdx.x * 256 + threadIdx.x;
+    // one panorama's level plane is < 2^31 pixels (the host checks out_w * out_h), so the
+    // pixel arithmetic is 32-bit: no 64-bit division in the index split
+    const int top = L.h0 * L.w;
+    const int bot = (L.h - 1 - L.h1) * L.w;
+    const int i = (int)blockIdx.x * 256 + (int)threadIdx.x;
     if (i >= top + bot) return;
     const int b = blockIdx.y;
-    long long o = i < top ? i : (long long)(L.h1 + 1) * L.w + (i - top);
-    int y = (int)(o / L.w), x = (int)(o - (long long)y * L.w);
+    const int y = i < top ? i / L.w : L.h1 + 1 + (i - top) / L.w;
+    const int x = i < top ? i - y * L.w : (i - top) - (y - L.h1 - 1) * L.w;
+    const int o = y * L.w + x;
     float v = 0.0f;
-    if (prev) v = prev[b * pstride + (long long)(y / 2) * (L.w / 2) + x / 2];
+    if (prev) v = prev[b * pstride + (y / 2) * (L.w / 2) + x / 2];
     if (out) {
         float q = v;
         if (q < 0) q = 0;
