@@ -113,6 +113,15 @@ int pf_warp_depth(pf_ctx* ctx, const float* pano, int pw, int ph, int batch,
  * GL_LINEAR + GL_REPEAT, rows top-first. */
 int pf_warp_rgb(pf_ctx* ctx, const uint8_t* pano, int pw, int ph, int batch, uint8_t* tiles);
 
+/* SolveDepthBySmoothing (Depth.cpp:1773-1878; Depth.h:309), the reference's alternate solver
+ * (not called by mode 0): every tile written into the out_w x out_h grid (a later tile
+ * overwrites an earlier one), 500 in-place Gauss-Seidel smoothing iterations on the pixels within
+ * 10 of a tile-box edge in rows [floor(h*zr0/MYPI), ceil(h*zr1/MYPI)], u16 quantisation.
+ * tiles: [batch][tile_elems] float (channel 0 read); coeffs: NULL, or [batch][ntiles][4] applied
+ * as Depth2DepthTransform on the fly; out: [batch][out_h][out_w] u16.  Bit-exact. */
+int pf_solve_smoothing(pf_ctx* ctx, const float* tiles, const float* coeffs, int batch,
+                       int out_w, int out_h, float zr0, float zr1, uint16_t* out);
+
 /* ---- multi-GPU fusion of one panorama (tiles sharded over ranks) ----
  * pf_fuse_partial scatters the Laplacian targets of tiles [t0, t1) for level `level` into
  * lsum/cnt ([out levels h][w] fp32 and fp32 counts); the caller sums them over ranks

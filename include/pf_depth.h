@@ -13,6 +13,7 @@
  *   MergeDepthMaps                                                     Depth.h:286-289
  *   SolveDepthToDepth                                                  Depth.h:297-298
  *   SolveDepthAll                                                      Depth.h:306-307
+ *   SolveDepthBySmoothing                                              Depth.h:309
  *   ErrorData / ErrorEmap                                              Depth.h:313-316
  *   SphericalToWorld / WorldToSpherical                                Depth.h:326-329
  *   Save16BitPNG                                                       Depth.cpp:27-32
@@ -162,6 +163,10 @@ bool SolveDepthToDepth(EquirectangularMap& emap, std::vector<PerspectiveMap>& pm
 bool SolveDepthAll(EquirectangularMap& emap, std::vector<PerspectiveMap>& pmaps,
                    unsigned short* data, int& out_width, int& out_height, Vec2f& zenith_range,
                    const char* Laplacian_filename = nullptr);
+// Depth.h:309, Depth.cpp:1773-1878: the reference's alternate solver (tiles written into the
+// grid, 500 Gauss-Seidel smoothing iterations near the tile-box edges), on the GPU, bit-exact.
+bool SolveDepthBySmoothing(std::vector<PerspectiveMap>& pmaps, unsigned short* data,
+                           int& out_width, int& out_height, Vec2f& zenith_range);
 
 bool ErrorData(EquirectangularMap& emap_gt, unsigned short* data, int data_width,
                int data_height, float& mse, float& mae, float& mre, float& mse_log,

@@ -902,3 +902,71 @@ void pfo_error_metrics(const float* gt, int gw, int gh, int gc, const float* giv
     cnt[0] = n;
     cnt[1] = nlog;
 }
+
+/* ---------------- SolveDepthBySmoothing (Depth.cpp:1773-1878) ---------------- */
+int pfo_solve_smoothing(const pfo_tile* tiles, int ntiles, const float* tile_data, int width,
+                        int height, float zr0, float zr1, uint16_t* data)
+{ /* Returns -1 for a degenerate box (x0 == x1: the reference never terminates), -2 when a box
+   * or the smoothing stencil leaves the buffer (the reference reads/writes out of bounds).
+   * Taps whose linear index leaves the tile are clamped as in pfo_targets. */
+    long long n = (long long)width * height;
+    float* buffer = (float*)calloc((size_t)n, sizeof(float));         /* :1775-1777 */
+    unsigned char* to_smooth = (unsigned char*)calloc((size_t)n, 1);   /* :1785-1786 */
+    const int range = 10;                                              /* :1787 */
+    int height0 = (int)floor((double)((float)height * zr0) / MYPI);     /* :1781 */
+    int height1 = (int)ceil((double)((float)height * zr1) / MYPI);      /* :1782 */
+    int rc = 0;
+    long long oob = 0;
+    if (!buffer || !to_smooth) { rc = -3; goto done; }
+    if (height0 < 1 || height1 > height - 2) { rc = -2; goto done; }
+    for (int p = 0; p < ntiles; p++) { /* :1790-1835 */
+        const pfo_tile* t = &tiles[p];
+        int x0 = (int)round((double)t->ranges[0] / (2 * MYPI) * (double)(width - 1));
+        int x1 = (int)round((double)t->ranges[1] / (2 * MYPI) * (double)(width - 1));
+        int y0 = (int)round((double)t->ranges[2] / MYPI * (double)(height - 1));
+        int y1 = (int)round((double)t->ranges[3] / MYPI * (double)(height - 1));
+        int xs = x1 >= x0 ? 1 : -1, ys = 1;
+        if (x0 == x1) { rc = -1; goto done; }
+        if (x0 < 0 || x0 >= width || x1 < 0 || x1 >= width || y0 < 0 || y1 >= height) {
+            rc = -2;
+            goto done;
+        }
+        int X = x0;
+        while (1) { /* X from x0 up to, but excluding, x1 */
+            for (int Y = y0; Y <= y1; Y += ys) {
+                float xy[2];
+                pfo_sph_to_2d(t, pfo_grid_azimuth(X, width), pfo_grid_zenith(Y, height), xy);
+                long long idx = clamp_index(t, pfo_tile_index(t, xy[0], xy[1]), &oob);
+                buffer[(long long)Y * width + X] = tile_data[t->offset + idx];
+                if (abs(X - x0) <= range || abs(X - x1) <= range || abs(Y - y0) <= range ||
+                    abs(Y - y1) <= range)
+                    to_smooth[(long long)Y * width + X] = 1;
+            }
+            X += xs;
+            if (X == x1) break;
+        }
+    }
+    for (int iter = 0; iter < 500; iter++) /* :1838-1856, in place, row-major */
+        for (int Y = height0; Y <= height1; Y++)
+            for (int X = 1; X < width - 1; X++) {
+                long long o = (long long)Y * width + X;
+                if (!to_smooth[o]) continue;
+                float val = buffer[o];
+                float val0 = buffer[o - 1];
+                float val1 = buffer[o + 1];
+                float val2 = buffer[o - width];
+                float val3 = buffer[o + width];
+                float avg = (val0 + val1 + val2 + val3) / 4;
+                buffer[o] = (float)((double)val + 0.5 * (double)(avg - val)); /* 0.5: double */
+            }
+    for (long long i = 0; i < n; i++) { /* :1859-1872 */
+        float val = buffer[i];
+        if (val < 0) val = 0;
+        if (val > 1) val = 1;
+        data[i] = (uint16_t)(val * 65535.0f);
+    }
+done:
+    free(buffer);
+    free(to_smooth);
+    return rc;
+}

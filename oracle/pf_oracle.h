@@ -104,6 +104,12 @@ int  pfo_merge_lm(const float* emap, int ew, int eh, int ec, const pfo_tile* til
                   float* tile_data, int out_w, float zr0, float zr1, uint16_t* out,
                   float* abcd_out);
 
+/* SolveDepthBySmoothing (Depth.cpp:1773-1878): tiles written into the width x height grid (a
+ * later tile overwrites), 500 in-place Gauss-Seidel iterations on the pixels within 10 of a box
+ * edge, u16.  Returns 0, -1 (x0 == x1), -2 (box or stencil leaves the buffer). */
+int  pfo_solve_smoothing(const pfo_tile* tiles, int ntiles, const float* tile_data, int width,
+                         int height, float zr0, float zr1, uint16_t* data);
+
 /* ---------------- fusion (Depth.cpp:1416-1771) ---------------- */
 typedef struct pfo_level {
     int w, h, h0, h1, iters, max_level;

@@ -95,6 +95,8 @@ def lib():
                                 C.c_float, C.c_float, C.c_int, C.c_int, C.POINTER(C.c_uint16),
                                 fp]
         L.pfo_warp_depth.argtypes = [fp, C.c_int, C.c_int, TP, C.c_int, C.POINTER(Response), fp]
+        L.pfo_solve_smoothing.argtypes = [TP, C.c_int, fp, C.c_int, C.c_int, C.c_float,
+                                          C.c_float, C.POINTER(C.c_uint16)]
         L.pfo_warp_rgb.argtypes = [C.POINTER(C.c_uint8), C.c_int, C.c_int, TP, C.c_int,
                                    C.POINTER(C.c_uint8)]
         L.pfo_hash32.argtypes = [C.c_uint32, C.c_uint32]
@@ -207,6 +209,16 @@ def solve_depth_all(emap, tiles, tile_data, out_w, zr):
     if rc != 0:
         raise ValueError(f"pfo_solve_depth_all rc={rc}")
     return out.reshape(out_w // 2, out_w), oops.value
+
+
+def solve_smoothing(tiles, tile_data, out_w, out_h, zr):
+    """SolveDepthBySmoothing (Depth.cpp:1773-1878) -> u16 [out_h, out_w]."""
+    out = np.zeros(out_w * out_h, np.uint16)
+    rc = lib().pfo_solve_smoothing(tiles, len(tiles), _p(tile_data), out_w, out_h, zr[0], zr[1],
+                                   _p(out, C.c_uint16))
+    if rc != 0:
+        raise ValueError(f"pfo_solve_smoothing rc={rc}")
+    return out.reshape(out_h, out_w)
 
 
 SOLVERS = {"normal": 0, "lm": 1}  # PFO_SOLVER_*; "lm" (the reference's Ceres LM) is the default

@@ -7,7 +7,8 @@
 //                               SphericalToWorld, WorldToSpherical (host only, no GPU)
 //   facade_check solve IN OUT   per tile SolveDepthToDepth (one active map) +
 //                               Depth2DepthTransform (Depth.cpp:794-805), then SolveDepthAll
-//                               (:913), then SolveDepthToDepth with several active maps
+//                               (:913), then SolveDepthToDepth with several active maps, then
+//                               SolveDepthBySmoothing (:1773-1878) on the transformed maps
 //
 // IN/OUT are flat little-endian binaries written/read by tests/test_facade.py.
 #include "../../include/pf_depth.h"
@@ -135,6 +136,9 @@ int solve(Reader& r, Writer& w)
     Vec4f joint;
     if (!SolveDepthToDepth(emap, pmaps, actives, zr, joint)) return 4;
     w.put(joint.v, 4);
+    // the alternate solver on the same (transformed) maps (Depth.h:309)
+    if (!SolveDepthBySmoothing(pmaps, out.data(), out_w, out_h, zr)) return 5;
+    w.put(out.data(), out.size());
     return 0;
 }
 }  // namespace

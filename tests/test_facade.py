@@ -114,6 +114,8 @@ def test_facade_solvers_bit_exact(tmp_path):
     u16 = out[off:off + 2 * 512 * 256].view(np.uint16).reshape(256, 512)
     off += 2 * 512 * 256
     joint = out[off:off + 16].view(np.float32)
+    off += 16
+    smooth = out[off:off + 2 * 512 * 256].view(np.uint16).reshape(256, 512)
     # the oracle runs MergeDepthMaps' sequence on the same inputs (LM registration, Ceres-style)
     ref_data = data.copy()
     for p in range(n):
@@ -123,6 +125,8 @@ def test_facade_solvers_bit_exact(tmp_path):
     assert np.array_equal(tdata.view(np.uint32), ref_data.view(np.uint32))
     ref_out, _ = O.solve_depth_all(emap, tiles, ref_data, 512, ZR)
     assert int((u16 != ref_out).sum()) == 0
+    ref_smooth = O.solve_smoothing(tiles, ref_data, 512, 256, ZR)
+    assert int((smooth != ref_smooth).sum()) == 0
     xs, ys = [], []
     for p in act:
         x, y, _, _ = O.reg_samples(tiles[p], ref_data, emap, ZR)

@@ -1,0 +1,86 @@
+"""SolveDepthBySmoothing (Depth.cpp:1773-1878) on the GPU against the oracle.
+
+pf_solve_smoothing reproduces the reference's lexicographic in-place Gauss-Seidel with a
+wavefront schedule (pf_smooth.hip); bar: bit-exact u16 output.  Parity against the reference
+itself is unpinned (pf_oracle.h), as for every path here.
+"""
+import numpy as np
+import pytest
+
+torch = pytest.importorskip("torch")
+
+pytestmark = pytest.mark.gpu
+
+import panofuse  # noqa: E402
+import pf_layouts as PL  # noqa: E402
+import pf_synth  # noqa: E402
+import pyoracle as O  # noqa: E402
+
+ZR = PL.ZENITH_RANGE
+DEV = "cuda:0"
+CFGS = {"C1": 512, "C2": 2048, "LERES": 1024}
+
+
+@pytest.fixture(scope="module")
+def fuser():
+    if not torch.cuda.is_available():
+        pytest.fail("GPU test collected on a host without a GPU")
+    return panofuse.Fuser(0)
+
+
+def _tiles(cfg, seed, n=1):
+    out_w = CFGS[cfg]
+    lay = PL.config_layout(cfg)
+    tiles, total = O.make_tiles(lay)
+    datas = []
+    for k in range(n):
+        seeds = pf_synth.seeds_for(1, 20261015 + 97 * seed + k)
+        gt = pf_synth.scene_depth(seeds, out_w, out_w // 2)[0].numpy()
+        resp = pf_synth.responses(seeds, lay.ntiles)
+        datas.append(O.warp_depth(gt, tiles, total, O.responses(resp)))
+    return lay, tiles, np.stack(datas), out_w
+
+
+@pytest.mark.parametrize("cfg,batch", [("C1", 3), ("C2", 2), ("LERES", 1)])
+def test_smoothing_bit_exact(fuser, cfg, batch):
+    lay, tiles, data, out_w = _tiles(cfg, 1, batch)
+    fuser.set_tiles(lay)
+    out = torch.zeros((batch, out_w // 2, out_w), dtype=torch.int16, device=DEV)
+    fuser.solve_smoothing(torch.from_numpy(data).to(DEV), out, ZR)
+    got = out.cpu().numpy().view(np.uint16)
+    for b in range(batch):
+        ref = O.solve_smoothing(tiles, np.ascontiguousarray(data[b]), out_w, out_w // 2, ZR)
+        bad = int((got[b] != ref).sum())
+        assert bad == 0, f"{cfg} panorama {b}: {bad} pixels differ (max |d| " \
+                         f"{int(np.abs(got[b].astype(np.int64) - ref).max())})"
+        assert int((ref != 0).sum()) > out_w  # non-trivial output
+
+
+def test_smoothing_with_transform_equals_pretransformed(fuser):
+    """coeffs applied on the fly == Depth2DepthTransform applied to the tiles first."""
+    lay, tiles, data, out_w = _tiles("C1", 2, 2)
+    rng = np.random.default_rng(5)
+    coeffs = np.zeros((2, lay.ntiles, 4), np.float32)
+    coeffs[:, :, 0] = rng.uniform(-0.3, 0.3, (2, lay.ntiles))
+    coeffs[:, :, 1] = rng.uniform(-0.3, 0.3, (2, lay.ntiles))
+    coeffs[:, :, 2] = rng.uniform(0.8, 1.2, (2, lay.ntiles))
+    coeffs[:, :, 3] = rng.uniform(-0.05, 0.05, (2, lay.ntiles))
+    fuser.set_tiles(lay)
+    out = torch.zeros((2, out_w // 2, out_w), dtype=torch.int16, device=DEV)
+    fuser.solve_smoothing(torch.from_numpy(data).to(DEV), out, ZR,
+                          coeffs=torch.from_numpy(coeffs).to(DEV))
+    got = out.cpu().numpy().view(np.uint16)
+    for b in range(2):
+        d = np.ascontiguousarray(data[b]).copy()
+        for p in range(lay.ntiles):
+            O.depth_to_depth(tiles[p], d, coeffs[b, p])
+        ref = O.solve_smoothing(tiles, d, out_w, out_w // 2, ZR)
+        assert int((got[b] != ref).sum()) == 0
+
+
+def test_smoothing_rejects_stencil_outside(fuser):
+    lay, tiles, data, out_w = _tiles("C1", 3, 1)
+    fuser.set_tiles(lay)
+    out = torch.zeros((1, out_w // 2, out_w), dtype=torch.int16, device=DEV)
+    with pytest.raises(RuntimeError):
+        fuser.solve_smoothing(torch.from_numpy(data).to(DEV), out, (0.0, ZR[1]))

@@ -252,3 +252,22 @@ def test_layout_coverage_counts():
             else:
                 assert n.max() == 4 and len(many) == 7, (level, len(many))
                 assert set(many[:, 1].tolist()) == {lv.w // 2}
+
+
+def test_oracle_smoothing_restatement():
+    """SolveDepthBySmoothing (Depth.cpp:1773-1878): pixels no tile covers stay 0 (the poles, and
+    column 0: every box stops before x1 = 0), smoothing never leaves the range of its inputs, and
+    a zenith range whose stencil leaves the buffer is refused (the reference reads out of
+    bounds there)."""
+    lay = PL.config_layout("C1")
+    tiles, total = O.make_tiles(lay)
+    data = np.random.default_rng(3).uniform(0.2, 0.8, total).astype(np.float32)
+    out = O.solve_smoothing(tiles, data, 512, 256, PL.ZENITH_RANGE)
+    again = O.solve_smoothing(tiles, data, 512, 256, PL.ZENITH_RANGE)
+    assert np.array_equal(out, again)
+    assert out[0].max() == 0 and out[-1].max() == 0  # the poles: outside every tile box
+    assert out[:, 0].max() == 0
+    covered = out[40:216, 1:]
+    assert covered.max() <= int(0.8 * 65535) and (covered >= int(0.2 * 65535) - 1).mean() > 0.95
+    with pytest.raises(ValueError):
+        O.solve_smoothing(tiles, data, 512, 256, (0.0, PL.ZENITH_RANGE[1]))

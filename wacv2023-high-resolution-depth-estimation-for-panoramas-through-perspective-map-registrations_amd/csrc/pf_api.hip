@@ -75,6 +75,8 @@ struct pf_ctx {
     DevBuf wmap, wfxy, wpatch;
     // workspace
     DevBuf buf[3], lnorm, coeffs, lsum_ws, metrics_ws, reg_sums, reg_active;
+    // SolveDepthBySmoothing (pf_smooth.hip): boxes, grid tables, per-pixel source and mask
+    DevBuf sm_box, sm_cols, sm_rows, sm_src, sm_mask;
     // stage profiling
     struct Span {
         int stage;
@@ -1157,6 +1159,60 @@ int pf_merge(pf_ctx* c, const float* emap, int ew, int eh, int ec, const float* 
                           cf, nullptr)))
         return rc;
     return fuse_impl(c, emap, ew, eh, ec, tiles, cf, batch, out_w, out_w / 2, zr0, zr1, out);
+}
+
+int pf_solve_smoothing(pf_ctx* c, const float* tiles, const float* coeffs, int batch, int out_w,
+                       int out_h, float zr0, float zr1, uint16_t* out)
+{  // SolveDepthBySmoothing (Depth.cpp:1773-1878)
+    int rc;
+    if ((rc = check_common(c, batch))) return rc;
+    if (!tiles || !out) return fail(c, PF_EINVAL, "tiles/out is NULL");
+    if (out_w < 3 || out_h < 3 || (long long)out_w * out_h >= (1LL << 31))
+        return fail(c, PF_EINVAL, "output %dx%d out of range", out_w, out_h);
+    LevelDims L{};
+    L.w = out_w;
+    L.h = out_h;
+    L.h0 = (int)floor((double)((float)out_h * zr0) / PF_MYPI);  // height0/height1 (:1781-1782)
+    L.h1 = (int)ceil((double)((float)out_h * zr1) / PF_MYPI);
+    if (L.h0 < 1 || L.h1 > out_h - 2 || L.h0 > L.h1)
+        return fail(c, PF_EINVAL, "rows [%d, %d] of %d: the smoothing stencil would leave the "
+                    "buffer (the reference reads out of bounds)", L.h0, L.h1, out_h);
+    std::vector<SmoothBox> boxes(c->ntiles);
+    for (int p = 0; p < c->ntiles; p++) {  // :1795-1805, no clamps
+        const pf_window& r = c->rng[p];
+        SmoothBox b{};
+        b.x0 = (int)round((double)r.az_left / (2 * PF_MYPI) * (double)(out_w - 1));
+        b.x1 = (int)round((double)r.az_right / (2 * PF_MYPI) * (double)(out_w - 1));
+        b.y0 = (int)round((double)r.zen_top / PF_MYPI * (double)(out_h - 1));
+        b.y1 = (int)round((double)r.zen_down / PF_MYPI * (double)(out_h - 1));
+        b.xs = b.x1 >= b.x0 ? 1 : -1;
+        if (b.x0 == b.x1)
+            return fail(c, PF_EDEGENERATE, "tile %d: box x0 == x1 == %d (the reference never "
+                        "terminates here)", p, b.x0);
+        if (b.x0 < 0 || b.x0 >= out_w || b.x1 < 0 || b.x1 >= out_w || b.y0 < 0 || b.y1 >= out_h)
+            return fail(c, PF_EINVAL, "tile %d: box (%d..%d, %d..%d) leaves the %dx%d output (the "
+                        "reference writes out of bounds)", p, b.x0, b.x1, b.y0, b.y1, out_w, out_h);
+        boxes[p] = b;
+    }
+    std::vector<GridCol> cols;
+    std::vector<GridRow> rows;
+    grid_tables(L, cols, rows);
+    const long long n = (long long)out_w * out_h;
+    if ((rc = upload(c, c->sm_box, boxes))) return rc;
+    if ((rc = upload(c, c->sm_cols, cols))) return rc;
+    if ((rc = upload(c, c->sm_rows, rows))) return rc;
+    if ((rc = ensure(c, c->sm_src, sizeof(int2) * n))) return rc;
+    if ((rc = ensure(c, c->sm_mask, n))) return rc;
+    if ((rc = ensure(c, c->buf[0], sizeof(float) * n * batch))) return rc;
+    launch_smooth_map(c->stream, (const TileGeom*)c->geom.p, (const SmoothBox*)c->sm_box.p,
+                      c->ntiles, (const GridCol*)c->sm_cols.p, (const GridRow*)c->sm_rows.p,
+                      out_w, out_h, (int2*)c->sm_src.p, (uint8_t*)c->sm_mask.p);
+    launch_smooth(c->stream, (const TileGeom*)c->geom.p, c->ntiles, (const int2*)c->sm_src.p,
+                  (const uint8_t*)c->sm_mask.p, tiles, c->tile_elems, coeffs, out_w, out_h, L.h0,
+                  L.h1, 500, (float*)c->buf[0].p, batch);  // 500 iterations (:1838)
+    launch_quantize(c->stream, (const float*)c->buf[0].p, n, (int)n, out, n, batch);
+    HIPCHK(c, hipGetLastError());
+    return PF_OK;
 }
 
 int pf_warp_depth(pf_ctx* c, const float* pano, int pw, int ph, int batch,

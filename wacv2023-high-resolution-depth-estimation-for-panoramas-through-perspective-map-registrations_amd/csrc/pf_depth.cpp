@@ -531,6 +531,25 @@ bool SolveDepthAll(EquirectangularMap& emap, std::vector<PerspectiveMap>& pmaps,
     return hip_ok(hipMemcpy(data, dout.p, no * 2, hipMemcpyDeviceToHost), "download");
 }
 
+bool SolveDepthBySmoothing(std::vector<PerspectiveMap>& pmaps, unsigned short* data,
+                           int& out_width, int& out_height, Vec2f& zr)
+{  // Depth.cpp:1773-1878 on the GPU (pf_solve_smoothing)
+    pf_ctx* c = facade_ctx();
+    if (!c) return false;
+    std::vector<PerspectiveMap*> pm;
+    for (auto& p : pmaps) pm.push_back(&p);
+    std::vector<float> packed;
+    if (!set_layout(c, pm, packed)) return false;
+    const size_t no = (size_t)out_width * out_height;
+    DevMem dt(packed.size() * 4), dout(no * 2);
+    if (!upload(dt, packed.data(), packed.size()) || !dout.ok) return false;
+    if (!pf_ok(c, pf_solve_smoothing(c, dt.as<float>(), nullptr, 1, out_width, out_height, zr[0],
+                                     zr[1], dout.as<uint16_t>()),
+               "pf_solve_smoothing"))
+        return false;
+    return hip_ok(hipMemcpy(data, dout.p, no * 2, hipMemcpyDeviceToHost), "download");
+}
+
 bool ErrorData(EquirectangularMap& gt, unsigned short* data, int w, int h, float& mse,
                float& mae, float& mre, float& mselog, float& d1, float& d2, float& d3,
                int align_way, bool cap_depth, Vec2f* ls, float* shift)

@@ -43,6 +43,11 @@ struct TapBox {
     long long off;
 };
 
+// Tile box of SolveDepthBySmoothing (Depth.cpp:1795-1808): the fusion box without its clamps.
+struct SmoothBox {
+    int x0, x1, y0, y1, xs, pad[3];
+};
+
 struct GridCol { float az, ca, sa, pad; };   // column xx (index xx+1): az, cos az, sin az
 struct GridRow { float zen, sz, cz, pad; };  // row yy (index yy+1): zen, sin zen, cos zen
 
@@ -224,6 +229,15 @@ void launch_warp_rgb(hipStream_t s, const RgbCam* cams, const TileGeom* geom, in
                      long long npix_total, const long long* pix_prefix,
                      const long long* rgb_off, const uint8_t* pano, int pw, int ph,
                      long long pstride, uint8_t* tiles, long long tstride, int batch);
+
+// SolveDepthBySmoothing (pf_smooth.hip).
+void launch_smooth_map(hipStream_t s, const TileGeom* geom, const SmoothBox* box, int ntiles,
+                       const GridCol* cols, const GridRow* rows, int w, int h, int2* src,
+                       uint8_t* mask);
+void launch_smooth(hipStream_t s, const TileGeom* geom, int ntiles, const int2* src,
+                   const uint8_t* mask, const float* tiles, long long tstride,
+                   const float* coeffs, int w, int h, int h0, int h1, int iters, float* buf,
+                   int batch);
 
 // Accuracy metrics (pf_metrics.hip).
 struct MetricsJob {

@@ -26,7 +26,7 @@ EXPORTS = [
     "pf_probe_taps", "pf_profile_enable", "pf_profile_read", "pf_error_metrics",
     "pf_depth_transform", "pf_register_joint", "pf_set_solver", "pf_fuse_normalize",
     "pf_fuse_border", "pf_fuse_band_plan", "pf_fuse_band_pass", "pf_fuse_multicover",
-    "pf_fuse_multicover_patch",
+    "pf_fuse_multicover_patch", "pf_solve_smoothing",
 ]
 SOLVERS = {"normal": 0, "lm": 1}  # PF_SOLVER_*; "lm" = the reference's Ceres LM (default)
 
@@ -77,6 +77,7 @@ def load():
     L.pf_merge.argtypes = [vp, vp, ip, ip, ip, vp, ip, ip, fp, fp, vp, vp]
     L.pf_warp_depth.argtypes = [vp, vp, ip, ip, ip, vp, vp]
     L.pf_warp_rgb.argtypes = [vp, vp, ip, ip, ip, vp]
+    L.pf_solve_smoothing.argtypes = [vp, vp, vp, ip, ip, ip, fp, fp, vp]
     L.pf_level_info.argtypes = [ip, ip, fp, fp, ip] + [C.POINTER(C.c_int)] * 6
     L.pf_fuse_partial.argtypes = [vp, vp, vp, ip, ip, ip, ip, fp, fp, ip, vp, vp]
     L.pf_fuse_seed.argtypes = [vp, vp, ip, ip, ip, vp, ip, ip, fp, fp, ip, vp]
@@ -213,6 +214,13 @@ class Fuser:
             raise ValueError("MergeDepthMaps output height is out_w/2")
         self._check(self.L.pf_merge(self.h, _ptr(emap), ew, eh, ec, _ptr(tiles), B, ow,
                                     float(zr[0]), float(zr[1]), _ptr(coeffs), _ptr(out)))
+
+    def solve_smoothing(self, tiles, out, zr, coeffs=None):
+        """SolveDepthBySmoothing (Depth.cpp:1773-1878) into out [B, out_h, out_w] (int16 view
+        of u16); coeffs: None or [B, ntiles, 4], applied as Depth2DepthTransform on the fly."""
+        B, oh, ow = out.shape
+        self._check(self.L.pf_solve_smoothing(self.h, _ptr(tiles), _ptr(coeffs), B, ow, oh,
+                                              float(zr[0]), float(zr[1]), _ptr(out)))
 
     def warp_depth(self, pano, tiles, resp=None):
         B, ph, pw = pano.shape
