@@ -331,10 +331,16 @@ def main():
     # Accuracy metrics (ErrorData of each result against its ground truth, median alignment,
     # Depth.cpp:1980-2213): not part of the step (the reference computes them only when a
     # ground-truth file is given), timed the same way on the same batch.
+    # The fp64-tree summation is timed for the roofline; the reference's own (sequential float)
+    # order, the library default, is timed beside it.
     mres = torch.zeros((B, 16), dtype=torch.int32, device=dev)
+    fz.set_metrics_order("tree")
     for _ in range(max(1, args.prof_steps)):
         fz.error_metrics_async(gt, out, zr, mres, 1, True)
     prof["metrics"] = fz.profile_read()["metrics"]
+    fz.set_metrics_order("sequential")
+    fz.error_metrics_async(gt, out, zr, mres, 1, True)
+    metrics_seq_ms = fz.profile_read()["metrics"][0]
     fz.profile(False)
     nprof = max(1, args.prof_steps)
 
@@ -415,8 +421,12 @@ def main():
                                  "peak": HBM_PEAK_GBS, "unit": "GB/s",
                                  "frac": stages["metrics"]["GBps"] / HBM_PEAK_GBS,
                                  "kernel": "pf_error_metrics (k_med_hist x3, k_med_scan x3, "
-                                           "k_err_sums, k_align, k_err_final)",
-                                 "ms_per_batch": stages["metrics"]["ms_per_step"]},
+                                           "k_err_sums, k_align, k_err_final), fp64 tree order",
+                                 "ms_per_batch": stages["metrics"]["ms_per_step"],
+                                 "ms_per_batch_sequential": metrics_seq_ms,
+                                 "sequential": "the reference's float summation order (library "
+                                               "default, bit-exact means): terms in parallel, "
+                                               "one lane per panorama adds them in order"},
             "nonzero_px_pano0": nz,
         }
         if not args.no_cpu_baseline:

@@ -218,6 +218,15 @@ typedef struct pf_metrics {
 int pf_error_metrics(pf_ctx* ctx, const float* gt, int gw, int gh, int gc, const float* given,
                      const uint16_t* given16, int w, int h, int given_c, int batch, float zr0,
                      float zr1, int align_way, int cap_depth, pf_metrics* out);
+/* Summation order of the means (mse, mae, mre, mselog) and of the least-squares sums:
+ *   PF_METRICS_SEQUENTIAL (default) -- the reference's: row-major, float accumulators (mse and
+ *     mselog through a double add, Depth.cpp:2119-2123, 2178-2186); bit-exact to it.  The
+ *     per-pixel terms are computed in parallel, one lane per panorama adds them in order.
+ *   PF_METRICS_TREE -- fp64 partial sums in a fixed tree: deterministic, ~10x faster at large
+ *     batches, means within 1e-5 relative of exact fp64 sums (not of the reference's floats). */
+#define PF_METRICS_TREE 0
+#define PF_METRICS_SEQUENTIAL 1
+int pf_set_metrics_order(pf_ctx* ctx, int order);
 
 /* Depth2DepthTransform of one map (Depth.cpp:245-274): channel 0 of npix pixels of a DEVICE
  * buffer with `channels` interleaved channels, X = clamp(v, 1e-4, 1-1e-4),

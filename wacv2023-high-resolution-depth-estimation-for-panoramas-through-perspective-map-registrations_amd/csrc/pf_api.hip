@@ -58,6 +58,7 @@ struct pf_ctx {
     // layout
     int ntiles = 0, tile_c = 1;
     int solver = PF_SOLVER_LM;  // degree-3 registration solver (pf_set_solver)
+    int metrics_order = PF_METRICS_SEQUENTIAL;  // pf_set_metrics_order
     std::vector<pf_window> fov, rng;
     std::vector<int> tw_h, th_h;
     bool layout_ok = false;  // the stored layout was set completely
@@ -1497,6 +1498,15 @@ int pf_probe_taps(pf_ctx* c, int out_w, int out_h, float zr0, float zr1, int lev
     return PF_OK;
 }
 
+int pf_set_metrics_order(pf_ctx* c, int order)
+{
+    if (!c) return PF_EINVAL;
+    if (order != PF_METRICS_SEQUENTIAL && order != PF_METRICS_TREE)
+        return fail(c, PF_EINVAL, "metrics order %d", order);
+    c->metrics_order = order;
+    return PF_OK;
+}
+
 int pf_error_metrics(pf_ctx* c, const float* gt, int gw, int gh, int gc, const float* given,
                      const uint16_t* given16, int w, int h, int given_c, int batch, float zr0,
                      float zr1, int align_way, int cap_depth, pf_metrics* out)
@@ -1529,8 +1539,12 @@ int pf_error_metrics(pf_ctx* c, const float* gt, int gw, int gh, int gc, const f
     if (j.h1 < j.h0) return fail(c, PF_EINVAL, "pf_error_metrics: empty zenith band");
     j.align_way = align_way;
     j.cap_depth = cap_depth ? 1 : 0;
+    j.sequential = c->metrics_order == PF_METRICS_SEQUENTIAL ? 1 : 0;
     int rc;
-    if ((rc = ensure(c, c->metrics_ws, metrics_workspace_bytes(batch)))) return rc;
+    if ((rc = ensure(c, c->metrics_ws,
+                     metrics_workspace_bytes(batch, (long long)(j.h1 - j.h0 + 1) * w,
+                                             j.sequential != 0))))
+        return rc;
     // algorithmic bytes: one read of the compared band of gt (4 B, channel 0) and of the
     // result (2 B u16 / 4 B f32); the kernels make 4 passes (3 radix digits + the sums) for
     // align_way 1, 2 for align_way 2, 1 otherwise

@@ -248,8 +248,9 @@ struct MetricsJob {
     int w, h, gc_given, batch;
     int h0, h1;  // compared rows, inclusive, clipped to [0, h-1]
     int align_way, cap_depth;
+    int sequential;  // the reference's summation order (PF_METRICS_SEQUENTIAL)
 };
-size_t metrics_workspace_bytes(int batch);
+size_t metrics_workspace_bytes(int batch, long long band, bool sequential);
 void launch_d2d_map(hipStream_t s, float* data, long long npx, int c, const float* abcd);
 void launch_metrics(hipStream_t s, const MetricsJob& j, void* ws, pf_metrics* out);
 

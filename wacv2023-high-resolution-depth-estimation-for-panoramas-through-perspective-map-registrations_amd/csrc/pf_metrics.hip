@@ -420,16 +420,220 @@ __global__ __launch_bounds__(MB) void k_err_final(const double* part, int nblk, 
     out[b] = m;
 }
 
+// ---------------------------------------------------------------------------------------------
+// The reference's own summation order (pf_set_metrics_order(PF_METRICS_SEQUENTIAL)).  The
+// reference accumulates in row-major order into floats: mse and mselog through a double
+// (`mse += pow(val0 - val1, 2)` is float = (float)((double)float + double)), mae and mre in
+// float, the least-squares sums a_00..b_1 in float (Depth.cpp:2119-2123, 2178-2186).  Each
+// pixel's terms are computed in parallel (k_seq_terms) and written in that order; one lane per
+// panorama then adds them in sequence (k_ls_seq / k_err_seq).  A pixel that the reference skips
+// contributes exact zeros (x + 0 == x for every finite x >= 0), so the lanes need no masks; the
+// counts (n, nlog, delta fails) are integers and stay in the parallel pass (k_err_sums).
+struct SeqTerms {  // term of band pixel i = (y - h0) * w + x of panorama b at [i * nb + b]: the
+                  // lanes (panoramas) of the summing wave read one contiguous row per pixel
+    double* sq;    // ERR: (double)d * (double)d (exact);  LS: v1 * v1 and v0 * v1 (float pair)
+    double* lg2;   // ERR: (double)lg * (double)lg (exact), 0 where the log is skipped
+    float* ad;     // ERR: fabsf(d);   LS: v1
+    float* re;     // ERR: fabsf(d) / v0;   LS: v0
+    float* one;    // LS: 1 where compared, else 0
+};
+
+template <bool LS>
+__global__ __launch_bounds__(MB) void k_seq_terms(MArgs a, int align_way, const Align* al,
+                                                  SeqTerms T, long long band)
+{
+    const int b = blockIdx.y, nb = gridDim.y;
+    const Align A = al ? al[b] : Align{1.0f, 0.0f, 0.0f, 0.0f, 0.0f};
+    for (int y = a.h0 + blockIdx.x; y <= a.h1; y += gridDim.x)
+    for (int x0 = 4 * threadIdx.x; x0 < a.w; x0 += 4 * MB) {
+      float V0[4], V1[4];
+      bool ok[4];
+      eval4(a, b, x0, y, false, V0, V1, ok);
+      for (int k = 0; k < 4 && x0 + k < a.w; ++k) {
+        const long long i = ((long long)(y - a.h0) * a.w + x0 + k) * nb + b;
+        const float v0 = V0[k];
+        float v1 = V1[k];
+        if (LS) {
+            float2 pr = make_float2(0.0f, 0.0f);
+            if (ok[k]) pr = make_float2(v1 * v1, v0 * v1);
+            reinterpret_cast<float2*>(T.sq)[i] = pr;
+            T.ad[i] = ok[k] ? v1 : 0.0f;
+            T.re[i] = ok[k] ? v0 : 0.0f;
+            T.one[i] = ok[k] ? 1.0f : 0.0f;
+            continue;
+        }
+        double sq = 0.0, lg2 = 0.0;
+        float ad = 0.0f, re = 0.0f;
+        if (ok[k]) {
+            if (align_way == 1)
+                v1 *= A.shift;
+            else if (align_way == 2)
+                v1 = v1 * A.s + A.o;
+            const float d = v0 - v1;
+            sq = (double)d * (double)d;
+            ad = fabsf(d);
+            re = fabsf(d) / v0;
+            if ((double)v0 > 1e-4 && (double)v1 > 1e-4) {
+                const float lg = log10f(v0) - log10f(v1);
+                lg2 = (double)lg * (double)lg;
+            }
+        }
+        T.sq[i] = sq;
+        T.lg2[i] = lg2;
+        T.ad[i] = ad;
+        T.re[i] = re;
+      }
+    }
+}
+
+// Depth.cpp:2119-2134 in the reference's float order, one lane per panorama.  The loads of a
+// block of PU pixels are issued before its additions (they do not depend on the accumulators),
+// so the lone summing wave keeps PU rows in flight.
+constexpr int PU = 16;
+__global__ __launch_bounds__(64) void k_ls_seq(SeqTerms T, long long band, int batch, Align* al)
+{
+    const int b = blockIdx.x * 64 + threadIdx.x;
+    if (b >= batch) return;
+    const float2* sq = reinterpret_cast<const float2*>(T.sq);
+    float a00 = 0, a01 = 0, a11 = 0, b0 = 0, b1 = 0;
+    long long i = 0;
+    for (; i + PU <= band; i += PU) {
+        float2 p[PU];
+        float v1[PU], v0[PU], one[PU];
+#pragma unroll
+        for (int u = 0; u < PU; ++u) {
+            const long long o = (i + u) * batch + b;
+            p[u] = sq[o];
+            v1[u] = T.ad[o];
+            v0[u] = T.re[o];
+            one[u] = T.one[o];
+        }
+#pragma unroll
+        for (int u = 0; u < PU; ++u) {
+            a00 += p[u].x;
+            a01 += v1[u];
+            a11 += one[u];
+            b0 += p[u].y;
+            b1 += v0[u];
+        }
+    }
+    for (; i < band; ++i) {
+        const long long o = i * batch + b;
+        a00 += sq[o].x;
+        a01 += T.ad[o];
+        a11 += T.one[o];
+        b0 += sq[o].y;
+        b1 += T.re[o];
+    }
+    const float det = a00 * a11 - a01 * a01;
+    Align A{1.0f, 0.0f, 0.0f, 0.0f, 0.0f};
+    A.s = (a11 * b0 - a01 * b1) / det;
+    A.o = (-a01 * b0 + a00 * b1) / det;
+    al[b] = A;
+}
+
+// Depth.cpp:2178-2186, 2207-2210 in the reference's order, one lane per panorama; the integer
+// counts come from the parallel pass's part[] (exact in any order).
+__global__ __launch_bounds__(64) void k_err_seq(SeqTerms T, long long band, int batch,
+                                                const double* part, int nblk, const Align* al,
+                                                pf_metrics* out)
+{
+    const int b = blockIdx.x * 64 + threadIdx.x;
+    if (b >= batch) return;
+    float mse = 0, mae = 0, mre = 0, mselog = 0;
+    // software pipeline: the loads of block k+1 are in flight while block k is added
+    struct Blk {
+        double sq[PU], lg2[PU];
+        float ad[PU], re[PU];
+    };
+    auto load = [&](Blk& B, long long i) {
+#pragma unroll
+        for (int u = 0; u < PU; ++u) {
+            const long long o = (i + u) * batch + b;
+            B.sq[u] = T.sq[o];
+            B.lg2[u] = T.lg2[o];
+            B.ad[u] = T.ad[o];
+            B.re[u] = T.re[o];
+        }
+    };
+    auto add = [&](const Blk& B) {
+#pragma unroll
+        for (int u = 0; u < PU; ++u) {
+            mse = (float)((double)mse + B.sq[u]);
+            mae += B.ad[u];
+            mre += B.re[u];
+            mselog = (float)((double)mselog + B.lg2[u]);
+        }
+    };
+    const long long nfull = band / PU;
+    long long i = 0;
+    if (nfull > 0) {
+        Blk A, B;
+        load(A, 0);
+        long long k = 1;
+        for (; k + 1 < nfull; k += 2) {
+            load(B, k * PU);
+            add(A);
+            load(A, (k + 1) * PU);
+            add(B);
+        }
+        if (k < nfull) {
+            load(B, k * PU);
+            add(A);
+            add(B);
+        } else {
+            add(A);
+        }
+        i = nfull * PU;
+    }
+    for (; i < band; ++i) {
+        const long long o = i * batch + b;
+        mse = (float)((double)mse + T.sq[o]);
+        mae += T.ad[o];
+        mre += T.re[o];
+        mselog = (float)((double)mselog + T.lg2[o]);
+    }
+    double cnt[5] = {0, 0, 0, 0, 0};  // n, nlog, fail1..3: integer-valued, order-free
+    for (int i = 0; i < nblk; ++i)
+        for (int k = 0; k < 5; ++k) cnt[k] += part[((long long)b * nblk + i) * (NSUM + 1) + 4 + k];
+    const int n = (int)cnt[0], nlog = (int)cnt[1];
+    const int f1 = (int)cnt[2], f2 = (int)cnt[3], f3 = (int)cnt[4];
+    pf_metrics m;
+    m.mse = mse / (float)n;
+    m.mae = mae / (float)n;
+    m.mre = mre / (float)n;
+    m.mselog = mselog / (float)nlog;
+    m.delta1 = (float)(n - f1) / (float)n;
+    m.delta2 = (float)(n - f2) / (float)n;
+    m.delta3 = (float)(n - f3) / (float)n;
+    const Align A = al[b];
+    m.median_shift = A.shift;
+    m.ls_s = A.s;
+    m.ls_o = A.o;
+    m.gt_median = A.gt_med;
+    m.given_median = A.gv_med;
+    m.n = n;
+    m.nlog = nlog;
+    m.reserved[0] = m.reserved[1] = 0;
+    out[b] = m;
+}
+
 }  // namespace
 
-size_t metrics_workspace_bytes(int batch)
+static size_t seq_bytes(long long band, int batch)
+{  // SeqTerms: sq + lg2 (8 B each), ad + re + one (4 B each) per band pixel and panorama
+    return (size_t)band * batch * (8 + 8 + 4 + 4 + 4) + 5 * 256;
+}
+
+size_t metrics_workspace_bytes(int batch, long long band, bool sequential)
 {
     const size_t hist = sizeof(uint32_t) * 2 * HBINS * batch;
     const size_t st = sizeof(SelState) * 2 * batch;
     const size_t part = sizeof(double) * (NSUM + 1) * MNBLK * batch;
     const size_t al = sizeof(Align) * batch;
     return ((hist + 255) & ~(size_t)255) + ((st + 255) & ~(size_t)255) +
-           ((part + 255) & ~(size_t)255) + al + 256;
+           ((part + 255) & ~(size_t)255) + ((al + 255) & ~(size_t)255) + 256 +
+           (sequential ? seq_bytes(band, batch) : 0);
 }
 
 void launch_metrics(hipStream_t s, const MetricsJob& j, void* ws, pf_metrics* out)
@@ -468,6 +672,15 @@ void launch_metrics(hipStream_t s, const MetricsJob& j, void* ws, pf_metrics* ou
     SelState* st = (SelState*)carve(sizeof(SelState) * 2 * j.batch);
     double* part = (double*)carve(sizeof(double) * (NSUM + 1) * MNBLK * j.batch);
     Align* al = (Align*)carve(sizeof(Align) * j.batch);
+    const long long band = (long long)(j.h1 - j.h0 + 1) * j.w;
+    SeqTerms T{};
+    if (j.sequential) {
+        T.sq = (double*)carve(sizeof(double) * band * j.batch);
+        T.lg2 = (double*)carve(sizeof(double) * band * j.batch);
+        T.ad = (float*)carve(sizeof(float) * band * j.batch);
+        T.re = (float*)carve(sizeof(float) * band * j.batch);
+        T.one = (float*)carve(sizeof(float) * band * j.batch);
+    }
 
     // Panoramas in chunks (all at once by default).  Chunks sized to the 256 MB Infinity Cache
     // were measured slower at C3 (1.47 vs 1.42 ms for 64 panoramas): the passes are not
@@ -483,6 +696,7 @@ void launch_metrics(hipStream_t s, const MetricsJob& j, void* ws, pf_metrics* ou
         SelState* sc = st + 2 * b0;
         double* pc = part + (long long)b0 * (NSUM + 1) * MNBLK;
         Align* ac = al + b0;
+        SeqTerms Tc = T;  // (one chunk holds the whole batch: the terms are batch-interleaved)
         const dim3 grid(MNBLK, nb);
         if (j.align_way == 1) {
             (void)hipMemsetAsync(hc, 0, sizeof(uint32_t) * 2 * HBINS * nb, s);
@@ -491,12 +705,25 @@ void launch_metrics(hipStream_t s, const MetricsJob& j, void* ws, pf_metrics* ou
                 hipLaunchKernelGGL(k_med_hist, grid, dim3(MB), 0, s, c, pass, sc, hc);
                 hipLaunchKernelGGL(k_med_scan, dim3(2 * nb), dim3(MB), 0, s, pass, hc, sc);
             }
-        } else if (j.align_way == 2) {
+        } else if (j.align_way == 2 && !j.sequential) {
             hipLaunchKernelGGL(k_ls_sums, grid, dim3(MB), 0, s, c, pc);
         }
-        hipLaunchKernelGGL(k_align, dim3(nb), dim3(64), 0, s, j.align_way, sc, pc, MNBLK, ac);
+        if (j.align_way == 2 && j.sequential) {  // least squares in the reference's float order
+            hipLaunchKernelGGL(k_seq_terms<true>, grid, dim3(MB), 0, s, c, 0, (const Align*)nullptr,
+                               Tc, band);
+            hipLaunchKernelGGL(k_ls_seq, dim3((nb + 63) / 64), dim3(64), 0, s, Tc, band, nb, ac);
+        } else {
+            hipLaunchKernelGGL(k_align, dim3(nb), dim3(64), 0, s, j.align_way, sc, pc, MNBLK, ac);
+        }
         hipLaunchKernelGGL(k_err_sums, grid, dim3(MB), 0, s, c, j.align_way, ac, pc);
-        hipLaunchKernelGGL(k_err_final, dim3(nb), dim3(MB), 0, s, pc, MNBLK, ac, out + b0);
+        if (j.sequential) {
+            hipLaunchKernelGGL(k_seq_terms<false>, grid, dim3(MB), 0, s, c, j.align_way, ac, Tc,
+                               band);
+            hipLaunchKernelGGL(k_err_seq, dim3((nb + 63) / 64), dim3(64), 0, s, Tc, band, nb, pc,
+                               MNBLK, ac, out + b0);
+        } else {
+            hipLaunchKernelGGL(k_err_final, dim3(nb), dim3(MB), 0, s, pc, MNBLK, ac, out + b0);
+        }
     }
 }
 

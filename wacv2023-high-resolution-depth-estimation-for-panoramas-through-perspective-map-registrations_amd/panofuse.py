@@ -26,8 +26,9 @@ EXPORTS = [
     "pf_probe_taps", "pf_profile_enable", "pf_profile_read", "pf_error_metrics",
     "pf_depth_transform", "pf_register_joint", "pf_set_solver", "pf_fuse_normalize",
     "pf_fuse_border", "pf_fuse_band_plan", "pf_fuse_band_pass", "pf_fuse_multicover",
-    "pf_fuse_multicover_patch", "pf_solve_smoothing",
+    "pf_fuse_multicover_patch", "pf_solve_smoothing", "pf_set_metrics_order",
 ]
+METRICS_ORDERS = {"tree": 0, "sequential": 1}  # PF_METRICS_*; "sequential" = the reference's
 SOLVERS = {"normal": 0, "lm": 1}  # PF_SOLVER_*; "lm" = the reference's Ceres LM (default)
 
 STAGES = ["warp", "register", "seed", "targets", "jacobi", "quantize", "metrics"]
@@ -78,6 +79,7 @@ def load():
     L.pf_warp_depth.argtypes = [vp, vp, ip, ip, ip, vp, vp]
     L.pf_warp_rgb.argtypes = [vp, vp, ip, ip, ip, vp]
     L.pf_solve_smoothing.argtypes = [vp, vp, vp, ip, ip, ip, fp, fp, vp]
+    L.pf_set_metrics_order.argtypes = [vp, ip]
     L.pf_level_info.argtypes = [ip, ip, fp, fp, ip] + [C.POINTER(C.c_int)] * 6
     L.pf_fuse_partial.argtypes = [vp, vp, vp, ip, ip, ip, ip, fp, fp, ip, vp, vp]
     L.pf_fuse_seed.argtypes = [vp, vp, ip, ip, ip, vp, ip, ip, fp, fp, ip, vp]
@@ -214,6 +216,11 @@ class Fuser:
             raise ValueError("MergeDepthMaps output height is out_w/2")
         self._check(self.L.pf_merge(self.h, _ptr(emap), ew, eh, ec, _ptr(tiles), B, ow,
                                     float(zr[0]), float(zr[1]), _ptr(coeffs), _ptr(out)))
+
+    def set_metrics_order(self, order):
+        """"sequential" (default): the reference's float summation order, bit-exact; "tree":
+        fp64 partial sums (fast, means within 1e-5 of exact sums)."""
+        self._check(self.L.pf_set_metrics_order(self.h, METRICS_ORDERS[order]))
 
     def solve_smoothing(self, tiles, out, zr, coeffs=None):
         """SolveDepthBySmoothing (Depth.cpp:1773-1878) into out [B, out_h, out_w] (int16 view
