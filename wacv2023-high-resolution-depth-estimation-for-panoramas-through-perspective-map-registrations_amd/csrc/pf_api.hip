@@ -78,6 +78,9 @@ struct pf_ctx {
     DevBuf buf[3], lnorm, coeffs, lsum_ws, metrics_ws, reg_sums, reg_active;
     // SolveDepthBySmoothing (pf_smooth.hip): boxes, grid tables, per-pixel source and mask
     DevBuf sm_box, sm_cols, sm_rows, sm_src, sm_mask;
+    // level-0 seed index tables of the streaming Jacobi (run_jacobi), keyed by level and emap
+    DevBuf seed_ecol, seed_erow;
+    int seed_key[5] = {0, 0, 0, 0, 0};
     // stage profiling
     struct Span {
         int stage;
@@ -681,6 +684,8 @@ static int check_emap(pf_ctx* c, const float* emap, int ew, int eh, int ec)
 {
     if (!emap || ew < 2 || eh < 2 || ec < 1)
         return fail(c, PF_EINVAL, "bad emap %p %dx%dx%d", (const void*)emap, ew, eh, ec);
+    if ((long long)ew * eh * ec >= (1LL << 31))  // 32-bit emap indices (run_jacobi's seed tables)
+        return fail(c, PF_EINVAL, "emap %dx%dx%d too large", ew, eh, ec);
     return PF_OK;
 }
 
@@ -829,6 +834,31 @@ static int jacobi_tcap(const LevelDims& L)
     return cap;
 }
 
+// SRC_SEED passes: ValueAtCoord's index (emap_index) split into its column term x * ec and row
+// term y * ew * ec over the level's grid (the az / zen of grid_tables, then emap_index's fp64
+// expression), cached per (level size, emap size).  Returns PF_OK or the upload's error.
+static int seed_tables(pf_ctx* c, const LevelDims& L, int ew, int eh, int ec, JacobiPass& P)
+{
+    const int key[5] = {L.w, L.h, ew, eh, ec};
+    if (memcmp(key, c->seed_key, sizeof(key)) != 0) {
+        std::vector<int> ecol(L.w + 2), erow(L.h + 2);
+        for (int xx = -1; xx <= L.w; xx++) {
+            const float az = (float)((double)((float)xx / (float)(L.w - 1) * 2.0f) * PF_MYPI);
+            ecol[xx + 1] = (int)((double)az / (PF_MYPI * 2) * (double)(float)(ew - 1)) * ec;
+        }
+        for (int yy = -1; yy <= L.h; yy++) {
+            const float zen = (float)((double)((float)yy / (float)(L.h - 1)) * PF_MYPI);
+            erow[yy + 1] = (int)((double)zen / PF_MYPI * (double)(float)(eh - 1)) * ew * ec;
+        }
+        int rc;
+        if ((rc = upload(c, c->seed_ecol, ecol)) || (rc = upload(c, c->seed_erow, erow))) return rc;
+        memcpy(c->seed_key, key, sizeof(key));
+    }
+    P.ecol = (const int*)c->seed_ecol.p;
+    P.erow = (const int*)c->seed_erow.p;
+    return PF_OK;
+}
+
 static float* run_jacobi(pf_ctx* c, const LevelDims& L, int first, const float* emap, int ew,
                          int eh, int ec, long long estride, const GridCol* cols,
                          const GridRow* rows, const float* prev, long long pstride,
@@ -856,6 +886,7 @@ static float* run_jacobi(pf_ctx* c, const LevelDims& L, int first, const float* 
         }
     }
     JacobiPass P{};
+    if (first == 2 && emap && seed_tables(c, L, ew, eh, ec, P)) return nullptr;
     P.prev = prev; P.pstride = pstride;
     P.emap = emap; P.estride = estride; P.ew = ew; P.eh = eh; P.ec = ec;
     P.cols = cols; P.rows = rows;
@@ -1050,6 +1081,7 @@ static int fuse_range(pf_ctx* c, const float* emap, int ew, int eh, int ec, cons
                                  lc.full[l] ? (const float*)lc.hcol[l].p : nullptr);
                 t.set_launches(passes);  // k_jlag launches (rocprof's count for that kernel)
             }
+            if (!res) return PF_ENOMEM;  // the seed tables' upload failed (message in c->err)
         }
         prev = res;
     }
@@ -1458,6 +1490,7 @@ int pf_fuse_band_pass(pf_ctx* c, const float* emap, int ew, int eh, int ec, cons
                               4 * c->num_cu, tune.step_overhead, tune.lone_cycles, tune.c4_eff);
     const long long st = (long long)L.w * L.h;
     JacobiPass P{};
+    if (src_mode == 2 && (rc = seed_tables(c, L, ew, eh, ec, P))) return rc;
     P.prev = prev; P.pstride = 0;
     P.emap = emap; P.estride = 0; P.ew = ew; P.eh = eh; P.ec = ec;
     P.cols = (const GridCol*)lc.cols[level].p; P.rows = (const GridRow*)lc.rows[level].p;

@@ -149,6 +149,10 @@ struct JacobiPass {
     const float* prev; long long pstride;   // SRC_UPSAMPLE input (previous level, w/2 x h/2)
     const float* emap; long long estride;   // SRC_SEED input
     int ew, eh, ec, src_mode;
+    // SRC_SEED: ValueAtCoord's index split into its column and row terms (emap_index is
+    // separable): x * ec per virtual column xx at ecol[xx + 1], y * ew * ec per row yy at
+    // erow[yy + 1] (host-computed with the same fp64 expression, run_jacobi)
+    const int* ecol; const int* erow;
     const GridCol* cols; const GridRow* rows;
     const float* lnorm; long long lstride;
     float* dst; long long dstride;

@@ -198,9 +198,9 @@ struct JLag {
                     if constexpr (SRC == SRC_UPSAMPLE) {
                         v0 = v1 = prev[(long long)(Y >> 1) * (w >> 1) + (xr >> 1)];
                     } else if (Y >= P->h0 && Y <= P->h1) {  // level-0 seed (Depth.cpp:1442-1465)
-                        const float zen = P->rows[Y + 1].zen;
-                        v0 = emap[emap_index(P->cols[xr + 1].az, zen, P->ew, P->eh, P->ec)];
-                        v1 = emap[emap_index(P->cols[xr + 2].az, zen, P->ew, P->eh, P->ec)];
+                        const int ro = P->erow[Y + 1];
+                        v0 = emap[ro + P->ecol[xr + 1]];
+                        v1 = emap[ro + P->ecol[xr + 2]];
                     }
                 }
                 r.v[j] = v0;
@@ -694,9 +694,9 @@ struct JPipe {
                 if constexpr (SRC == SRC_UPSAMPLE) {
                     v0 = v1 = prev[(long long)(Y >> 1) * (w >> 1) + (xr >> 1)];
                 } else if (Y >= P->h0 && Y <= P->h1) {
-                    const float zen = P->rows[Y + 1].zen;
-                    v0 = emap[emap_index(P->cols[xr + 1].az, zen, P->ew, P->eh, P->ec)];
-                    v1 = emap[emap_index(P->cols[xr + 2].az, zen, P->ew, P->eh, P->ec)];
+                    const int ro = P->erow[Y + 1];
+                    v0 = emap[ro + P->ecol[xr + 1]];
+                    v1 = emap[ro + P->ecol[xr + 2]];
                 }
             }
             r.v[0] = v0;
