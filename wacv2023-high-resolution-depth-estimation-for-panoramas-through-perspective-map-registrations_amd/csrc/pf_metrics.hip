@@ -429,13 +429,11 @@ __global__ __launch_bounds__(MB) void k_err_final(const double* part, int nblk, 
 // panorama then adds them in sequence (k_ls_seq / k_err_seq).  A pixel that the reference skips
 // contributes exact zeros (x + 0 == x for every finite x >= 0), so the lanes need no masks; the
 // counts (n, nlog, delta fails) are integers and stay in the parallel pass (k_err_sums).
-struct SeqTerms {  // term of band pixel i = (y - h0) * w + x of panorama b at [i * nb + b]: the
-                  // lanes (panoramas) of the summing wave read one contiguous row per pixel
-    double* sq;    // ERR: (double)d * (double)d (exact);  LS: v1 * v1 and v0 * v1 (float pair)
-    double* lg2;   // ERR: (double)lg * (double)lg (exact), 0 where the log is skipped
-    float* ad;     // ERR: fabsf(d);   LS: v1
-    float* re;     // ERR: fabsf(d) / v0;   LS: v0
-    float* one;    // LS: 1 where compared, else 0
+struct SeqTerms {  // one float4 per band pixel i = (y - h0) * w + x of panorama b, at [i * nb + b]:
+                  // the lanes (panoramas) of the summing wave read one contiguous row per pixel
+    float4* t;    // ERR: {d, |d|, |d| / v0, lg} (d, lg = 0 where skipped; the double squares
+                  //      (double)d * (double)d and (double)lg * (double)lg are exact);
+                  // LS:  {v1 * v1, v1, v0 * v1, v0} (0 where skipped; v0 > 0 where compared)
 };
 
 template <bool LS>
@@ -453,78 +451,74 @@ __global__ __launch_bounds__(MB) void k_seq_terms(MArgs a, int align_way, const 
         const long long i = ((long long)(y - a.h0) * a.w + x0 + k) * nb + b;
         const float v0 = V0[k];
         float v1 = V1[k];
+        float4 o = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
         if (LS) {
-            float2 pr = make_float2(0.0f, 0.0f);
-            if (ok[k]) pr = make_float2(v1 * v1, v0 * v1);
-            reinterpret_cast<float2*>(T.sq)[i] = pr;
-            T.ad[i] = ok[k] ? v1 : 0.0f;
-            T.re[i] = ok[k] ? v0 : 0.0f;
-            T.one[i] = ok[k] ? 1.0f : 0.0f;
-            continue;
-        }
-        double sq = 0.0, lg2 = 0.0;
-        float ad = 0.0f, re = 0.0f;
-        if (ok[k]) {
+            if (ok[k]) o = make_float4(v1 * v1, v1, v0 * v1, v0);
+        } else if (ok[k]) {
             if (align_way == 1)
                 v1 *= A.shift;
             else if (align_way == 2)
                 v1 = v1 * A.s + A.o;
             const float d = v0 - v1;
-            sq = (double)d * (double)d;
-            ad = fabsf(d);
-            re = fabsf(d) / v0;
-            if ((double)v0 > 1e-4 && (double)v1 > 1e-4) {
-                const float lg = log10f(v0) - log10f(v1);
-                lg2 = (double)lg * (double)lg;
-            }
+            o.x = d;
+            o.y = fabsf(d);
+            o.z = fabsf(d) / v0;
+            if ((double)v0 > 1e-4 && (double)v1 > 1e-4) o.w = log10f(v0) - log10f(v1);
         }
-        T.sq[i] = sq;
-        T.lg2[i] = lg2;
-        T.ad[i] = ad;
-        T.re[i] = re;
+        T.t[i] = o;
       }
     }
 }
 
-// Depth.cpp:2119-2134 in the reference's float order, one lane per panorama.  The loads of a
-// block of PU pixels are issued before its additions (they do not depend on the accumulators),
-// so the lone summing wave keeps PU rows in flight.
-constexpr int PU = 16;
+// The sequential lanes: blocks of PU pixels, the next block's loads in flight while one block
+// is added (the additions do not depend on the loads of later pixels).
+constexpr int PU = 32;
+template <class F>
+__device__ __forceinline__ void seq_walk(const float4* t, long long band, int batch, int b, F add)
+{
+    const long long nfull = band / PU;
+    float4 A[PU], B[PU];
+    auto load = [&](float4* X, long long k) {
+#pragma unroll
+        for (int u = 0; u < PU; ++u) X[u] = t[(k * PU + u) * batch + b];
+    };
+    auto run = [&](const float4* X) {
+#pragma unroll
+        for (int u = 0; u < PU; ++u) add(X[u]);
+    };
+    if (nfull > 0) {
+        load(A, 0);
+        long long k = 1;
+        for (; k + 1 < nfull; k += 2) {
+            load(B, k);
+            run(A);
+            load(A, k + 1);
+            run(B);
+        }
+        if (k < nfull) {
+            load(B, k);
+            run(A);
+            run(B);
+        } else {
+            run(A);
+        }
+    }
+    for (long long i = nfull * PU; i < band; ++i) add(t[i * batch + b]);
+}
+
+// Depth.cpp:2119-2134 in the reference's float order, one lane per panorama.
 __global__ __launch_bounds__(64) void k_ls_seq(SeqTerms T, long long band, int batch, Align* al)
 {
     const int b = blockIdx.x * 64 + threadIdx.x;
     if (b >= batch) return;
-    const float2* sq = reinterpret_cast<const float2*>(T.sq);
     float a00 = 0, a01 = 0, a11 = 0, b0 = 0, b1 = 0;
-    long long i = 0;
-    for (; i + PU <= band; i += PU) {
-        float2 p[PU];
-        float v1[PU], v0[PU], one[PU];
-#pragma unroll
-        for (int u = 0; u < PU; ++u) {
-            const long long o = (i + u) * batch + b;
-            p[u] = sq[o];
-            v1[u] = T.ad[o];
-            v0[u] = T.re[o];
-            one[u] = T.one[o];
-        }
-#pragma unroll
-        for (int u = 0; u < PU; ++u) {
-            a00 += p[u].x;
-            a01 += v1[u];
-            a11 += one[u];
-            b0 += p[u].y;
-            b1 += v0[u];
-        }
-    }
-    for (; i < band; ++i) {
-        const long long o = i * batch + b;
-        a00 += sq[o].x;
-        a01 += T.ad[o];
-        a11 += T.one[o];
-        b0 += sq[o].y;
-        b1 += T.re[o];
-    }
+    seq_walk(T.t, band, batch, b, [&](const float4& v) {
+        a00 += v.x;
+        a01 += v.y;
+        a11 += v.w > 0.0f ? 1.0f : 0.0f;
+        b0 += v.z;
+        b1 += v.w;
+    });
     const float det = a00 * a11 - a01 * a01;
     Align A{1.0f, 0.0f, 0.0f, 0.0f, 0.0f};
     A.s = (a11 * b0 - a01 * b1) / det;
@@ -541,58 +535,12 @@ __global__ __launch_bounds__(64) void k_err_seq(SeqTerms T, long long band, int 
     const int b = blockIdx.x * 64 + threadIdx.x;
     if (b >= batch) return;
     float mse = 0, mae = 0, mre = 0, mselog = 0;
-    // software pipeline: the loads of block k+1 are in flight while block k is added
-    struct Blk {
-        double sq[PU], lg2[PU];
-        float ad[PU], re[PU];
-    };
-    auto load = [&](Blk& B, long long i) {
-#pragma unroll
-        for (int u = 0; u < PU; ++u) {
-            const long long o = (i + u) * batch + b;
-            B.sq[u] = T.sq[o];
-            B.lg2[u] = T.lg2[o];
-            B.ad[u] = T.ad[o];
-            B.re[u] = T.re[o];
-        }
-    };
-    auto add = [&](const Blk& B) {
-#pragma unroll
-        for (int u = 0; u < PU; ++u) {
-            mse = (float)((double)mse + B.sq[u]);
-            mae += B.ad[u];
-            mre += B.re[u];
-            mselog = (float)((double)mselog + B.lg2[u]);
-        }
-    };
-    const long long nfull = band / PU;
-    long long i = 0;
-    if (nfull > 0) {
-        Blk A, B;
-        load(A, 0);
-        long long k = 1;
-        for (; k + 1 < nfull; k += 2) {
-            load(B, k * PU);
-            add(A);
-            load(A, (k + 1) * PU);
-            add(B);
-        }
-        if (k < nfull) {
-            load(B, k * PU);
-            add(A);
-            add(B);
-        } else {
-            add(A);
-        }
-        i = nfull * PU;
-    }
-    for (; i < band; ++i) {
-        const long long o = i * batch + b;
-        mse = (float)((double)mse + T.sq[o]);
-        mae += T.ad[o];
-        mre += T.re[o];
-        mselog = (float)((double)mselog + T.lg2[o]);
-    }
+    seq_walk(T.t, band, batch, b, [&](const float4& v) {
+        mse = (float)((double)mse + (double)v.x * (double)v.x);  // += pow(val0 - val1, 2)
+        mae += v.y;
+        mre += v.z;
+        mselog = (float)((double)mselog + (double)v.w * (double)v.w);
+    });
     double cnt[5] = {0, 0, 0, 0, 0};  // n, nlog, fail1..3: integer-valued, order-free
     for (int i = 0; i < nblk; ++i)
         for (int k = 0; k < 5; ++k) cnt[k] += part[((long long)b * nblk + i) * (NSUM + 1) + 4 + k];
@@ -621,8 +569,8 @@ __global__ __launch_bounds__(64) void k_err_seq(SeqTerms T, long long band, int 
 }  // namespace
 
 static size_t seq_bytes(long long band, int batch)
-{  // SeqTerms: sq + lg2 (8 B each), ad + re + one (4 B each) per band pixel and panorama
-    return (size_t)band * batch * (8 + 8 + 4 + 4 + 4) + 5 * 256;
+{  // SeqTerms: one float4 per band pixel and panorama
+    return (size_t)band * batch * sizeof(float4) + 256;
 }
 
 size_t metrics_workspace_bytes(int batch, long long band, bool sequential)
@@ -675,11 +623,7 @@ void launch_metrics(hipStream_t s, const MetricsJob& j, void* ws, pf_metrics* ou
     const long long band = (long long)(j.h1 - j.h0 + 1) * j.w;
     SeqTerms T{};
     if (j.sequential) {
-        T.sq = (double*)carve(sizeof(double) * band * j.batch);
-        T.lg2 = (double*)carve(sizeof(double) * band * j.batch);
-        T.ad = (float*)carve(sizeof(float) * band * j.batch);
-        T.re = (float*)carve(sizeof(float) * band * j.batch);
-        T.one = (float*)carve(sizeof(float) * band * j.batch);
+        T.t = (float4*)carve(sizeof(float4) * band * j.batch);
     }
 
     // Panoramas in chunks (all at once by default).  Chunks sized to the 256 MB Infinity Cache

@@ -142,7 +142,10 @@ __global__ void __launch_bounds__(256) k_targets_map(const TileGeom* __restrict_
 static constexpr int kTPW = 64, kTPH = PF_TGT_PH;                // patch of kTPW x kTPH pixels
 static constexpr int kTPP = kTPW * kTPH / 256;                   // pixels per thread
 static constexpr int kTGW = kTPW + 2, kTGH = kTPH + 2, kTG = kTGW * kTGH;  // grid points + ring
-static constexpr int kTNB = 8;                                   // panoramas per block
+#ifndef PF_TGT_NB
+#define PF_TGT_NB 8
+#endif
+static constexpr int kTNB = PF_TGT_NB;                           // panoramas per block
 
 __device__ __forceinline__ bool box_meets(const TileBox& bx, int X0, int X1, int Y0, int Y1)
 {  // does the box (X from x0 stepping xs, stopping before x1; rows y0..y1) meet [X0,X1]x[Y0,Y1]
