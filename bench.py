@@ -51,6 +51,10 @@ def parse():
     ap.add_argument("--prof-steps", type=int, default=2,
                     help="extra untimed steps with the per-stage hipEvent timers on (roofline)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--pipeline", type=int, default=1,
+                    help="1: software-pipelined steps -- the warp of batch k+1 (second stream) "
+                         "runs while batch k is registered and fused; every step still warps, "
+                         "registers and fuses one whole batch")
     ap.add_argument("--stand-in", action="store_true",
                     help="test hook (tests/test_bench_dist.py): the launcher, seeding and timing "
                          "path with a CPU stand-in step over gloo; no GPU is touched")
@@ -320,7 +324,37 @@ def main():
         fz.warp_depth(gt, tiles, resp)
         fz.merge(emap, tiles, out, zr, coeffs=coeffs)
 
-    _, elapsed = timed_steps(step, torch.cuda.synchronize, args, world, dist, dev)
+    if args.pipeline:
+        # two tile buffers: step k fuses buffer k%2 (warped during step k-1) on the main stream
+        # while the second stream warps batch k+1 into the other buffer, once the fusion that
+        # last read it (step k-1) is done.  Same work per step: one warp, one merge.
+        sw = torch.cuda.Stream(dev, priority=int(os.environ.get("PF_WARP_PRIO", "0")))
+        fw = panofuse.Fuser(local, stream=sw)
+        fw.set_tiles(lay)
+        bufs = [tiles, torch.empty_like(tiles)]
+        main = torch.cuda.current_stream(dev)
+        st = {"k": 0, "warped": None, "fused": None}
+        fw.warp_depth(gt, bufs[0], resp)
+        st["warped"] = torch.cuda.Event()
+        st["warped"].record(sw)
+
+        def pstep():
+            k = st["k"]
+            cur, nxt = bufs[k % 2], bufs[(k + 1) % 2]
+            main.wait_event(st["warped"])
+            fz.merge(emap, cur, out, zr, coeffs=coeffs)
+            fused = torch.cuda.Event()
+            fused.record(main)
+            if st["fused"] is not None:
+                sw.wait_event(st["fused"])  # the fusion of step k-1 read nxt
+            fw.warp_depth(gt, nxt, resp)
+            warped = torch.cuda.Event()
+            warped.record(sw)
+            st.update(k=k + 1, warped=warped, fused=fused)
+
+        _, elapsed = timed_steps(pstep, torch.cuda.synchronize, args, world, dist, dev)
+    else:
+        _, elapsed = timed_steps(step, torch.cuda.synchronize, args, world, dist, dev)
     # Per-kernel roofline: the same steps again with the library's hipEvent stage timers on
     # (recorded on the stream the kernels run on).  With the timers on, the library runs each
     # batch unsplit (no half-batch stream overlap), so every stage's time is its own.
@@ -376,7 +410,10 @@ def main():
             "config": {"workload": f"C3/C4: {B} panoramas per GPU per step, 2048x1024 output, "
                                    f"20 tiles of 512x512 (5x4 layout), 512x256 baseline",
                        "global_batch": B * world, "out": "2048x1024", "tiles": "20x512x512",
-                       "parallelism": f"dp{world} (panorama sharding, no collective)"},
+                       "parallelism": f"dp{world} (panorama sharding, no collective)",
+                       "pipeline": ("warp of batch k+1 on a second stream during the "
+                                    "registration + fusion of batch k" if args.pipeline
+                                    else "off")},
             # Headline: the dominant kernel (k_jlag, the temporally blocked Jacobi) against its
             # real roof, VALU issue: algorithmic FLOP = 14 fp32 operations per pixel-update as the
             # reference writes them (Depth.cpp:1680-1717: 4 mul + 4 add for Lcur; sub, mul, add;
