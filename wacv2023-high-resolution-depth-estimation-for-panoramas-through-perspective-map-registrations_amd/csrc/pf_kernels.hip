@@ -553,26 +553,44 @@ __global__ void __launch_bounds__(kRegLanes) k_register(
     double acc[kRegSums];
 #pragma unroll
     for (int k = 0; k < kRegSums; k++) acc[k] = 0.0;
-    for (int s = l; s < ns; s += kRegLanes) {
-        int r = s / ncol, c = s - r * ncol;
-        const GridCol cc = rcols[rg.col_off + c];
-        const GridRow rr = rrows[rg.row_off + r];
-        float x, y;
-        sph_to_2d(g, rr.sz, rr.cz, cc.ca, cc.sa, x, y);
-        if (x < 0) x = 0;
-        if (x > 1) x = 1;
-        if (y < 0) y = 0;
-        if (y > 1) y = 1;
-        double X = clamp_depth((double)tile[tile_index(g, x, y)]);
-        double Yv = clamp_depth((double)em[emap_index(cc.az, rr.zen, ew, eh, ec)]);
-        double X2 = X * X, X3 = X * X * X;
-        acc[0] = acc[0] + X3 * X3; acc[1] = acc[1] + X3 * X2; acc[2] = acc[2] + X3 * X;
-        acc[3] = acc[3] + X3;      acc[4] = acc[4] + X2 * X2; acc[5] = acc[5] + X2 * X;
-        acc[6] = acc[6] + X2;      acc[7] = acc[7] + X * X;   acc[8] = acc[8] + X;
-        acc[9] = acc[9] + 1.0;
-        acc[10] = acc[10] + X3 * Yv; acc[11] = acc[11] + X2 * Yv; acc[12] = acc[12] + X * Yv;
-        acc[13] = acc[13] + Yv;
-        acc[14] = acc[14] + Yv * Yv;
+    // The lane's samples l, l + 256, ... in groups of kRegU: the gathers of a group are issued
+    // together (they are independent), then added in sample order -- the same per-lane order as
+    // one sample per iteration, so the sums are unchanged bit for bit.
+    constexpr int kRegU = 4;
+    for (int s0 = l; s0 < ns; s0 += kRegU * kRegLanes) {
+        float tv[kRegU], ev[kRegU];
+#pragma unroll
+        for (int u = 0; u < kRegU; u++) {
+            const int s = s0 + u * kRegLanes;
+            tv[u] = 0.0f;
+            ev[u] = 0.0f;
+            if (s >= ns) continue;
+            int r = s / ncol, c = s - r * ncol;
+            const GridCol cc = rcols[rg.col_off + c];
+            const GridRow rr = rrows[rg.row_off + r];
+            float x, y;
+            sph_to_2d(g, rr.sz, rr.cz, cc.ca, cc.sa, x, y);
+            if (x < 0) x = 0;
+            if (x > 1) x = 1;
+            if (y < 0) y = 0;
+            if (y > 1) y = 1;
+            tv[u] = tile[tile_index(g, x, y)];
+            ev[u] = em[emap_index(cc.az, rr.zen, ew, eh, ec)];
+        }
+#pragma unroll
+        for (int u = 0; u < kRegU; u++) {
+            if (s0 + u * kRegLanes >= ns) break;
+            double X = clamp_depth((double)tv[u]);
+            double Yv = clamp_depth((double)ev[u]);
+            double X2 = X * X, X3 = X * X * X;
+            acc[0] = acc[0] + X3 * X3; acc[1] = acc[1] + X3 * X2; acc[2] = acc[2] + X3 * X;
+            acc[3] = acc[3] + X3;      acc[4] = acc[4] + X2 * X2; acc[5] = acc[5] + X2 * X;
+            acc[6] = acc[6] + X2;      acc[7] = acc[7] + X * X;   acc[8] = acc[8] + X;
+            acc[9] = acc[9] + 1.0;
+            acc[10] = acc[10] + X3 * Yv; acc[11] = acc[11] + X2 * Yv; acc[12] = acc[12] + X * Yv;
+            acc[13] = acc[13] + Yv;
+            acc[14] = acc[14] + Yv * Yv;
+        }
     }
 #pragma unroll
     for (int k = 0; k < kRegSums; k++) part[k][l] = acc[k];
