@@ -230,6 +230,42 @@ def rank_seeds(batch, rank):
     return pf_dist.panorama_block(batch, rank)
 
 
+def pipelined_step(fz, lay, local, dev, gt, emap, resp, tiles, out, coeffs, zr):
+    """The software-pipelined bench step: step k registers and fuses the tiles warped during step
+    k-1 (buffer k % 2) on the main stream while a second stream (its own context) warps batch k+1
+    into the other buffer, once the fusion that last read it (step k-1) is done.  Same work per
+    step as the serial one: one warp, one merge of the whole batch.  Primes buffer 0."""
+    import torch
+
+    import panofuse
+
+    sw = torch.cuda.Stream(dev, priority=int(os.environ.get("PF_WARP_PRIO", "0")))
+    fw = panofuse.Fuser(local, stream=sw)
+    fw.set_tiles(lay)
+    bufs = [tiles, torch.empty_like(tiles)]
+    main = torch.cuda.current_stream(dev)
+    st = {"k": 0, "warped": None, "fused": None, "fw": fw}
+    fw.warp_depth(gt, bufs[0], resp)
+    st["warped"] = torch.cuda.Event()
+    st["warped"].record(sw)
+
+    def pstep():
+        k = st["k"]
+        cur, nxt = bufs[k % 2], bufs[(k + 1) % 2]
+        main.wait_event(st["warped"])
+        fz.merge(emap, cur, out, zr, coeffs=coeffs)
+        fused = torch.cuda.Event()
+        fused.record(main)
+        if st["fused"] is not None:
+            sw.wait_event(st["fused"])  # the fusion of step k-1 read nxt
+        fw.warp_depth(gt, nxt, resp)
+        warped = torch.cuda.Event()
+        warped.record(sw)
+        st.update(k=k + 1, warped=warped, fused=fused)
+
+    return pstep
+
+
 def timed_steps(step, sync, args, world, dist, device=None):
     """W untimed warmup steps, then EXACTLY K steps bracketed by a barrier + device sync on both
     sides; returns (elapsed seconds of this rank, elapsed MAX over ranks)."""
@@ -325,33 +361,7 @@ def main():
         fz.merge(emap, tiles, out, zr, coeffs=coeffs)
 
     if args.pipeline:
-        # two tile buffers: step k fuses buffer k%2 (warped during step k-1) on the main stream
-        # while the second stream warps batch k+1 into the other buffer, once the fusion that
-        # last read it (step k-1) is done.  Same work per step: one warp, one merge.
-        sw = torch.cuda.Stream(dev, priority=int(os.environ.get("PF_WARP_PRIO", "0")))
-        fw = panofuse.Fuser(local, stream=sw)
-        fw.set_tiles(lay)
-        bufs = [tiles, torch.empty_like(tiles)]
-        main = torch.cuda.current_stream(dev)
-        st = {"k": 0, "warped": None, "fused": None}
-        fw.warp_depth(gt, bufs[0], resp)
-        st["warped"] = torch.cuda.Event()
-        st["warped"].record(sw)
-
-        def pstep():
-            k = st["k"]
-            cur, nxt = bufs[k % 2], bufs[(k + 1) % 2]
-            main.wait_event(st["warped"])
-            fz.merge(emap, cur, out, zr, coeffs=coeffs)
-            fused = torch.cuda.Event()
-            fused.record(main)
-            if st["fused"] is not None:
-                sw.wait_event(st["fused"])  # the fusion of step k-1 read nxt
-            fw.warp_depth(gt, nxt, resp)
-            warped = torch.cuda.Event()
-            warped.record(sw)
-            st.update(k=k + 1, warped=warped, fused=fused)
-
+        pstep = pipelined_step(fz, lay, local, dev, gt, emap, resp, tiles, out, coeffs, zr)
         _, elapsed = timed_steps(pstep, torch.cuda.synchronize, args, world, dist, dev)
     else:
         _, elapsed = timed_steps(step, torch.cuda.synchronize, args, world, dist, dev)
