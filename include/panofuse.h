@@ -221,7 +221,7 @@ int pf_error_metrics(pf_ctx* ctx, const float* gt, int gw, int gh, int gc, const
 /* Summation order of the means (mse, mae, mre, mselog) and of the least-squares sums:
  *   PF_METRICS_SEQUENTIAL (default) -- the reference's: row-major, float accumulators (mse and
  *     mselog through a double add, Depth.cpp:2119-2123, 2178-2186); bit-exact to it.  The
- *     per-pixel terms are computed in parallel, one lane per panorama adds them in order.
+ *     per-pixel terms are computed in parallel, one wave per panorama adds them in order.
  *   PF_METRICS_TREE -- fp64 partial sums in a fixed tree: deterministic, ~10x faster at large
  *     batches, means within 1e-5 relative of exact fp64 sums (not of the reference's floats). */
 #define PF_METRICS_TREE 0

@@ -429,26 +429,28 @@ __global__ __launch_bounds__(MB) void k_err_final(const double* part, int nblk, 
 // panorama then adds them in sequence (k_ls_seq / k_err_seq).  A pixel that the reference skips
 // contributes exact zeros (x + 0 == x for every finite x >= 0), so the lanes need no masks; the
 // counts (n, nlog, delta fails) are integers and stay in the parallel pass (k_err_sums).
-struct SeqTerms {  // one float4 per band pixel i = (y - h0) * w + x of panorama b, at [i * nb + b]:
-                  // the lanes (panoramas) of the summing wave read one contiguous row per pixel
-    float4* t;    // ERR: {d, |d|, |d| / v0, lg} (d, lg = 0 where skipped; the double squares
+struct SeqTerms {  // four planes per panorama: component k of band pixel i = (y - h0) * w + x of
+                  // panorama b at t[(b * 4 + k) * bandp + i] (bandp = band rounded up to 4)
+    float* t;     // ERR: {d, |d|, |d| / v0, lg} (d, lg = 0 where skipped; the double squares
                   //      (double)d * (double)d and (double)lg * (double)lg are exact);
                   // LS:  {v1 * v1, v1, v0 * v1, v0} (0 where skipped; v0 > 0 where compared)
+    long long bandp;
 };
 
 template <bool LS>
 __global__ __launch_bounds__(MB) void k_seq_terms(MArgs a, int align_way, const Align* al,
                                                   SeqTerms T, long long band)
 {
-    const int b = blockIdx.y, nb = gridDim.y;
+    const int b = blockIdx.y;
     const Align A = al ? al[b] : Align{1.0f, 0.0f, 0.0f, 0.0f, 0.0f};
     for (int y = a.h0 + blockIdx.x; y <= a.h1; y += gridDim.x)
     for (int x0 = 4 * threadIdx.x; x0 < a.w; x0 += 4 * MB) {
       float V0[4], V1[4];
       bool ok[4];
       eval4(a, b, x0, y, false, V0, V1, ok);
+      float* pl = T.t + (long long)b * 4 * T.bandp;
       for (int k = 0; k < 4 && x0 + k < a.w; ++k) {
-        const long long i = ((long long)(y - a.h0) * a.w + x0 + k) * nb + b;
+        const long long i = (long long)(y - a.h0) * a.w + x0 + k;
         const float v0 = V0[k];
         float v1 = V1[k];
         float4 o = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
@@ -465,60 +467,91 @@ __global__ __launch_bounds__(MB) void k_seq_terms(MArgs a, int align_way, const 
             o.z = fabsf(d) / v0;
             if ((double)v0 > 1e-4 && (double)v1 > 1e-4) o.w = log10f(v0) - log10f(v1);
         }
-        T.t[i] = o;
+        pl[i] = o.x;
+        pl[T.bandp + i] = o.y;
+        pl[2 * T.bandp + i] = o.z;
+        pl[3 * T.bandp + i] = o.w;
       }
     }
 }
 
-// The sequential lanes: blocks of PU pixels, the next block's loads in flight while one block
-// is added (the additions do not depend on the loads of later pixels).
-constexpr int PU = 32;
-template <class F>
-__device__ __forceinline__ void seq_walk(const float4* t, long long band, int batch, int b, F add)
+// The sequential sums: one wave per panorama.  The whole wave streams the panorama's term planes
+// through LDS in chunks of SCH pixels (16 B per lane per load, the next chunk's loads in flight
+// while the current one is added), and lane k adds plane sel[k] in row-major order into its own
+// float accumulator: acc = (float)((double)acc + term), term = (double)v * (double)v for the
+// squared planes (exact: 48 significant bits), v > 0 ? 1 : 0 for an indicator, (double)v else --
+// for a float term that is exactly the float sum acc + v (double rounding is innocuous for +).
+// The wave's critical path is then the dependent add chain of one pixel per step, not a load.
+constexpr int SCH = 1024, SPS = SCH + 16;  // LDS plane stride: the summing lanes' planes in
+                                          // different banks
+struct SeqLane {
+    int plane;  // 0..3
+    bool sq, ind;
+};
+__device__ __forceinline__ float seq_sum_wave(const float* __restrict__ pl, long long band,
+                                              long long bandp, SeqLane m, float (*lds)[4 * SPS])
 {
-    const long long nfull = band / PU;
-    float4 A[PU], B[PU];
-    auto load = [&](float4* X, long long k) {
+    const int lane = threadIdx.x;
+    constexpr int NM = SCH / 256;  // float4 loads per lane per plane and chunk
+    float4 R[4][NM];
+    auto load = [&](long long c) {
 #pragma unroll
-        for (int u = 0; u < PU; ++u) X[u] = t[(k * PU + u) * batch + b];
-    };
-    auto run = [&](const float4* X) {
+        for (int p = 0; p < 4; ++p)
 #pragma unroll
-        for (int u = 0; u < PU; ++u) add(X[u]);
+            for (int u = 0; u < NM; ++u) {
+                const long long off = c * SCH + u * 256 + lane * 4;  // < bandp => off + 3 < bandp
+                R[p][u] = off < bandp ? *reinterpret_cast<const float4*>(pl + p * bandp + off)
+                                      : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+            }
     };
-    if (nfull > 0) {
-        load(A, 0);
-        long long k = 1;
-        for (; k + 1 < nfull; k += 2) {
-            load(B, k);
-            run(A);
-            load(A, k + 1);
-            run(B);
+    auto put = [&](float* L) {
+#pragma unroll
+        for (int p = 0; p < 4; ++p)
+#pragma unroll
+            for (int u = 0; u < NM; ++u)
+                *reinterpret_cast<float4*>(L + p * SPS + u * 256 + lane * 4) = R[p][u];
+    };
+    float acc = 0.0f;
+    auto add = [&](float v) {
+        const double t = m.ind ? (v > 0.0f ? 1.0 : 0.0) : (m.sq ? (double)v * (double)v : (double)v);
+        acc = (float)((double)acc + t);
+    };
+    const long long nch = (band + SCH - 1) / SCH;
+    if (nch == 0) return acc;
+    load(0);
+    put(lds[0]);
+    __syncthreads();
+    for (long long c = 0; c < nch; ++c) {
+        if (c + 1 < nch) load(c + 1);
+        const float* L = lds[c & 1] + m.plane * SPS;
+        const int n = (int)(band - c * SCH < SCH ? band - c * SCH : SCH);
+        int j = 0;
+        for (; j + 4 <= n; j += 4) {
+            const float4 v = *reinterpret_cast<const float4*>(L + j);
+            add(v.x);
+            add(v.y);
+            add(v.z);
+            add(v.w);
         }
-        if (k < nfull) {
-            load(B, k);
-            run(A);
-            run(B);
-        } else {
-            run(A);
-        }
+        for (; j < n; ++j) add(L[j]);
+        if (c + 1 < nch) put(lds[(c + 1) & 1]);
+        __syncthreads();
     }
-    for (long long i = nfull * PU; i < band; ++i) add(t[i * batch + b]);
+    return acc;
 }
 
-// Depth.cpp:2119-2134 in the reference's float order, one lane per panorama.
-__global__ __launch_bounds__(64) void k_ls_seq(SeqTerms T, long long band, int batch, Align* al)
+// Depth.cpp:2119-2134 in the reference's float order, one wave per panorama: lanes 0..4 add
+// a00 (v1*v1), a01 (v1), a11 (count of compared pixels), b0 (v0*v1), b1 (v0).
+__global__ __launch_bounds__(64) void k_ls_seq(SeqTerms T, long long band, Align* al)
 {
-    const int b = blockIdx.x * 64 + threadIdx.x;
-    if (b >= batch) return;
-    float a00 = 0, a01 = 0, a11 = 0, b0 = 0, b1 = 0;
-    seq_walk(T.t, band, batch, b, [&](const float4& v) {
-        a00 += v.x;
-        a01 += v.y;
-        a11 += v.w > 0.0f ? 1.0f : 0.0f;
-        b0 += v.z;
-        b1 += v.w;
-    });
+    __shared__ float lds[2][4 * SPS];
+    const int b = blockIdx.x, lane = threadIdx.x;
+    static constexpr int plane[5] = {0, 1, 3, 2, 3};
+    const SeqLane m{lane < 5 ? plane[lane] : 0, false, lane == 2};
+    const float r = seq_sum_wave(T.t + (long long)b * 4 * T.bandp, band, T.bandp, m, lds);
+    const float a00 = __shfl(r, 0), a01 = __shfl(r, 1), a11 = __shfl(r, 2), b0 = __shfl(r, 3),
+                b1 = __shfl(r, 4);
+    if (lane != 0) return;
     const float det = a00 * a11 - a01 * a01;
     Align A{1.0f, 0.0f, 0.0f, 0.0f, 0.0f};
     A.s = (a11 * b0 - a01 * b1) / det;
@@ -526,51 +559,48 @@ __global__ __launch_bounds__(64) void k_ls_seq(SeqTerms T, long long band, int b
     al[b] = A;
 }
 
-// Depth.cpp:2178-2186, 2207-2210 in the reference's order, one lane per panorama; the integer
-// counts come from the parallel pass's part[] (exact in any order).
-__global__ __launch_bounds__(64) void k_err_seq(SeqTerms T, long long band, int batch,
-                                                const double* part, int nblk, const Align* al,
-                                                pf_metrics* out)
+// Depth.cpp:2178-2186, 2207-2210 in the reference's order, one wave per panorama: lanes 0..3
+// add mse (through a double), mae, mre, mselog (through a double); the integer counts come from
+// the parallel pass's part[] (exact in any order).
+__global__ __launch_bounds__(64) void k_err_seq(SeqTerms T, long long band, const double* part,
+                                                int nblk, const Align* al, pf_metrics* out)
 {
-    const int b = blockIdx.x * 64 + threadIdx.x;
-    if (b >= batch) return;
-    float mse = 0, mae = 0, mre = 0, mselog = 0;
-    seq_walk(T.t, band, batch, b, [&](const float4& v) {
-        mse = (float)((double)mse + (double)v.x * (double)v.x);  // += pow(val0 - val1, 2)
-        mae += v.y;
-        mre += v.z;
-        mselog = (float)((double)mselog + (double)v.w * (double)v.w);
-    });
+    __shared__ float lds[2][4 * SPS];
+    const int b = blockIdx.x, lane = threadIdx.x;
+    const SeqLane m{lane < 4 ? lane : 0, lane == 0 || lane == 3, false};
+    const float r = seq_sum_wave(T.t + (long long)b * 4 * T.bandp, band, T.bandp, m, lds);
+    const float mse = __shfl(r, 0), mae = __shfl(r, 1), mre = __shfl(r, 2), mselog = __shfl(r, 3);
+    if (lane != 0) return;
     double cnt[5] = {0, 0, 0, 0, 0};  // n, nlog, fail1..3: integer-valued, order-free
     for (int i = 0; i < nblk; ++i)
         for (int k = 0; k < 5; ++k) cnt[k] += part[((long long)b * nblk + i) * (NSUM + 1) + 4 + k];
     const int n = (int)cnt[0], nlog = (int)cnt[1];
     const int f1 = (int)cnt[2], f2 = (int)cnt[3], f3 = (int)cnt[4];
-    pf_metrics m;
-    m.mse = mse / (float)n;
-    m.mae = mae / (float)n;
-    m.mre = mre / (float)n;
-    m.mselog = mselog / (float)nlog;
-    m.delta1 = (float)(n - f1) / (float)n;
-    m.delta2 = (float)(n - f2) / (float)n;
-    m.delta3 = (float)(n - f3) / (float)n;
+    pf_metrics mt;
+    mt.mse = mse / (float)n;
+    mt.mae = mae / (float)n;
+    mt.mre = mre / (float)n;
+    mt.mselog = mselog / (float)nlog;
+    mt.delta1 = (float)(n - f1) / (float)n;
+    mt.delta2 = (float)(n - f2) / (float)n;
+    mt.delta3 = (float)(n - f3) / (float)n;
     const Align A = al[b];
-    m.median_shift = A.shift;
-    m.ls_s = A.s;
-    m.ls_o = A.o;
-    m.gt_median = A.gt_med;
-    m.given_median = A.gv_med;
-    m.n = n;
-    m.nlog = nlog;
-    m.reserved[0] = m.reserved[1] = 0;
-    out[b] = m;
+    mt.median_shift = A.shift;
+    mt.ls_s = A.s;
+    mt.ls_o = A.o;
+    mt.gt_median = A.gt_med;
+    mt.given_median = A.gv_med;
+    mt.n = n;
+    mt.nlog = nlog;
+    mt.reserved[0] = mt.reserved[1] = 0;
+    out[b] = mt;
 }
 
 }  // namespace
 
 static size_t seq_bytes(long long band, int batch)
-{  // SeqTerms: one float4 per band pixel and panorama
-    return (size_t)band * batch * sizeof(float4) + 256;
+{  // SeqTerms: four planes of band (rounded up to 4) floats per panorama
+    return (size_t)((band + 3) & ~3LL) * 4 * batch * sizeof(float) + 256;
 }
 
 size_t metrics_workspace_bytes(int batch, long long band, bool sequential)
@@ -623,7 +653,8 @@ void launch_metrics(hipStream_t s, const MetricsJob& j, void* ws, pf_metrics* ou
     const long long band = (long long)(j.h1 - j.h0 + 1) * j.w;
     SeqTerms T{};
     if (j.sequential) {
-        T.t = (float4*)carve(sizeof(float4) * band * j.batch);
+        T.bandp = (band + 3) & ~3LL;
+        T.t = (float*)carve(sizeof(float) * 4 * T.bandp * j.batch);
     }
 
     // Panoramas in chunks (all at once by default).  Chunks sized to the 256 MB Infinity Cache
@@ -640,7 +671,8 @@ void launch_metrics(hipStream_t s, const MetricsJob& j, void* ws, pf_metrics* ou
         SelState* sc = st + 2 * b0;
         double* pc = part + (long long)b0 * (NSUM + 1) * MNBLK;
         Align* ac = al + b0;
-        SeqTerms Tc = T;  // (one chunk holds the whole batch: the terms are batch-interleaved)
+        SeqTerms Tc = T;
+        if (Tc.t) Tc.t += (long long)b0 * 4 * T.bandp;
         const dim3 grid(MNBLK, nb);
         if (j.align_way == 1) {
             (void)hipMemsetAsync(hc, 0, sizeof(uint32_t) * 2 * HBINS * nb, s);
@@ -655,7 +687,7 @@ void launch_metrics(hipStream_t s, const MetricsJob& j, void* ws, pf_metrics* ou
         if (j.align_way == 2 && j.sequential) {  // least squares in the reference's float order
             hipLaunchKernelGGL(k_seq_terms<true>, grid, dim3(MB), 0, s, c, 0, (const Align*)nullptr,
                                Tc, band);
-            hipLaunchKernelGGL(k_ls_seq, dim3((nb + 63) / 64), dim3(64), 0, s, Tc, band, nb, ac);
+            hipLaunchKernelGGL(k_ls_seq, dim3(nb), dim3(64), 0, s, Tc, band, ac);
         } else {
             hipLaunchKernelGGL(k_align, dim3(nb), dim3(64), 0, s, j.align_way, sc, pc, MNBLK, ac);
         }
@@ -663,8 +695,8 @@ void launch_metrics(hipStream_t s, const MetricsJob& j, void* ws, pf_metrics* ou
         if (j.sequential) {
             hipLaunchKernelGGL(k_seq_terms<false>, grid, dim3(MB), 0, s, c, j.align_way, ac, Tc,
                                band);
-            hipLaunchKernelGGL(k_err_seq, dim3((nb + 63) / 64), dim3(64), 0, s, Tc, band, nb, pc,
-                               MNBLK, ac, out + b0);
+            hipLaunchKernelGGL(k_err_seq, dim3(nb), dim3(64), 0, s, Tc, band, pc, MNBLK, ac,
+                               out + b0);
         } else {
             hipLaunchKernelGGL(k_err_final, dim3(nb), dim3(MB), 0, s, pc, MNBLK, ac, out + b0);
         }
