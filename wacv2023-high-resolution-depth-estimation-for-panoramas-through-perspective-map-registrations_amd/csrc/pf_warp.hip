@@ -33,7 +33,7 @@ static constexpr int kWB = 256;                         // threads per block
 static constexpr int kPatch = 32;                       // patch edge in tile pixels
 static constexpr int kPx = kPatch * kPatch / kWB;       // pixels per thread
 #ifndef PF_WARP_CAP
-#define PF_WARP_CAP 3072
+#define PF_WARP_CAP 4096
 #endif
 static constexpr int kCap = PF_WARP_CAP;                // LDS floats per staged footprint
 static constexpr int kSlots = kCap / kWB;               // staging loads per thread
