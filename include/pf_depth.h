@@ -28,9 +28,9 @@
  * SphericalToWorld, WorldToSpherical) are host fp32 code with the reference's Imath semantics
  * and glibc calls (csrc/pf_geom.hpp), bit-identical to it; the per-pixel path runs on the GPU.
  *
- * Not provided: progressive JPEG, SolveDisparityToDepth / SolveDepthToDepth2 /
- * SolveDepthBySmoothing (dead code in the reference's mode 0), ErrorCompare / ErrorLaplacian,
- * the triangulation/subdivision members (vertices, faces, subd_*: never used on the path).
+ * Not provided: SolveDisparityToDepth (declared, never defined: Depth.h:293) and
+ * SolveDepthToDepth2 (never called), ErrorCompare / ErrorLaplacian, the triangulation/subdivision
+ * members (vertices, faces, subd_*: never used on the path).
  */
 #pragma once
 
@@ -39,44 +39,113 @@
 #include <vector>
 
 #ifndef PF_DEPTH_NO_VEC
-/* Minimal stand-ins for the Imath vectors of ILMBase.h (Vec2f / Vec3f / Vec4f), indexable like
- * the reference uses them; Vec3f carries the Imath operations a caller of the window members
- * uses (ImathVec.h: dot, cross, length with lengthTiny, normalize by division). */
-struct Vec2f {
-    float x = 0, y = 0;
-    Vec2f() = default;
-    explicit Vec2f(float a) : x(a), y(a) {}
-    Vec2f(float a, float b) : x(a), y(b) {}
-    float& operator[](int i) { return (&x)[i]; }
-    float operator[](int i) const { return (&x)[i]; }
-    float length() const;
-};
-struct Vec3f {
-    float x = 0, y = 0, z = 0;
-    Vec3f() = default;
-    explicit Vec3f(float a) : x(a), y(a), z(a) {}
-    Vec3f(float a, float b, float c) : x(a), y(b), z(c) {}
-    float& operator[](int i) { return (&x)[i]; }
-    float operator[](int i) const { return (&x)[i]; }
-    Vec3f operator+(const Vec3f& v) const { return Vec3f(x + v.x, y + v.y, z + v.z); }
-    Vec3f operator-(const Vec3f& v) const { return Vec3f(x - v.x, y - v.y, z - v.z); }
-    Vec3f operator*(float s) const { return Vec3f(x * s, y * s, z * s); }
-    float dot(const Vec3f& v) const { return x * v.x + y * v.y + z * v.z; }
-    Vec3f cross(const Vec3f& v) const
+/* The vector types of the reference's ILMBase.h:14-16 (`typedef Imath::Vec4<float> Vec4f`, ...)
+ * for callers that do not include Imath.  They are declared as class templates in namespace
+ * Imath with Imath's layout (public x, y[, z[, w]] of T, ImathVec.h:63-66, 259-262, 563-566),
+ * so the entry points below mangle exactly as the reference's do
+ * (`DepthNamespace::MergeDepthMaps(..., std::vector<Imath::Vec4<float>>&, ..., Imath::Vec2<float>&,
+ * ...)`): libpanofuse_depth.so is built with these, and a caller that includes the real
+ * ILMBase.h first and then this header with -DPF_DEPTH_NO_VEC (as Main.cpp:13-15 includes
+ * ILMBase.h before Depth.h) links against the same symbols.  Like Imath's, the copy
+ * constructors are user-provided (ImathVec.h:96, 294, 507), which makes the types non-trivial for
+ * calls: a Vec2f returned by value travels through a hidden pointer in both builds, so the
+ * calling convention matches as well as the names.  Every member is inline (and hidden
+ * in the library: -fvisibility-inlines-hidden), so nothing here competes with the real Imath.
+ * The operations are the ones a caller of the window members uses, with Imath's arithmetic
+ * (ImathVec.h:1467-1486 dot/cross, :1631-1700 length with lengthTiny, normalize by division). */
+#include <cmath>
+#include <limits>
+namespace Imath {
+template <class T>
+class Vec2 {
+public:
+    T x, y;
+    Vec2() : x(0), y(0) {}
+    explicit Vec2(T a) : x(a), y(a) {}
+    Vec2(T a, T b) : x(a), y(b) {}
+    Vec2(const Vec2& v) : x(v.x), y(v.y) {}
+    const Vec2& operator=(const Vec2& v) { x = v.x; y = v.y; return *this; }
+    T& operator[](int i) { return (&x)[i]; }
+    const T& operator[](int i) const { return (&x)[i]; }
+    T dot(const Vec2& v) const { return x * v.x + y * v.y; }
+    T length() const
     {
-        return Vec3f(y * v.z - z * v.y, z * v.x - x * v.z, x * v.y - y * v.x);
+        const T l2 = dot(*this);
+        if (l2 < T(2) * std::numeric_limits<T>::min()) {  // lengthTiny
+            T ax = x >= T(0) ? x : -x, ay = y >= T(0) ? y : -y;
+            const T mx = ax < ay ? ay : ax;
+            if (mx == T(0)) return T(0);
+            ax /= mx;
+            ay /= mx;
+            return mx * std::sqrt(ax * ax + ay * ay);
+        }
+        return std::sqrt(l2);
     }
-    float length() const;
-    const Vec3f& normalize();  /* in place, returns *this (Imath) */
 };
-inline Vec3f operator*(float s, const Vec3f& v) { return Vec3f(s * v.x, s * v.y, s * v.z); }
-struct Vec4f {
-    float v[4] = {0, 0, 0, 0};
-    Vec4f() = default;
-    Vec4f(float a, float b, float c, float d) : v{a, b, c, d} {}
-    float& operator[](int i) { return v[i]; }
-    float operator[](int i) const { return v[i]; }
+template <class T>
+class Vec3 {
+public:
+    T x, y, z;
+    Vec3() : x(0), y(0), z(0) {}
+    explicit Vec3(T a) : x(a), y(a), z(a) {}
+    Vec3(T a, T b, T c) : x(a), y(b), z(c) {}
+    Vec3(const Vec3& v) : x(v.x), y(v.y), z(v.z) {}
+    const Vec3& operator=(const Vec3& v) { x = v.x; y = v.y; z = v.z; return *this; }
+    T& operator[](int i) { return (&x)[i]; }
+    const T& operator[](int i) const { return (&x)[i]; }
+    Vec3 operator+(const Vec3& v) const { return Vec3(x + v.x, y + v.y, z + v.z); }
+    Vec3 operator-(const Vec3& v) const { return Vec3(x - v.x, y - v.y, z - v.z); }
+    Vec3 operator*(T s) const { return Vec3(x * s, y * s, z * s); }
+    T dot(const Vec3& v) const { return x * v.x + y * v.y + z * v.z; }
+    Vec3 cross(const Vec3& v) const
+    {
+        return Vec3(y * v.z - z * v.y, z * v.x - x * v.z, x * v.y - y * v.x);
+    }
+    T length() const
+    {
+        const T l2 = dot(*this);
+        if (l2 < T(2) * std::numeric_limits<T>::min()) {  // lengthTiny
+            T ax = x >= T(0) ? x : -x, ay = y >= T(0) ? y : -y, az = z >= T(0) ? z : -z;
+            T mx = ax;
+            if (mx < ay) mx = ay;
+            if (mx < az) mx = az;
+            if (mx == T(0)) return T(0);
+            ax /= mx;
+            ay /= mx;
+            az /= mx;
+            return mx * std::sqrt(ax * ax + ay * ay + az * az);
+        }
+        return std::sqrt(l2);
+    }
+    const Vec3& normalize()  /* in place, returns *this */
+    {
+        const T l = length();
+        if (l != T(0)) {
+            x /= l;
+            y /= l;
+            z /= l;
+        }
+        return *this;
+    }
 };
+template <class T>
+inline Vec3<T> operator*(T s, const Vec3<T>& v) { return Vec3<T>(s * v.x, s * v.y, s * v.z); }
+template <class T>
+class Vec4 {
+public:
+    T x, y, z, w;
+    Vec4() : x(0), y(0), z(0), w(0) {}
+    explicit Vec4(T a) : x(a), y(a), z(a), w(a) {}
+    Vec4(T a, T b, T c, T d) : x(a), y(b), z(c), w(d) {}
+    Vec4(const Vec4& v) : x(v.x), y(v.y), z(v.z), w(v.w) {}
+    const Vec4& operator=(const Vec4& v) { x = v.x; y = v.y; z = v.z; w = v.w; return *this; }
+    T& operator[](int i) { return (&x)[i]; }
+    const T& operator[](int i) const { return (&x)[i]; }
+};
+}  // namespace Imath
+typedef Imath::Vec2<float> Vec2f;
+typedef Imath::Vec3<float> Vec3f;
+typedef Imath::Vec4<float> Vec4f;
 #endif
 
 #define PF_MYPI_D 3.14159265359          /* Basic.h:11 */

@@ -9,8 +9,21 @@
 //                               Depth2DepthTransform (Depth.cpp:794-805), then SolveDepthAll
 //                               (:913), then SolveDepthToDepth with several active maps, then
 //                               SolveDepthBySmoothing (:1773-1878) on the transformed maps
+//   facade_check merge IN OUT   MergeDepthMaps on files, called as Main.cpp:592-594 calls it
+//                               (global FOV/range vectors, g_zenith_range, timing outputs)
 //
 // IN/OUT are flat little-endian binaries written/read by tests/test_facade.py.
+//
+// Built twice: with the header's own Imath-layout vectors (bin/pf_facade_check), and with
+// -DPF_FACADE_IMATH against the reference's ILMBase.h + IlmBase 2.2 headers
+// (oracle/_ref/pf_facade_check_imath, only where /root/reference exists): that build includes
+// ILMBase.h first and pf_depth.h with PF_DEPTH_NO_VEC, exactly as Main.cpp:13-15 includes
+// ILMBase.h before Depth.h, so it only links if the library's exported signatures carry
+// Imath::Vec2<float> / Imath::Vec4<float>.
+#ifdef PF_FACADE_IMATH
+#include "ILMBase.h"
+#define PF_DEPTH_NO_VEC
+#endif
 #include "../../include/pf_depth.h"
 
 #include <cstdio>
@@ -123,7 +136,7 @@ int solve(Reader& r, Writer& w)
         Vec4f abcd;
         if (!SolveDepthToDepth(emap, pmaps, actives, zr, abcd)) return 2;
         pmaps[p].Depth2DepthTransform(abcd);
-        w.put(abcd.v, 4);
+        w.put(abcd.x); w.put(abcd.y); w.put(abcd.z); w.put(abcd.w);
     }
     for (auto& p : pmaps) w.put(p.data, (size_t)tw * th);
     int out_h = out_w / 2;
@@ -135,10 +148,55 @@ int solve(Reader& r, Writer& w)
     for (int a : act) actives[a] = true;
     Vec4f joint;
     if (!SolveDepthToDepth(emap, pmaps, actives, zr, joint)) return 4;
-    w.put(joint.v, 4);
+    w.put(joint.x); w.put(joint.y); w.put(joint.z); w.put(joint.w);
     // the alternate solver on the same (transformed) maps (Depth.h:309)
     if (!SolveDepthBySmoothing(pmaps, out.data(), out_w, out_h, zr)) return 5;
     w.put(out.data(), out.size());
+    return 0;
+}
+
+// Main.cpp:32-33 keeps the layout in globals and passes them by reference (:592-594)
+std::vector<Vec4f> g_cubemap_FOVs;
+std::vector<Vec4f> g_cubemap_ranges;
+
+std::string get_str(Reader& r)
+{
+    const int n = r.get<int>();
+    std::string s(n, '\0');
+    r.get(&s[0], n);
+    return s;
+}
+
+int merge(Reader& r, Writer& w)
+{
+    const int n = r.get<int>();
+    for (int i = 0; i < n; i++) {
+        float fov[4], rng[4];
+        r.get(fov, 4);
+        r.get(rng, 4);
+        g_cubemap_FOVs.push_back(Vec4f(fov[0], fov[1], fov[2], fov[3]));
+        g_cubemap_ranges.push_back(Vec4f(rng[0], rng[1], rng[2], rng[3]));
+    }
+    const int out_width = r.get<int>();
+    std::string fn_baseline = get_str(r), output_filename = get_str(r), fn_gt = get_str(r);
+    std::vector<std::string> pmap_fns;
+    for (int i = 0; i < n; i++) pmap_fns.push_back(get_str(r));
+    DepthNamespace::Metrics metrics_aligned;
+    int time_Reg = 0, time_Laplacian = 0;
+    if (!DepthNamespace::MergeDepthMaps(fn_baseline, pmap_fns, output_filename, g_cubemap_FOVs,
+                                        g_cubemap_ranges, out_width, g_zenith_range, &fn_gt,
+                                        &metrics_aligned, &time_Reg, &time_Laplacian))
+        return 6;
+    const float m[14] = {metrics_aligned.mse_given,    metrics_aligned.mse_result,
+                         metrics_aligned.mae_given,    metrics_aligned.mae_result,
+                         metrics_aligned.mre_given,    metrics_aligned.mre_result,
+                         metrics_aligned.mselog_given, metrics_aligned.mselog_result,
+                         metrics_aligned.delta1_given, metrics_aligned.delta1_result,
+                         metrics_aligned.delta2_given, metrics_aligned.delta2_result,
+                         metrics_aligned.delta3_given, metrics_aligned.delta3_result};
+    w.put(m, 14);
+    w.put(time_Reg);
+    w.put(time_Laplacian);
     return 0;
 }
 }  // namespace
@@ -146,7 +204,7 @@ int solve(Reader& r, Writer& w)
 int main(int argc, char** argv)
 {
     if (argc != 4) {
-        fprintf(stderr, "usage: %s geom|solve IN OUT\n", argv[0]);
+        fprintf(stderr, "usage: %s geom|solve|merge IN OUT\n", argv[0]);
         return 1;
     }
     FILE* fi = fopen(argv[2], "rb");
@@ -156,7 +214,8 @@ int main(int argc, char** argv)
     Writer w{fo};
     int rc = 1;
     try {
-        rc = std::string(argv[1]) == "geom" ? geom(r, w) : solve(r, w);
+        const std::string mode = argv[1];
+        rc = mode == "geom" ? geom(r, w) : mode == "merge" ? merge(r, w) : solve(r, w);
     } catch (const std::string& e) {
         fprintf(stderr, "%s\n", e.c_str());
         rc = 1;

@@ -24,15 +24,28 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 PKG = os.path.join(ROOT, "wacv2023-high-resolution-depth-estimation-for-panoramas-through-"
                          "perspective-map-registrations_amd")
 BIN = os.path.join(PKG, "bin", "pf_facade_check")
+# The same caller built against the reference's own ILMBase.h (IlmBase 2.2 Imath::Vec2/Vec4<float>)
+# by oracle/Makefile where /root/reference exists; it travels to the GPU box in oracle/_ref/.
+IMATH_BIN = os.path.join(ROOT, "oracle", "_ref", "pf_facade_check_imath")
+CALLERS = ["standin", "imath"]
 ZR = PL.ZENITH_RANGE
 
 
-def _run(mode, blob, tmp_path):
+def _bin(caller):
+    if caller == "imath":
+        if not os.path.exists(IMATH_BIN):
+            pytest.skip("no Imath-built caller (needs /root/reference at build time)")
+        return IMATH_BIN
     if not os.path.exists(BIN):
         pytest.fail(f"{BIN} not built (make -C {PKG})")
+    return BIN
+
+
+def _run(mode, blob, tmp_path, caller="standin"):
+    exe = _bin(caller)
     fi, fo = tmp_path / "in.bin", tmp_path / "out.bin"
     fi.write_bytes(blob)
-    r = subprocess.run([BIN, mode, str(fi), str(fo)], capture_output=True, text=True,
+    r = subprocess.run([exe, mode, str(fi), str(fo)], capture_output=True, text=True,
                        timeout=300)
     assert r.returncode == 0, r.stdout + r.stderr
     return np.fromfile(fo, dtype=np.uint8)
@@ -47,8 +60,31 @@ def _layout_blob(lay):
     return b"".join(parts)
 
 
+def test_imath_caller_links_reference_signatures():
+    """The library's exported entry points mangle the reference's Imath types (Depth.h:286-309
+    as seen through ILMBase.h:14-16), so a Main.cpp-style caller links unchanged."""
+    r = subprocess.run(["nm", "-DC", os.path.join(PKG, "lib", "libpanofuse_depth.so")],
+                       capture_output=True, text=True, check=True)
+    exported = [ln for ln in r.stdout.splitlines() if " T " in ln]
+    for fn, types in (("MergeDepthMaps", ("std::vector<Imath::Vec4<float>", "Imath::Vec2<float>&")),
+                      ("SolveDepthToDepth", ("Imath::Vec2<float>&", "Imath::Vec4<float>&")),
+                      ("SolveDepthAll", ("Imath::Vec2<float>&",)),
+                      ("SphericalToWorld", ("",)), ("WorldToSpherical", ("Imath::Vec3<float>&",))):
+        sig = [ln for ln in exported if f"DepthNamespace::{fn}(" in ln]
+        assert sig, fn
+        for t in types:
+            assert t in sig[0], (fn, sig[0])
+    # no Imath member is exported (they are inline and hidden)
+    assert not [ln for ln in exported if "<float>::" in ln and " Imath::Vec" in ln]
+    if os.path.exists(IMATH_BIN):
+        und = subprocess.run(["nm", "-uC", IMATH_BIN], capture_output=True, text=True,
+                             check=True).stdout
+        assert "DepthNamespace::MergeDepthMaps(" in und and "Imath::Vec4<float>" in und
+
+
+@pytest.mark.parametrize("caller", CALLERS)
 @pytest.mark.parametrize("cfg", ["C1", "C2", "LERES"])
-def test_facade_geometry_bit_exact(cfg, tmp_path):
+def test_facade_geometry_bit_exact(cfg, caller, tmp_path):
     lay = PL.config_layout(cfg)
     tiles, _ = O.make_tiles(lay)
     rs = np.random.RandomState(7)
@@ -56,7 +92,7 @@ def test_facade_geometry_bit_exact(cfg, tmp_path):
     sp = np.stack([rs.uniform(0, 2 * np.pi, 96), rs.uniform(0.05, 3.09, 96)], 1).astype(np.float32)
     blob = (np.int32(lay.ntiles).tobytes() + _layout_blob(lay) + np.int32(len(xy)).tobytes()
             + xy.tobytes() + np.int32(len(sp)).tobytes() + sp.tobytes())
-    out = _run("geom", blob, tmp_path).view(np.float32)
+    out = _run("geom", blob, tmp_path, caller).view(np.float32)
     per_tile = 21 + 2 * len(xy) + 3 * len(sp)
     L = O.lib()
     import ctypes as C
@@ -93,7 +129,8 @@ def test_facade_geometry_bit_exact(cfg, tmp_path):
 
 
 @pytest.mark.gpu
-def test_facade_solvers_bit_exact(tmp_path):
+@pytest.mark.parametrize("caller", CALLERS)
+def test_facade_solvers_bit_exact(caller, tmp_path):
     lay = PL.config_layout("C1")
     tiles, total = O.make_tiles(lay)
     seeds = pf_synth.seeds_for(1, 31337)
@@ -105,7 +142,7 @@ def test_facade_solvers_bit_exact(tmp_path):
             + np.array([128, 64], np.int32).tobytes() + emap.astype(np.float32).tobytes()
             + data.astype(np.float32).tobytes() + np.int32(512).tobytes()
             + np.array(ZR, np.float32).tobytes() + np.int32(len(act)).tobytes() + act.tobytes())
-    out = _run("solve", blob, tmp_path)
+    out = _run("solve", blob, tmp_path, caller)
     n = lay.ntiles
     abcd = out[:16 * n].view(np.float32).reshape(n, 4)
     off = 16 * n
@@ -135,3 +172,75 @@ def test_facade_solvers_bit_exact(tmp_path):
     c, _ = O.lm_fit(np.concatenate(xs), np.concatenate(ys))
     rel = np.abs(joint.astype(np.float64) - c) / np.maximum(np.abs(c), 1e-6)
     assert rel.max() <= 1e-5, (joint, c)
+
+
+def _png16(path, a):
+    import struct
+    import zlib
+    h, w = a.shape
+    raw = b"".join(b"\0" + a[y].astype(">u2").tobytes() for y in range(h))
+
+    def chunk(t, d):
+        return struct.pack(">I", len(d)) + t + d + struct.pack(">I", zlib.crc32(t + d))
+    path.write_bytes(b"\x89PNG\r\n\x1a\n" + chunk(b"IHDR", struct.pack(">IIBBBBB", w, h, 16, 0, 0, 0, 0))
+                     + chunk(b"IDAT", zlib.compress(raw, 1)) + chunk(b"IEND", b""))
+
+
+def _png16_read(path):
+    import struct
+    import zlib
+    d = path.read_bytes()
+    pos, idat = 8, b""
+    while pos < len(d):
+        n = struct.unpack(">I", d[pos:pos + 4])[0]
+        t, body = d[pos + 4:pos + 8], d[pos + 8:pos + 8 + n]
+        if t == b"IHDR":
+            w, h = struct.unpack(">II", body[:8])
+        elif t == b"IDAT":
+            idat += body
+        pos += 12 + n
+    raw = zlib.decompress(idat)
+    return np.frombuffer(b"".join(raw[y * (2 * w + 1) + 1:(y + 1) * (2 * w + 1)]
+                                  for y in range(h)), ">u2").reshape(h, w).astype(np.uint16)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("caller", CALLERS)
+def test_facade_merge_files_main_cpp_call(caller, tmp_path):
+    """MergeDepthMaps called exactly as Main.cpp:592-594 calls it (global std::vector<Vec4f>
+    layout, g_zenith_range, ground truth, Metrics and both timings) on 16-bit PNG files: the
+    written u16 panorama is bit-exact against the oracle's merge of the same decoded inputs."""
+    q16 = lambda a: (np.clip(a, 0, 1) * 65535.0 + 0.5).astype(np.uint16)  # noqa: E731
+    lay = PL.config_layout("C1")
+    tiles, total = O.make_tiles(lay)
+    seeds = pf_synth.seeds_for(1, 4242)
+    gt = q16(pf_synth.scene_depth(seeds, 512, 256)[0].numpy())
+    base = q16(pf_synth.baseline_emap(seeds, 128, 64)[0].numpy())
+    gt_f = gt.astype(np.float32) / np.float32(65535.0)
+    base_f = base.astype(np.float32) / np.float32(65535.0)
+    tq = q16(O.warp_depth(gt_f, tiles, total, O.responses(pf_synth.responses(seeds, lay.ntiles))))
+    fns, off = [], 0
+    for t in range(lay.ntiles):
+        fn = tmp_path / f"tile{t}.png"
+        _png16(fn, tq[off:off + 256 * 256].reshape(256, 256))
+        fns.append(str(fn))
+        off += 256 * 256
+    _png16(tmp_path / "base.png", base)
+    _png16(tmp_path / "gt.png", gt)
+    out_fn = tmp_path / "out.png"
+
+    def s(x):
+        b = str(x).encode()
+        return np.int32(len(b)).tobytes() + b
+    blob = (np.int32(lay.ntiles).tobytes() + _layout_blob(lay) + np.int32(512).tobytes()
+            + s(tmp_path / "base.png") + s(out_fn) + s(tmp_path / "gt.png")
+            + b"".join(s(f) for f in fns))
+    res = _run("merge", blob, tmp_path, caller)
+    metrics = res[:56].view(np.float32)
+    ref, _ = O.merge(base_f, tiles, tq.astype(np.float32) / np.float32(65535.0), 512, ZR)
+    got = _png16_read(out_fn)
+    assert got.shape == (256, 512)
+    assert int((got != ref).sum()) == 0
+    ref_r = O.error_metrics(gt_f, ref, ZR, 1, True)
+    assert metrics[1] == pytest.approx(ref_r["mse"], rel=1e-5, abs=1e-9)  # mse_result
+    assert metrics[3] == pytest.approx(ref_r["mae"], rel=1e-5, abs=1e-9)  # mae_result

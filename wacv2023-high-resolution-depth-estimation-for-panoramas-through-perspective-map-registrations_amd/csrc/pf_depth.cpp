@@ -27,18 +27,6 @@
 
 Vec2f g_zenith_range((float)PF_D2R(26), (float)PF_D2R(154));  // Depth.cpp:22
 
-// Imath operations of the vector stand-ins (ImathVec.h:1145-1180, 1631-1700)
-float Vec2f::length() const { return pfgeom::length2(x, y); }
-float Vec3f::length() const { return pfgeom::length(pfgeom::V3{x, y, z}); }
-const Vec3f& Vec3f::normalize()
-{
-    const pfgeom::V3 n = pfgeom::normalized(pfgeom::V3{x, y, z});
-    x = n.x;
-    y = n.y;
-    z = n.z;
-    return *this;
-}
-
 namespace {
 
 // One context per device, created on first use (the reference is single-threaded and not
