@@ -93,6 +93,18 @@ typedef struct pfo_lm_summary {
 } pfo_lm_summary;
 /* Fit of y ~ a x^3 + b x^2 + c x + d over the samples (FunctorDepth2Depth3 residuals),
  * sample-wise exactly as Ceres evaluates it. */
+/* The LM strategy state of levenberg_marquardt_strategy.cc (radius schedule and the diagonal
+ * regulariser), shared by both LM forms and exposed for the Ceres-unit-test pins. */
+typedef struct pfo_lm_strategy {
+    double radius, max_radius, decrease, min_diag, max_diag;
+    int reuse_diag;
+    double diag[4];
+} pfo_lm_strategy;
+void pfo_lms_init(pfo_lm_strategy* s, double initial_radius, double max_radius, double min_diag,
+                  double max_diag);
+void pfo_lms_accepted(pfo_lm_strategy* s, double step_quality);
+void pfo_lms_rejected(pfo_lm_strategy* s, double step_quality);
+void pfo_lms_regularizer(pfo_lm_strategy* s, const double* colsq, int n, double* D);
 int  pfo_lm_fit(const double* xs, const double* ys, int n, double coef[4], pfo_lm_summary* s);
 int  pfo_register_tile_lm(const pfo_tile* t, const float* tiles, const float* emap, int ew,
                           int eh, int ec, float zr0, float zr1, double* coef64, float* abcd,

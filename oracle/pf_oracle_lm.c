@@ -182,6 +182,54 @@ static double norm4(const double v[4])
     return sqrt(v[0] * v[0] + v[1] * v[1] + v[2] * v[2] + v[3] * v[3]);
 }
 
+/* The LM strategy's trust-region state (levenberg_marquardt_strategy.cc), factored out so it
+ * can be held to Ceres' own unit tests (levenberg_marquardt_strategy_test.cc:81-110 radius
+ * schedule, :113-160 diagonal handed to the linear solver; tests/test_oracle_lm.py). */
+void pfo_lms_init(pfo_lm_strategy* s, double initial_radius, double max_radius, double min_diag,
+                  double max_diag)
+{ /* levenberg_marquardt_strategy.cc:47-61 */
+    s->radius = initial_radius;
+    s->max_radius = max_radius;
+    s->decrease = 2.0;
+    s->min_diag = min_diag;
+    s->max_diag = max_diag;
+    s->reuse_diag = 0;
+    s->diag[0] = s->diag[1] = s->diag[2] = s->diag[3] = 0.0;
+}
+
+void pfo_lms_rejected(pfo_lm_strategy* s, double step_quality)
+{ /* :156-160 (the quality is unused); an invalid step is rejected with quality 0 */
+    (void)step_quality;
+    s->radius = s->radius / s->decrease;
+    s->decrease *= 2.0;
+    s->reuse_diag = 1;
+}
+
+static void lms_accepted(pfo_lm_strategy* s, double step_quality, int use_pow)
+{ /* :147-154: radius /= max(1/3, 1 - (2 q - 1)^3), capped at max_radius */
+    const double q = 2.0 * step_quality - 1.0;
+    const double f = 1.0 - (use_pow ? pow(q, 3) : q * q * q);
+    s->radius = s->radius / (f > 1.0 / 3.0 ? f : 1.0 / 3.0);
+    s->radius = s->radius < s->max_radius ? s->radius : s->max_radius;
+    s->decrease = 2.0;
+    s->reuse_diag = 0;
+}
+
+void pfo_lms_accepted(pfo_lm_strategy* s, double step_quality) { lms_accepted(s, step_quality, 1); }
+
+void pfo_lms_regularizer(pfo_lm_strategy* s, const double* colsq, int n, double* D)
+{ /* :75-88, :122: the diagonal = squared column norms of the (scaled) Jacobian clamped to
+   * [min_lm_diagonal, max_lm_diagonal], recomputed only after an accepted step;
+   * D = sqrt(diagonal / radius) goes to the linear solver as PerSolveOptions::D */
+    if (!s->reuse_diag)
+        for (int k = 0; k < n; k++) {
+            const double d = colsq[k] > s->min_diag ? colsq[k] : s->min_diag;
+            s->diag[k] = d < s->max_diag ? d : s->max_diag;
+        }
+    for (int k = 0; k < n; k++) D[k] = sqrt(s->diag[k] / s->radius);
+    s->reuse_diag = 1;
+}
+
 int pfo_lm_fit(const double* xs, const double* ys, int n, double coef[4], pfo_lm_summary* sum)
 {
     if (n <= 0) return -1;
@@ -193,9 +241,10 @@ int pfo_lm_fit(const double* xs, const double* ys, int n, double coef[4], pfo_lm
     memset(&s, 0, sizeof(s));
     double x[4] = {1.0, 1.0, 1.0, 1.0};  /* Depth.cpp:1270-1274 */
     double best[4] = {1.0, 1.0, 1.0, 1.0};
-    double g[4], scale[4], diag[4], D[4], step[4], delta[4], cand[4];
-    double radius = LM_INIT_RADIUS, decrease = 2.0;
-    int reuse_diag = 0, invalid_run = 0;
+    double g[4], scale[4], colsq[4], D[4], step[4], delta[4], cand[4];
+    pfo_lm_strategy lms;
+    pfo_lms_init(&lms, LM_INIT_RADIUS, LM_MAX_RADIUS, LM_MIN_DIAG, LM_MAX_DIAG);
+    int invalid_run = 0;
     double x_norm = -1.0;  /* trust_region_minimizer.cc:167: not set again until a step is accepted */
 
     /* iteration zero (:177-212, :226-279) */
@@ -223,21 +272,14 @@ int pfo_lm_fit(const double* xs, const double* ys, int n, double coef[4], pfo_lm
             }
             if (gmax <= LM_GRAD_TOL) { term = PFO_LM_GRADIENT_TOL; break; }
         }
-        if (radius <= LM_MIN_RADIUS) { term = PFO_LM_MIN_RADIUS; break; }
+        if (lms.radius <= LM_MIN_RADIUS) { term = PFO_LM_MIN_RADIUS; break; }
         iteration++;
 
         /* ComputeTrustRegionStep -> LevenbergMarquardtStrategy::ComputeStep (:355-424) */
-        if (!reuse_diag) {
-            col_sqnorm(P.J, n, diag);
-            for (int k = 0; k < 4; k++) {
-                double d = diag[k] > LM_MIN_DIAG ? diag[k] : LM_MIN_DIAG;
-                diag[k] = d < LM_MAX_DIAG ? d : LM_MAX_DIAG;
-            }
-        }
-        for (int k = 0; k < 4; k++) D[k] = sqrt(diag[k] / radius);
+        if (!lms.reuse_diag) col_sqnorm(P.J, n, colsq);
+        pfo_lms_regularizer(&lms, colsq, 4, D);
         int ok = dense_schur(P.J, r, n, D, step) == 0;
         for (int k = 0; ok && k < 4; k++) ok = isfinite(step[k]);
-        reuse_diag = 1;
         int valid = 0;
         if (ok) {
             for (int k = 0; k < 4; k++) step[k] = step[k] * -1.0;
@@ -254,8 +296,7 @@ int pfo_lm_fit(const double* xs, const double* ys, int n, double coef[4], pfo_lm
         }
         if (!valid) { /* HandleInvalidStep (:429-462) */
             if (++invalid_run >= LM_MAX_INVALID) { term = PFO_LM_FAILURE; break; }
-            radius = radius / decrease;  /* StepIsInvalid = StepRejected(0) */
-            decrease *= 2.0;
+            pfo_lms_rejected(&lms, 0.0);  /* StepIsInvalid = StepRejected(0) */
             successful = 0;
             continue;
         }
@@ -278,15 +319,10 @@ int pfo_lm_fit(const double* xs, const double* ys, int n, double coef[4], pfo_lm
             x_cost = lm_evaluate(&P, x, r, P.J, g);
             for (int i = 0; i < n; i++)
                 for (int k = 0; k < 4; k++) P.J[4 * (size_t)i + k] *= scale[k];
-            double f = 1.0 - pow(2.0 * rel_decrease - 1.0, 3);
-            radius = radius / (f > 1.0 / 3.0 ? f : 1.0 / 3.0);
-            radius = radius < LM_MAX_RADIUS ? radius : LM_MAX_RADIUS;
-            decrease = 2.0;
-            reuse_diag = 0;
+            pfo_lms_accepted(&lms, rel_decrease);
             successful = 1;
         } else { /* HandleUnsuccessfulStep (:782-786) */
-            radius = radius / decrease;
-            decrease *= 2.0;
+            pfo_lms_rejected(&lms, rel_decrease);
             successful = 0;
         }
     }
@@ -382,12 +418,14 @@ int pfo_lm_moments(const double S[15], double coef[4], pfo_lm_summary* sum)
     pfo_lm_summary s;
     memset(&s, 0, sizeof(s));
     double x[4] = {1.0, 1.0, 1.0, 1.0}, best[4] = {1.0, 1.0, 1.0, 1.0};
-    double sc[4], Ms[4][4], g[4], gs[4], diag[4], D[4], step[4], cand[4];
+    double sc[4], Ms[4][4], g[4], gs[4], colsq[4], D[4], step[4], cand[4];
     for (int k = 0; k < 4; k++) sc[k] = 1.0 / (1.0 + sqrt(M[k][k]));
     for (int i = 0; i < 4; i++)
         for (int j = 0; j < 4; j++) Ms[i][j] = (M[i][j] * sc[i]) * sc[j];
-    double radius = LM_INIT_RADIUS, decrease = 2.0, x_norm = -1.0;
-    int reuse_diag = 0, invalid_run = 0;
+    double x_norm = -1.0;
+    pfo_lm_strategy lms;
+    pfo_lms_init(&lms, LM_INIT_RADIUS, LM_MAX_RADIUS, LM_MIN_DIAG, LM_MAX_DIAG);
+    int invalid_run = 0;
     double x_cost = mom_cost(S, x);
     mom_gradient(S, x, g);
     s.initial_cost = x_cost;
@@ -407,14 +445,10 @@ int pfo_lm_moments(const double S[15], double coef[4], pfo_lm_summary* sum)
             }
             if (gmax <= LM_GRAD_TOL) { term = PFO_LM_GRADIENT_TOL; break; }
         }
-        if (radius <= LM_MIN_RADIUS) { term = PFO_LM_MIN_RADIUS; break; }
+        if (lms.radius <= LM_MIN_RADIUS) { term = PFO_LM_MIN_RADIUS; break; }
         iteration++;
-        if (!reuse_diag)
-            for (int k = 0; k < 4; k++) {
-                double d = Ms[k][k] > LM_MIN_DIAG ? Ms[k][k] : LM_MIN_DIAG;
-                diag[k] = d < LM_MAX_DIAG ? d : LM_MAX_DIAG;
-            }
-        for (int k = 0; k < 4; k++) D[k] = sqrt(diag[k] / radius);
+        for (int k = 0; k < 4; k++) colsq[k] = Ms[k][k];
+        pfo_lms_regularizer(&lms, colsq, 4, D);
         for (int k = 0; k < 4; k++) gs[k] = sc[k] * g[k];  /* J_s' r */
         /* Schur elimination of column 0 (as dense_schur above, from the moments) */
         double ete = D[0] * D[0] + Ms[0][0];
@@ -437,7 +471,6 @@ int pfo_lm_moments(const double S[15], double coef[4], pfo_lm_summary* sum)
             step[1] = z[0]; step[2] = z[1]; step[3] = z[2];
             for (int k = 0; ok && k < 4; k++) ok = isfinite(step[k]);
         }
-        reuse_diag = 1;
         int valid = 0;
         double mcc = 0.0;
         if (ok) {
@@ -455,8 +488,7 @@ int pfo_lm_moments(const double S[15], double coef[4], pfo_lm_summary* sum)
         }
         if (!valid) {
             if (++invalid_run >= LM_MAX_INVALID) { term = PFO_LM_FAILURE; break; }
-            radius = radius / decrease;
-            decrease *= 2.0;
+            pfo_lms_rejected(&lms, 0.0);
             successful = 0;
             continue;
         }
@@ -474,16 +506,10 @@ int pfo_lm_moments(const double S[15], double coef[4], pfo_lm_summary* sum)
             x_norm = norm4(x);
             x_cost = mom_cost(S, x);
             mom_gradient(S, x, g);
-            const double q = 2.0 * rel - 1.0;
-            const double f = 1.0 - q * q * q;
-            radius = radius / (f > 1.0 / 3.0 ? f : 1.0 / 3.0);
-            radius = radius < LM_MAX_RADIUS ? radius : LM_MAX_RADIUS;
-            decrease = 2.0;
-            reuse_diag = 0;
+            lms_accepted(&lms, rel, 0);  /* (2 rel - 1)^3 as q*q*q, as the GPU */
             successful = 1;
         } else {
-            radius = radius / decrease;
-            decrease *= 2.0;
+            pfo_lms_rejected(&lms, rel);
             successful = 0;
         }
     }

@@ -106,3 +106,74 @@ def test_fused_u16_tolerances(cfg):
         assert d.max() <= 2 and (d > 0).mean() <= 1e-3, (seed, d.max(), (d > 0).mean())
         d = np.abs(ne.astype(np.int64) - ref)
         assert d.max() <= 8 and (d <= 1).mean() >= 0.99, (seed, d.max(), (d <= 1).mean())
+
+
+# ------------------------------------------------------------------------------------------------
+# Reference-held pins for the LM restatement: Ceres 1.13's own unit tests of the strategy that
+# SolveDepthToDepth's Solve runs (vendored in the reference as
+# ceres-solver/internal/ceres/levenberg_marquardt_strategy_test.cc), replayed against the
+# oracle's factored-out strategy (pfo_lms_*), which both LM forms -- and, through the moment form
+# it is bit-identical to, the HIP kernel -- use.
+import ctypes as C  # noqa: E402
+
+
+class _Lms(C.Structure):
+    _fields_ = [("radius", C.c_double), ("max_radius", C.c_double), ("decrease", C.c_double),
+                ("min_diag", C.c_double), ("max_diag", C.c_double), ("reuse_diag", C.c_int),
+                ("diag", C.c_double * 4)]
+
+
+def _lms(initial_radius, max_radius, min_diag, max_diag):
+    L = O.lib()
+    L.pfo_lms_init.argtypes = [C.POINTER(_Lms)] + [C.c_double] * 4
+    for f in (L.pfo_lms_accepted, L.pfo_lms_rejected):
+        f.argtypes = [C.POINTER(_Lms), C.c_double]
+    L.pfo_lms_regularizer.argtypes = [C.POINTER(_Lms), C.POINTER(C.c_double), C.c_int,
+                                      C.POINTER(C.c_double)]
+    s = _Lms()
+    L.pfo_lms_init(C.byref(s), initial_radius, max_radius, min_diag, max_diag)
+    return L, s
+
+
+def test_ceres_lm_strategy_accept_reject_radius_scaling():
+    """levenberg_marquardt_strategy_test.cc:81-110 (AcceptRejectStepRadiusScaling), with its
+    exact EXPECT_EQs on the radius after each accept/reject."""
+    L, s = _lms(2.0, 20.0, 1e-8, 1e8)
+    assert s.radius == 2.0
+    L.pfo_lms_rejected(C.byref(s), 0.0)
+    assert s.radius == 1.0
+    L.pfo_lms_rejected(C.byref(s), -1.0)
+    assert s.radius == 0.25
+    for q, expect in ((1.0, 0.25 * 3.0), (1.0, 0.25 * 3.0 * 3.0), (0.25, 0.25 * 3.0 * 3.0 / 1.125),
+                      (1.0, 0.25 * 3.0 * 3.0 / 1.125 * 3.0),
+                      (1.0, 0.25 * 3.0 * 3.0 / 1.125 * 3.0 * 3.0)):
+        L.pfo_lms_accepted(C.byref(s), q)
+        assert s.radius == expect, (q, s.radius, expect)
+    L.pfo_lms_accepted(C.byref(s), 1.0)
+    assert s.radius == 20.0  # capped at max_radius
+    # a rejection after acceptances restarts the decrease factor at 2
+    L.pfo_lms_rejected(C.byref(s), 0.0)
+    assert s.radius == 10.0 and s.decrease == 4.0
+
+
+def test_ceres_lm_strategy_correct_diagonal_to_linear_solver():
+    """levenberg_marquardt_strategy_test.cc:113-160 (CorrectDiagonalToLinearSolver): for the
+    Jacobian [[0, 1, 100], [0, 1, 0]] with min/max LM diagonal 1e-2/1e2 and radius 2, the D
+    handed to the linear solver is sqrt({1e-2, 2, 1e2} / 2) -- the squared column norms
+    {0, 2, 1e4} clamped.  Also: the diagonal is reused after a rejection (only D's radius
+    changes) and recomputed after an acceptance."""
+    L, s = _lms(2.0, 20.0, 1e-2, 1e2)
+    J = np.array([[0.0, 1.0, 100.0], [0.0, 1.0, 0.0]])
+    colsq = np.ascontiguousarray((J * J).sum(0))
+    D = np.zeros(3)
+    dp = C.POINTER(C.c_double)
+    L.pfo_lms_regularizer(C.byref(s), colsq.ctypes.data_as(dp), 3, D.ctypes.data_as(dp))
+    expect = np.sqrt(np.array([1e-2, 2.0, 1e2]) / 2.0)
+    assert np.allclose(D, expect, rtol=0, atol=1e-16), (D, expect)
+    L.pfo_lms_rejected(C.byref(s), 0.0)  # radius 1, diagonal reused even for new norms
+    other = np.array([5.0, 5.0, 5.0])
+    L.pfo_lms_regularizer(C.byref(s), other.ctypes.data_as(dp), 3, D.ctypes.data_as(dp))
+    assert np.allclose(D, np.sqrt(np.array([1e-2, 2.0, 1e2]) / 1.0), rtol=0, atol=1e-16)
+    L.pfo_lms_accepted(C.byref(s), 1.0)  # radius 3, diagonal recomputed
+    L.pfo_lms_regularizer(C.byref(s), other.ctypes.data_as(dp), 3, D.ctypes.data_as(dp))
+    assert np.allclose(D, np.sqrt(other / 3.0), rtol=0, atol=1e-16)

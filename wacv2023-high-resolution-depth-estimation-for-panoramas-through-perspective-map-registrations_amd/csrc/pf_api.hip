@@ -69,11 +69,10 @@ struct pf_ctx {
     LevelCache lc;
     bool reg_valid = false;
     uint32_t reg_zr0 = 0, reg_zr1 = 0;
-    // E->P depth warp for one panorama size (pf_warp.hip): tile patches with their panorama
-    // boxes, per tile pixel the corner index in its box and the (fx, fy) weights; built on
-    // first use
-    int wmap_pw = 0, wmap_ph = 0, npatch = 0;
-    DevBuf wmap, wfxy, wpatch;
+    // E->P depth warp for one panorama size (pf_warp.hip): per tile pixel the bilinear corner
+    // and (fx, fy) weights, the panorama regions and their pixel entries; built on first use
+    int wmap_pw = 0, wmap_ph = 0, nregions = 0;
+    DevBuf wmap, wfxy, wregion, wperm, wentry;
     // workspace
     DevBuf buf[3], lnorm, coeffs, lsum_ws, metrics_ws, reg_sums, reg_active;
     // SolveDepthBySmoothing (pf_smooth.hip): boxes, grid tables, per-pixel source and mask
@@ -293,7 +292,7 @@ void pf_destroy(pf_ctx* c)
     (void)hipStreamSynchronize(c->stream);
     DevBuf* all[] = {&c->geom, &c->reg, &c->rcols, &c->rrows, &c->cams, &c->rgb_off,
                      &c->buf[0], &c->buf[1], &c->buf[2], &c->lnorm, &c->coeffs, &c->lsum_ws,
-                     &c->wmap, &c->wfxy, &c->wpatch, &c->metrics_ws, &c->reg_sums,
+                     &c->wmap, &c->wfxy, &c->wregion, &c->wperm, &c->wentry, &c->metrics_ws, &c->reg_sums,
                      &c->reg_active};
     for (DevBuf* b : all) release(*b);
     for (int l = 0; l < 4; l++) {
@@ -481,14 +480,7 @@ int pf_set_tiles(pf_ctx* c, const pf_window* fovs, const pf_window* ranges, int 
     c->lc.out_w = 0;  // boxes and registration grids depend on the ranges: rebuild lazily
     c->reg_valid = false;
     c->wmap_pw = c->wmap_ph = 0;
-    std::vector<WarpPatch> patches;
-    const int pe = warp_patch_edge();
-    for (int i = 0; i < ntiles; i++)
-        for (int y = 0; y < tile_h[i]; y += pe)
-            for (int x = 0; x < tile_w[i]; x += pe) patches.push_back(WarpPatch{i, x, y, 0, 0, 0, 0, 0});
-    c->npatch = (int)patches.size();
     int rc;
-    if ((rc = upload(c, c->wpatch, patches))) return rc;
     if ((rc = upload(c, c->geom, c->geom_h))) return rc;
     if ((rc = upload(c, c->cams, cams))) return rc;
     if ((rc = upload(c, c->rgb_off, rgb_off))) return rc;
@@ -1108,26 +1100,164 @@ static int fuse_impl(pf_ctx* c, const float* emap, int ew, int eh, int ec, const
                       (float*)c->lnorm.p);
 }
 
-// Once per (layout, panorama size): order the warp patches by panorama footprint -- 32-row bands
-// of the box centre, then its azimuth -- instead of tile by tile.  The blocks resident on one XCD
-// then stage overlapping boxes (neighbouring patches of a tile and the overlapping patches of the
-// neighbouring tiles) at about the same time, so a panorama line is fetched from HBM once and
-// re-read from that XCD's L2 instead of once per box that holds it (the boxes hold each panorama
-// pixel ~3 times at the C2 layout).  Patches are self-describing, so the permutation is free.
-static int sort_warp_patches(pf_ctx* c, int pw)
+// Once per (layout, panorama size): the depth warp's regions (pf_warp.hip).  Every tile row is
+// cut into aligned strips of kWarpStrip pixels; a strip's footprint is the box of its pixels'
+// bilinear corners (azimuth unwrapped around its first pixel).  Strips are sorted by (band of
+// kWarpBand rows of the footprint's centre, centre column) -- so strips of different tiles that
+// look at the same panorama lines end up together -- and cut greedily into regions of at most
+// kWarpRegionPx pixels and kWarpSlots tiles whose joint footprint, +1 row and column (and the
+// column alignment of quad staging), fits kWarpRows x kWarpPitch.  Inside a region the strips
+// are in layout order.  A strip whose own footprint does not fit goes to a "wide" region (direct
+// gathers).  Regions are ordered by band, then column, so neighbouring boxes, which share
+// lines, are staged by neighbouring blocks.
+static int build_warp_regions(pf_ctx* c, int pw, int ph, long long npix)
 {
-    std::vector<WarpPatch> p(c->npatch);
-    HIPCHK(c, hipMemcpyAsync(p.data(), c->wpatch.p, sizeof(WarpPatch) * p.size(),
+    std::vector<uint32_t> wxy((size_t)npix);
+    HIPCHK(c, hipMemcpyAsync(wxy.data(), c->wmap.p, sizeof(uint32_t) * npix,
                              hipMemcpyDeviceToHost, c->stream));
     HIPCHK(c, hipStreamSynchronize(c->stream));
-    auto key = [pw](const WarpPatch& w) {
-        const long long band = (w.gy0 + w.bh / 2) / 32;
-        const long long col = (w.gx0 + w.bw / 2) % pw;
-        return band * 65536 + col;
+    const bool quads = (pw & 3) == 0;
+    auto wrap = [pw](int d) {
+        if (d > pw / 2) d -= pw;
+        if (d < -(pw / 2)) d += pw;
+        return d;
     };
-    std::stable_sort(p.begin(), p.end(),
-                     [&](const WarpPatch& a, const WarpPatch& b) { return key(a) < key(b); });
-    return upload(c, c->wpatch, p);
+    struct Strip {
+        int tile, len, xref, umin, umax, ymin, ymax;
+        uint32_t p0;
+        long long key;
+    };
+    std::vector<Strip> strips;
+    strips.reserve((size_t)(npix / kWarpStrip + c->ntiles * 64));
+    for (int t = 0; t < c->ntiles; t++) {
+        const TileGeom& g = c->geom_h[t];
+        for (int Y = 0; Y < g.h; Y++)
+            for (int X0 = 0; X0 < g.w; X0 += kWarpStrip) {
+                Strip S;
+                S.tile = t;
+                S.len = std::min(kWarpStrip, g.w - X0);
+                S.p0 = (uint32_t)(g.pix_off + (long long)Y * g.w + X0);
+                S.xref = (int)(wxy[S.p0] & 0xFFFFu);
+                S.umin = S.umax = 0;
+                S.ymin = INT32_MAX;
+                S.ymax = INT32_MIN;
+                for (int j = 0; j < S.len; j++) {
+                    const uint32_t m = wxy[S.p0 + j];
+                    const int du = wrap((int)(m & 0xFFFFu) - S.xref), y = (int)(m >> 16);
+                    S.umin = std::min(S.umin, du);
+                    S.umax = std::max(S.umax, du);
+                    S.ymin = std::min(S.ymin, y);
+                    S.ymax = std::max(S.ymax, y);
+                }
+                int xc = S.xref + (S.umin + S.umax) / 2;
+                xc = ((xc % pw) + pw) % pw;
+                S.key = (long long)((S.ymin + S.ymax) / 2 / kWarpBand) * pw + xc;
+                strips.push_back(S);
+            }
+    }
+    std::stable_sort(strips.begin(), strips.end(),
+                     [](const Strip& a, const Strip& b) { return a.key < b.key; });
+    const int slack = quads ? 3 : 0;  // columns added by aligning the box origin to a quad
+    auto fits = [&](int u0, int u1, int y0, int y1) {
+        return u1 - u0 + 2 + slack <= kWarpPitch && y1 - y0 + 2 <= kWarpRows;
+    };
+    std::vector<WarpRegion> regions;
+    std::vector<std::vector<int>> members;  // strip indices per region
+    std::vector<int> wide;
+    size_t k = 0;
+    while (k < strips.size()) {
+        if (!fits(strips[k].umin, strips[k].umax, strips[k].ymin, strips[k].ymax)) {
+            wide.push_back((int)k++);
+            continue;
+        }
+        WarpRegion R{};
+        const int xr = strips[k].xref;
+        int U0 = INT32_MAX, U1 = INT32_MIN, Y0 = INT32_MAX, Y1 = INT32_MIN, px = 0;
+        std::vector<int> mem;
+        while (k < strips.size()) {
+            const Strip& S = strips[k];
+            if (!fits(S.umin, S.umax, S.ymin, S.ymax)) break;  // wide: handled by the outer loop
+            const int off = wrap(S.xref - xr);
+            const int u0 = std::min(U0, off + S.umin), u1 = std::max(U1, off + S.umax);
+            const int y0 = std::min(Y0, S.ymin), y1 = std::max(Y1, S.ymax);
+            if (px + kWarpStrip > kWarpRegionPx || !fits(u0, u1, y0, y1)) break;
+            int s = 0;
+            while (s < R.nslot && R.tile[s] != S.tile) s++;
+            if (s == R.nslot) {
+                if (R.nslot == kWarpSlots) break;
+                R.tile[R.nslot++] = S.tile;
+            }
+            U0 = u0; U1 = u1; Y0 = y0; Y1 = y1;
+            px += kWarpStrip;
+            mem.push_back((int)k++);
+        }
+        std::sort(R.tile, R.tile + R.nslot);  // slot order = tile order (k_warp_entries)
+        int gx0 = ((xr + U0) % pw + pw) % pw;
+        const int a = quads ? (gx0 & 3) : 0;
+        gx0 -= a;
+        const int width = U1 - U0 + 2 + a;
+        R.gx0 = gx0;
+        R.gy0 = Y0;
+        R.bwu = quads ? (width + 3) / 4 : width;
+        R.units = R.bwu * (Y1 - Y0 + 2);
+        regions.push_back(R);
+        members.push_back(std::move(mem));
+    }
+    for (size_t w = 0; w < wide.size(); w += kWarpRegionPx / kWarpStrip) {
+        WarpRegion R{};
+        R.wide = 1;
+        std::vector<int> mem;
+        for (size_t j = w; j < std::min(wide.size(), w + kWarpRegionPx / kWarpStrip); j++) {
+            const int t = strips[wide[j]].tile;
+            int s = 0;
+            while (s < R.nslot && R.tile[s] != t) s++;
+            if (s == R.nslot) {
+                if (R.nslot == kWarpSlots) break;
+                R.tile[R.nslot++] = t;
+            }
+            mem.push_back(wide[j]);
+        }
+        w -= kWarpRegionPx / kWarpStrip - mem.size();  // a slot-limited region ends early
+        std::sort(R.tile, R.tile + R.nslot);
+        regions.push_back(R);
+        members.push_back(std::move(mem));
+    }
+    // entries: each region's strips in layout order, kWarpStrip entries per strip
+    std::vector<uint32_t> perm;
+    perm.reserve(strips.size() * kWarpStrip);
+    for (size_t r = 0; r < regions.size(); r++) {
+        std::vector<int>& mem = members[r];
+        std::sort(mem.begin(), mem.end(),
+                  [&](int x, int y) { return strips[x].p0 < strips[y].p0; });
+        regions[r].e0 = (int)perm.size();
+        regions[r].n = (int)mem.size() * kWarpStrip;
+        for (int m : mem)
+            for (int j = 0; j < kWarpStrip; j++)
+                perm.push_back(j < strips[m].len ? strips[m].p0 + j : 0xFFFFFFFFu);
+    }
+    if (perm.size() >= (1u << 31))
+        return fail(c, PF_EINVAL, "depth warp: %zu entries (< 2^31)", perm.size());
+    int rc;
+    if ((rc = upload(c, c->wregion, regions))) return rc;
+    if ((rc = upload(c, c->wperm, perm))) return rc;
+    if ((rc = ensure(c, c->wentry, sizeof(WarpEntry) * perm.size()))) return rc;
+    c->nregions = (int)regions.size();
+    if (getenv("PF_WARP_STATS")) {
+        double boxf = 0;
+        int maxslot = 0;
+        for (const WarpRegion& R : regions) {
+            boxf += (double)R.units * (quads ? 4 : 1);
+            maxslot = std::max(maxslot, R.nslot);
+        }
+        fprintf(stderr, "[pf warp] %d regions (%zu wide strips), %.1f px/region, staged %.3f x "
+                "the panorama, max %d tiles/region\n", c->nregions, wide.size(),
+                (double)npix / regions.size(), boxf / ((double)pw * ph), maxslot);
+    }
+    launch_warp_entries(c->stream, (const TileGeom*)c->geom.p, (const WarpRegion*)c->wregion.p,
+                        c->nregions, (const uint32_t*)c->wperm.p, (const uint32_t*)c->wmap.p,
+                        (const float*)c->wfxy.p, pw, ph, (WarpEntry*)c->wentry.p);
+    HIPCHK(c, hipGetLastError());
+    return PF_OK;
 }
 
 extern "C" {
@@ -1265,18 +1395,17 @@ int pf_warp_depth(pf_ctx* c, const float* pano, int pw, int ph, int batch,
     if (c->wmap_pw != pw || c->wmap_ph != ph) {
         if ((rc = ensure(c, c->wmap, sizeof(uint32_t) * npix))) return rc;
         if ((rc = ensure(c, c->wfxy, sizeof(float) * 2 * npix))) return rc;
-        launch_warp_prepare(c->stream, (const TileGeom*)c->geom.p, c->ntiles, c->npix_max,
-                            (WarpPatch*)c->wpatch.p, c->npatch, pw, ph, (uint32_t*)c->wmap.p,
-                            (float*)c->wfxy.p);
+        launch_warp_coords(c->stream, (const TileGeom*)c->geom.p, c->ntiles, c->npix_max, pw, ph,
+                           (uint32_t*)c->wmap.p, (float*)c->wfxy.p);
         HIPCHK(c, hipGetLastError());
-        if ((rc = sort_warp_patches(c, pw))) return rc;
+        if ((rc = build_warp_regions(c, pw, ph, npix))) return rc;
         c->wmap_pw = pw;
         c->wmap_ph = ph;
     }
     StageTimer t(c, PF_STAGE_WARP, batch * (4.0 * pw * ph + 4.0 * (double)npix), 1);
     launch_warp_depth(c->stream, (const TileGeom*)c->geom.p, c->ntiles,
-                      (const WarpPatch*)c->wpatch.p, c->npatch, (const uint32_t*)c->wmap.p,
-                      (const float*)c->wfxy.p, pano, pw, ph, (long long)pw * ph,
+                      (const WarpRegion*)c->wregion.p, c->nregions,
+                      (const WarpEntry*)c->wentry.p, pano, pw, ph, (long long)pw * ph,
                       (const Resp*)resp, tiles, c->tile_elems, batch);
     HIPCHK(c, hipGetLastError());
     return PF_OK;
