@@ -279,7 +279,14 @@ void pf_leres_layout(std::vector<Vec4f>& fovs, std::vector<Vec4f>& ranges);
 extern "C" int pfd_load_map(const char* fn, int is_emap, float* out, long long cap, int* w,
                             int* h, int* c);
 extern "C" int pfd_save_png16(const char* fn, const uint16_t* data, int w, int h);
-/* the tile writer of the RGB export: baseline JPEG, 4:4:4, stb/IJG quality scaling (>= 100:
- * every quantiser 1), 8-bit gray (c = 1) or RGB (c = 3) rows top-first */
-extern "C" int pfd_save_jpeg(const char* fn, const uint8_t* px, int w, int h, int c, int quality);
+/* the tile writer of the RGB export: the bytes of stbi_write_jpg(fn, w, h, c, px, quality) with
+ * stbi_flip_vertically_on_write(flip) (Main.cpp:319-320), c = 1..4 channels, rows top-first */
+extern "C" int pfd_save_jpeg(const char* fn, const uint8_t* px, int w, int h, int c, int quality,
+                             int flip);
+/* the image decoders behind Load (stbi_load / stbi_load_16 with req_comp 0, Depth.cpp:56-100):
+ * native samples (u8, or u16 when *is16) into out (capacity cap bytes); -1 load failure, -2 out
+ * too small (dims written either way).  pfd_is_16_bit = stbi_is_16_bit. */
+extern "C" int pfd_decode_image(const char* fn, void* out, long long cap, int* w, int* h, int* c,
+                                int* is16);
+extern "C" int pfd_is_16_bit(const char* fn);
 extern "C" void pfd_leres_layout(float* fovs, float* ranges);

@@ -5,9 +5,9 @@ facade, and writes <raw>.png (u16), <raw>.aligned.txt, .res.png and .giv.png.
 
 Bars: the fused u16 PNG is bit-exact against the CPU oracle's MergeDepthMaps on the same
 (u16-quantised) inputs; the metrics file agrees with the oracle's ErrorData/ErrorEmap within
-the tolerances of tests/test_gpu_metrics.py (plus the file's 6-decimal printing).  The
-reference's tiles are JPEG (not decodable by this build): the tiles here are 16-bit PNGs, the
-MiDaS naming of Main.cpp:570-573."""
+the tolerances of tests/test_gpu_metrics.py (plus the file's 6-decimal printing).  The first
+test's tiles are 16-bit PNGs (the MiDaS naming of Main.cpp:570-573); test_mode0_cli_jpeg_inputs
+covers the reference's JPEG conventions with stb-decoded pixels as the oracle's inputs."""
 import math
 import os
 import struct
@@ -193,48 +193,47 @@ def test_export_rgb_tiles(tmp_path):
 def test_mode0_cli_jpeg_inputs(tmp_path):
     """The reference's own file conventions: LeReS tiles as 8-bit gray JPEG in test_images
     naming (<raw>.<a0>_<a1>_<z0>_<z1>.jpg, Main.cpp:576-578) and a bifuse baseline <raw>.jpg
-    (Main.cpp:499).  The oracle is fed the same decoded floats (the library's loader), so the
-    fused u16 output is still bit-exact."""
+    (Main.cpp:499).  The oracle is run on the pixels the reference's stb_image decodes from
+    those files: tests/golden/cli_jpeg_stb.json (tools/make_stb_golden.py, from the stb build of
+    /root/reference) records each file's SHA-256 and the SHA-256 of stb's decode; the files
+    generated here must hash the same, and the facade's decoder must reproduce stb's hashes, so
+    the oracle's inputs below are stb's pixels.  The CLI's fused u16 output is then bit-exact
+    against the oracle."""
     import ctypes as C
-    Image = pytest.importorskip("PIL.Image")
-    L = C.CDLL(os.path.join(os.path.dirname(panofuse.LIB_PATH), "libpanofuse_depth.so"))
-    L.pfd_load_map.argtypes = [C.c_char_p, C.c_int, C.POINTER(C.c_float), C.c_longlong,
-                               C.POINTER(C.c_int), C.POINTER(C.c_int), C.POINTER(C.c_int)]
+    import hashlib
+    import json
 
-    def load(fn, is_emap):
-        w, h, c = C.c_int(), C.c_int(), C.c_int()
-        buf = np.zeros(1 << 22, np.float32)
-        assert L.pfd_load_map(str(fn).encode(), is_emap, buf.ctypes.data_as(C.POINTER(C.c_float)),
-                              buf.size, C.byref(w), C.byref(h), C.byref(c)) == 0
-        return buf[:w.value * h.value * c.value].reshape(h.value, w.value, c.value)
+    import codec_cases as CC
+    pytest.importorskip("PIL.Image")
+    L = C.CDLL(os.path.join(os.path.dirname(panofuse.LIB_PATH), "libpanofuse_depth.so"))
+    ip = C.POINTER(C.c_int)
+    L.pfd_decode_image.argtypes = [C.c_char_p, C.c_void_p, C.c_longlong, ip, ip, ip, ip]
+    golden = json.load(open(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden",
+                                         "cli_jpeg_stb.json")))
+
+    def stb_pixels(fn):
+        rec = golden[fn.name]
+        assert hashlib.sha256(fn.read_bytes()).hexdigest() == rec["file_sha256"], fn.name
+        w, h, c, s16 = C.c_int(), C.c_int(), C.c_int(), C.c_int()
+        buf = np.zeros(1 << 22, np.uint8)
+        assert L.pfd_decode_image(str(fn).encode(), buf.ctypes.data, buf.size, C.byref(w),
+                                  C.byref(h), C.byref(c), C.byref(s16)) == 0
+        px = buf[:w.value * h.value * c.value].reshape(h.value, w.value, c.value)
+        assert list(px.shape) == rec["stb_shape"]
+        assert hashlib.sha256(px.tobytes()).hexdigest() == rec["stb_px_sha256"], fn.name
+        return px.astype(np.float32) / np.float32(255.0)  # Depth.cpp:96-98
 
     d = {k: tmp_path / k for k in ("rgb", "gt", "base", "result", "test_images")}
     for p in d.values():
         p.mkdir()
-    lay = PL.leres_layout(512, 494)
-    tiles_o, total = O.make_tiles(lay)
-    raw = "room_rgb"
+    raw, names, base_fn, gt = CC.cli_jpeg_inputs(d)
     (d["rgb"] / (raw + ".png")).write_bytes(b"\x89PNG")
-    seeds = pf_synth.seeds_for(1, 20261015 + 555)
-    gt = _q16(pf_synth.scene_depth(seeds, 2048, 1024)[0].numpy())
     _png16_write(d["gt"] / "room_depth.png", gt)
-    base8 = (np.clip(pf_synth.baseline_emap(seeds, 512, 256)[0].numpy(), 0, 1) * 255 + 0.5
-             ).astype(np.uint8)
-    Image.fromarray(base8, "L").save(d["base"] / (raw + ".jpg"), "JPEG", quality=95)
-    gt_f = gt.astype(np.float32) / np.float32(65535.0)
-    tdata = O.warp_depth(gt_f, tiles_o, total, O.responses(pf_synth.responses(seeds, lay.ntiles)))
-    t8 = (np.clip(tdata, 0, 1) * 255 + 0.5).astype(np.uint8)
-    dec = []
-    off = 0
-    for t in range(lay.ntiles):
-        f = [_cround(float(v) / MYPI * 180.0) for v in lay.fovs[t]]
-        fn = d["test_images"] / f"{raw}.{f[0]}_{f[1]}_{f[2]}_{f[3]}.jpg"
-        Image.fromarray(t8[off:off + 512 * 494].reshape(494, 512), "L").save(fn, "JPEG",
-                                                                              quality=95)
-        dec.append(load(fn, 0)[..., 0].reshape(-1))
-        off += 512 * 494
-    base_f = load(d["base"] / (raw + ".jpg"), 1)[..., 0]
-    ref, _ = O.merge(base_f, tiles_o, np.concatenate(dec), 2048, ZR)
+    lay = PL.leres_layout(512, 494)
+    tiles_o, _ = O.make_tiles(lay)
+    dec = np.concatenate([stb_pixels(fn)[..., 0].reshape(-1) for fn in names])
+    base_f = stb_pixels(base_fn)[..., 0]
+    ref, _ = O.merge(base_f, tiles_o, dec, 2048, ZR)
     cmd = [BIN, "0", str(d["rgb"]), str(d["gt"]), str(d["base"]), str(d["result"]), "--tiles",
            str(d["test_images"])]
     r = subprocess.run(cmd, capture_output=True, text=True, timeout=300)

@@ -29,7 +29,7 @@ def lib():
     L.pfd_save_png16.argtypes = [C.c_char_p, C.POINTER(C.c_uint16), C.c_int, C.c_int]
     L.pfd_leres_layout.argtypes = [fp, fp]
     L.pfd_save_jpeg.argtypes = [C.c_char_p, C.POINTER(C.c_uint8), C.c_int, C.c_int, C.c_int,
-                                C.c_int]
+                                C.c_int, C.c_int]
     return L
 
 
@@ -165,10 +165,15 @@ def test_pfm_endianness_and_cap(lib, tmp_path, little):
 
 
 def test_pgm_and_rejections(lib, tmp_path):
-    a = np.random.default_rng(5).integers(0, 4096, (4, 5), dtype=np.uint16)
-    open(tmp_path / "a.pgm", "wb").write(b"P5\n# c\n5 4\n4095\n" + a.astype(">u2").tobytes())
+    """8-bit PGM samples as stored (stb does not rescale a maxval below 255); a PGM with maxval
+    above 255 is refused, as stb_image v2.23 refuses it."""
+    a = np.random.default_rng(5).integers(0, 201, (4, 5), dtype=np.uint8)
+    open(tmp_path / "a.pgm", "wb").write(b"P5\n# c\n5 4\n200\n" + a.tobytes())
     got = _load(lib, tmp_path / "a.pgm")
-    np.testing.assert_array_equal(got[..., 0], a.astype(np.float32) / np.float32(65535.0))
+    np.testing.assert_array_equal(got[..., 0], a.astype(np.float32) / np.float32(255.0))
+    b = a.astype(np.uint16) * 20
+    open(tmp_path / "b.pgm", "wb").write(b"P5\n5 4\n4095\n" + b.astype(">u2").tobytes())
+    assert _load(lib, tmp_path / "b.pgm") is None
     open(tmp_path / "x.jpg", "wb").write(b"\xff\xd8\xff\xe0" + b"\0" * 64)
     assert _load(lib, tmp_path / "x.jpg") is None
     assert _load(lib, tmp_path / "missing.png") is None
@@ -200,13 +205,14 @@ def test_cli_binary_usage():
 @pytest.mark.parametrize("mode,sub,restart", [("L", None, 0), ("RGB", 0, 0), ("RGB", 2, 0),
                                               ("RGB", 1, 0), ("L", None, 4), ("RGB", 2, 3)])
 def test_jpeg_decoder_vs_libjpeg(lib, tmp_path, mode, sub, restart):
-    """The baseline JPEG decoder behind the loaders (pf_jpeg.cpp; the reference reads its LeReS
-    tiles and some baselines as JPEG through stb_image) against PIL's libjpeg on PIL-encoded
-    files: gray, 4:4:4, 4:2:0, 4:2:2, restart intervals, odd sizes.  Bar: within 2 levels (the
-    integer IDCTs and fixed-point colour conversion of stb and libjpeg differ from each other by
-    about as much), 3 with subsampled chroma (the upsampler rounds as stb does, +8/+2, where
-    libjpeg alternates +8/+7, and a 1-level chroma difference becomes 1.772 levels of blue);
-    mean under 0.3.  Parity with stb itself is unpinned (no stb build here)."""
+    """The JPEG decoder behind the loaders (pf_jpeg.cpp) beside PIL's libjpeg, as a sanity bound
+    on PIL-encoded files: gray, 4:4:4, 4:2:0, 4:2:2, restart intervals, odd sizes.  The decoder
+    is bit-exact to the reference's stb_image (tests/test_codecs_stb.py); stb and libjpeg differ
+    from each other by up to 2 levels without chroma subsampling (their integer IDCTs and
+    fixed-point colour conversions); with subsampled chroma only the mean is bounded (0.3): the
+    upsamplers differ (stb rounds +8/+2 where libjpeg alternates +8/+7) and at an odd width
+    stb's 4:2:2 edge column can differ from libjpeg's by a hundred levels on sharp chroma, which
+    the reference reproduces and so does this decoder (checked against stb itself)."""
     Image = pytest.importorskip("PIL.Image")
     rng = np.random.default_rng(6)
     h, w = 75, 101
@@ -239,14 +245,20 @@ def test_jpeg_decoder_vs_libjpeg(lib, tmp_path, mode, sub, restart):
     else:
         assert got.shape == (h, w, 3)
     d = np.abs(got - ref)
-    assert d.max() <= (3 if sub in (1, 2) else 2) and d.mean() < 0.3, (d.max(), d.mean())
+    assert (sub in (1, 2) or d.max() <= 2) and d.mean() < 0.3, (d.max(), d.mean())
 
 
-def test_jpeg_progressive_rejected(lib, tmp_path):
+def test_jpeg_progressive_decoded(lib, tmp_path):
+    """Progressive JPEG loads (stb_image does), within the libjpeg bound above."""
     Image = pytest.importorskip("PIL.Image")
-    a = np.random.default_rng(1).integers(0, 255, (32, 32), dtype=np.uint8)
-    Image.fromarray(a, "L").save(tmp_path / "p.jpg", "JPEG", progressive=True)
-    assert _load(lib, tmp_path / "p.jpg") is None
+    yy, xx = np.mgrid[0:40, 0:52]
+    a = np.clip(np.sin(xx / 6.0) * 80 + yy * 2 + 60, 0, 255).astype(np.uint8)
+    Image.fromarray(a, "L").save(tmp_path / "p.jpg", "JPEG", progressive=True, quality=90)
+    got = _load(lib, tmp_path / "p.jpg")
+    assert got is not None and got.shape == (40, 52, 1)
+    ref = np.asarray(Image.open(tmp_path / "p.jpg")).astype(np.int32)
+    d = np.abs(np.rint(got[..., 0] * 255.0).astype(np.int32) - ref)
+    assert d.max() <= 2 and d.mean() < 0.3
 
 
 def test_image_decoders_fuzz_sanitized(tmp_path):
@@ -286,11 +298,12 @@ def subprocess_run(cmd, timeout=300):
 @pytest.mark.parametrize("mode,quality", [("RGB", 3072), ("L", 100), ("RGB", 95)])
 def test_jpeg_writer_roundtrip(lib, tmp_path, mode, quality):
     """The tile writer of the RGB export (pfd_save_jpeg; the reference's stbi_write_jpg at
-    quality width*3, clamped to 100, 4:4:4, Main.cpp:320, stb_image_write.h:1448-1451): a
-    baseline JFIF file that libjpeg (PIL) reads as 4:4:4 with all-one quantisers at quality
-    >= 100.  Bar: decoded by libjpeg and by the in-tree decoder, the error against the input is
-    no worse than libjpeg's own encoder at the same quality and sampling (max + 1 level, mean
-    x 1.15); odd sizes exercise the edge blocks."""
+    quality width*3, clamped to 100, 4:4:4, Main.cpp:320, stb_image_write.h:1448-1451; its bytes
+    are pinned to stb's in tests/test_codecs_stb.py): a baseline JFIF file, always three
+    components as stb writes it, that libjpeg (PIL) reads as 4:4:4 with all-one quantisers at
+    quality >= 100.  Bar: decoded by libjpeg and by the in-tree decoder, the error against the
+    input is no worse than libjpeg's own encoder at the same quality and sampling (max + 1
+    level, mean x 1.15); odd sizes exercise the edge blocks."""
     import io
     Image = pytest.importorskip("PIL.Image")
     rng = np.random.default_rng(3)
@@ -307,22 +320,24 @@ def test_jpeg_writer_roundtrip(lib, tmp_path, mode, quality):
     fn = tmp_path / "w.jpg"
     arr = np.ascontiguousarray(a)
     assert lib.pfd_save_jpeg(str(fn).encode(), arr.ctypes.data_as(C.POINTER(C.c_uint8)), w, h,
-                             c, quality) == 0
+                             c, quality, 0) == 0
     im = Image.open(fn)
-    assert im.format == "JPEG" and im.size == (w, h) and im.mode == mode
+    assert im.format == "JPEG" and im.size == (w, h) and im.mode == "RGB"
     if quality >= 100:
         assert all(v == 1 for t in im.quantization.values() for v in t)
-    if c == 3:
-        assert im.layer[0][1:3] == (1, 1) and im.layer[1][1:3] == (1, 1)  # 4:4:4
+    assert im.layer[0][1:3] == (1, 1) and im.layer[1][1:3] == (1, 1)  # 4:4:4
+    # stb writes gray as Y with neutral chroma: compare on the gray level
+    pix = np.asarray(im.convert("L") if c == 1 else im)
     buf = io.BytesIO()  # libjpeg's own encoder at the same settings, the yardstick
     Image.fromarray(a, mode).save(buf, "JPEG", quality=min(quality, 100), subsampling=0)
     buf.seek(0)
     e = np.abs(np.asarray(Image.open(buf)).astype(np.int32) - a.astype(np.int32))
-    d = np.abs(np.asarray(im).astype(np.int32) - a.astype(np.int32))
+    d = np.abs(pix.astype(np.int32) - a.astype(np.int32))
     assert d.max() <= e.max() + 1 and d.mean() <= 1.15 * e.mean() + 0.02, (d.max(), d.mean(),
                                                                             e.max(), e.mean())
     got = _load(lib, fn, 0)
-    got = np.rint(got * 255.0).astype(np.int32).reshape(a.shape)
+    got = np.rint(got * 255.0).astype(np.int32)
+    got = (got[..., 0] if c == 1 else got).reshape(a.shape)
     d = np.abs(got - a.astype(np.int32))
     assert d.max() <= e.max() + 1 and d.mean() <= 1.15 * e.mean() + 0.02, (d.max(), d.mean(),
                                                                             e.max(), e.mean())

@@ -1110,12 +1110,11 @@ static int fuse_impl(pf_ctx* c, const float* emap, int ew, int eh, int ec, const
 // are in layout order.  A strip whose own footprint does not fit goes to a "wide" region (direct
 // gathers).  Regions are ordered by band, then column, so neighbouring boxes, which share
 // lines, are staged by neighbouring blocks.
-static int build_warp_regions(pf_ctx* c, int pw, int ph, long long npix)
+// Strip cut: see build_warp_regions.
+static void warp_cut_strips(pf_ctx* c, int pw, const std::vector<uint32_t>& wxy,
+                            std::vector<WarpRegion>& regions, std::vector<uint32_t>& perm,
+                            size_t& nwide)
 {
-    std::vector<uint32_t> wxy((size_t)npix);
-    HIPCHK(c, hipMemcpyAsync(wxy.data(), c->wmap.p, sizeof(uint32_t) * npix,
-                             hipMemcpyDeviceToHost, c->stream));
-    HIPCHK(c, hipStreamSynchronize(c->stream));
     const bool quads = (pw & 3) == 0;
     auto wrap = [pw](int d) {
         if (d > pw / 2) d -= pw;
@@ -1128,7 +1127,7 @@ static int build_warp_regions(pf_ctx* c, int pw, int ph, long long npix)
         long long key;
     };
     std::vector<Strip> strips;
-    strips.reserve((size_t)(npix / kWarpStrip + c->ntiles * 64));
+    strips.reserve(wxy.size() / kWarpStrip + (size_t)c->ntiles * 64);
     for (int t = 0; t < c->ntiles; t++) {
         const TileGeom& g = c->geom_h[t];
         for (int Y = 0; Y < g.h; Y++)
@@ -1161,7 +1160,6 @@ static int build_warp_regions(pf_ctx* c, int pw, int ph, long long npix)
     auto fits = [&](int u0, int u1, int y0, int y1) {
         return u1 - u0 + 2 + slack <= kWarpPitch && y1 - y0 + 2 <= kWarpRows;
     };
-    std::vector<WarpRegion> regions;
     std::vector<std::vector<int>> members;  // strip indices per region
     std::vector<int> wide;
     size_t k = 0;
@@ -1223,7 +1221,6 @@ static int build_warp_regions(pf_ctx* c, int pw, int ph, long long npix)
         members.push_back(std::move(mem));
     }
     // entries: each region's strips in layout order, kWarpStrip entries per strip
-    std::vector<uint32_t> perm;
     perm.reserve(strips.size() * kWarpStrip);
     for (size_t r = 0; r < regions.size(); r++) {
         std::vector<int>& mem = members[r];
@@ -1235,6 +1232,89 @@ static int build_warp_regions(pf_ctx* c, int pw, int ph, long long npix)
             for (int j = 0; j < kWarpStrip; j++)
                 perm.push_back(j < strips[m].len ? strips[m].p0 + j : 0xFFFFFFFFu);
     }
+    nwide = wide.size();
+}
+// Pixel cut (PF_WARP_CUT=pixel): every tile pixel goes to the region of its own corner --
+// bands of kWarpBand rows cut along their columns into regions of at most kWarpRegionPx pixels
+// and an x0 span that fits the box -- via two counting sorts (by band and column, then stably by
+// region, so a region's pixels are in layout order).  Stages each panorama line about once, but a
+// region's tile-row runs start and end anywhere in a 128-B line.
+static void warp_cut_pixels(pf_ctx* c, int pw, int ph, const std::vector<uint32_t>& wxy,
+                            std::vector<WarpRegion>& regions, std::vector<uint32_t>& perm)
+{
+    const long long npix = (long long)wxy.size();
+    const bool quads = (pw & 3) == 0;
+    std::vector<int> tile_of((size_t)npix);
+    for (int t = 0; t < c->ntiles; t++) {
+        const TileGeom& g = c->geom_h[t];
+        std::fill(tile_of.begin() + g.pix_off, tile_of.begin() + g.pix_off + (long long)g.w * g.h,
+                  t);
+    }
+    const int nband = (ph + kWarpBand - 1) / kWarpBand;
+    const size_t nbins = (size_t)nband * pw;
+    std::vector<uint32_t> cnt(nbins + 1, 0);
+    auto key = [&](uint32_t m) { return (size_t)((m >> 16) / kWarpBand) * pw + (m & 0xFFFFu); };
+    for (long long p = 0; p < npix; p++) cnt[key(wxy[p]) + 1]++;
+    for (size_t k = 0; k < nbins; k++) cnt[k + 1] += cnt[k];
+    std::vector<uint32_t> order((size_t)npix);
+    for (long long p = 0; p < npix; p++) order[cnt[key(wxy[p])]++] = (uint32_t)p;
+    const int span = kWarpPitch - 2 - (quads ? 3 : 0);
+    std::vector<uint32_t> rid((size_t)npix);
+    long long j = 0;
+    while (j < npix) {
+        const uint32_t m0 = wxy[order[j]];
+        const int band = (int)((m0 >> 16) / kWarpBand), xa = (int)(m0 & 0xFFFFu);
+        WarpRegion R{};
+        int xb = xa;
+        long long k = j;
+        while (k < npix && k - j < kWarpRegionPx) {
+            const uint32_t m = wxy[order[k]];
+            const int x = (int)(m & 0xFFFFu);
+            if ((int)((m >> 16) / kWarpBand) != band || x - xa > span) break;
+            const int t = tile_of[order[k]];
+            int s = 0;
+            while (s < R.nslot && R.tile[s] != t) s++;
+            if (s == R.nslot) {
+                if (R.nslot == kWarpSlots) break;
+                R.tile[R.nslot++] = t;
+            }
+            xb = x;
+            rid[order[k]] = (uint32_t)regions.size();
+            k++;
+        }
+        std::sort(R.tile, R.tile + R.nslot);
+        R.gy0 = band * kWarpBand;
+        R.gx0 = quads ? (xa & ~3) : xa;
+        const int width = xb + 2 - R.gx0;
+        R.bwu = quads ? (width + 3) / 4 : width;
+        R.units = R.bwu * (kWarpBand + 1);
+        R.n = (int)(k - j);
+        regions.push_back(R);
+        j = k;
+    }
+    std::vector<uint32_t> start(regions.size() + 1, 0);
+    for (long long p = 0; p < npix; p++) start[rid[p] + 1]++;
+    for (size_t r = 0; r < regions.size(); r++) {
+        start[r + 1] += start[r];
+        regions[r].e0 = (int)start[r];
+    }
+    perm.assign((size_t)npix, 0);
+    for (long long p = 0; p < npix; p++) perm[start[rid[p]]++] = (uint32_t)p;
+}
+
+static int build_warp_regions(pf_ctx* c, int pw, int ph, long long npix)
+{
+    std::vector<uint32_t> wxy((size_t)npix);
+    HIPCHK(c, hipMemcpyAsync(wxy.data(), c->wmap.p, sizeof(uint32_t) * npix,
+                             hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    const bool quads = (pw & 3) == 0;
+    std::vector<WarpRegion> regions;
+    std::vector<uint32_t> perm;
+    size_t nwide = 0;
+    const char* cut = getenv("PF_WARP_CUT");
+    if (cut && !strcmp(cut, "pixel")) warp_cut_pixels(c, pw, ph, wxy, regions, perm);
+    else warp_cut_strips(c, pw, wxy, regions, perm, nwide);
     if (perm.size() >= (1u << 31))
         return fail(c, PF_EINVAL, "depth warp: %zu entries (< 2^31)", perm.size());
     int rc;
@@ -1250,7 +1330,7 @@ static int build_warp_regions(pf_ctx* c, int pw, int ph, long long npix)
             maxslot = std::max(maxslot, R.nslot);
         }
         fprintf(stderr, "[pf warp] %d regions (%zu wide strips), %.1f px/region, staged %.3f x "
-                "the panorama, max %d tiles/region\n", c->nregions, wide.size(),
+                "the panorama, max %d tiles/region\n", c->nregions, nwide,
                 (double)npix / regions.size(), boxf / ((double)pw * ph), maxslot);
     }
     launch_warp_entries(c->stream, (const TileGeom*)c->geom.p, (const WarpRegion*)c->wregion.p,

@@ -909,10 +909,32 @@ extern "C" int pfd_load_map(const char* fn, int is_emap, float* out, long long c
     return 0;
 }
 
-extern "C" int pfd_save_jpeg(const char* fn, const uint8_t* px, int w, int h, int c, int quality)
+extern "C" int pfd_decode_image(const char* fn, void* out, long long cap, int* w, int* h, int* c,
+                                int* is16)
+{
+    pfio::Image im;
+    std::string err;
+    if (!pfio::load_image(fn, im, err)) {
+        std::cout << "[pfd_decode_image] " << err << std::endl;
+        return -1;
+    }
+    *w = im.w;
+    *h = im.h;
+    *c = im.c;
+    *is16 = im.is16 ? 1 : 0;
+    const long long n = (long long)im.w * im.h * im.c * (im.is16 ? 2 : 1);
+    if (!out || cap < n) return -2;
+    std::memcpy(out, im.is16 ? (const void*)im.px16.data() : (const void*)im.px8.data(), n);
+    return 0;
+}
+
+extern "C" int pfd_is_16_bit(const char* fn) { return pfio::is_16bit(fn) ? 1 : 0; }
+
+extern "C" int pfd_save_jpeg(const char* fn, const uint8_t* px, int w, int h, int c, int quality,
+                             int flip)
 {
     std::string err;
-    if (!pfio::save_jpeg(fn, px, w, h, c, quality, err)) {
+    if (!pfio::save_jpeg(fn, px, w, h, c, quality, err, flip != 0)) {
         std::cout << "[pfd_save_jpeg] " << err << std::endl;
         return -1;
     }

@@ -10,6 +10,7 @@
 #include <cstring>
 #include <fstream>
 #include <iterator>
+#include <type_traits>
 
 namespace pfio {
 
@@ -34,11 +35,34 @@ int paeth(int a, int b, int c)
     return pb <= pc ? b : c;
 }
 
+// Inflate a zlib stream into exactly `need` bytes (trailing data past them is ignored, as stb
+// ignores it).
+bool inflate_exact(const std::vector<uint8_t>& z, std::vector<uint8_t>& out, size_t need)
+{
+    out.assign(need, 0);
+    z_stream zs{};
+    if (inflateInit(&zs) != Z_OK) return false;
+    zs.next_in = const_cast<Bytef*>(z.data());
+    zs.avail_in = (uInt)z.size();
+    zs.next_out = out.data();
+    zs.avail_out = (uInt)need;
+    int rc = Z_OK;
+    while (zs.avail_out > 0 && rc == Z_OK) rc = inflate(&zs, Z_NO_FLUSH);
+    inflateEnd(&zs);
+    return zs.avail_out == 0;
+}
+
+// PNG (ISO 15948) as stb_image loads it with req_comp 0: every colour type and bit depth,
+// interlaced (Adam7) or not; palette expanded to RGB (RGBA with a tRNS chunk); sub-8-bit gray
+// scaled to 0..255 (stbi__depth_scale_table {0, 0xff, 0x55, 0, 0x11}); a gray / RGB colour key
+// (tRNS) adds an alpha channel, 0 where the pixel matches the key (compared after the scaling);
+// 16-bit samples kept as 16-bit.
 bool decode_png(const std::vector<uint8_t>& f, Image& out, std::string& err)
 {
     if (f.size() < 8 || std::memcmp(f.data(), kSig, 8) != 0) return err = "not a PNG", false;
     size_t pos = 8;
     int w = 0, h = 0, depth = 0, ctype = -1, interlace = 0;
+    bool seen_ihdr = false;
     std::vector<uint8_t> idat, plte, trns;
     while (pos + 8 <= f.size()) {
         const uint32_t len = be32(&f[pos]);
@@ -52,19 +76,26 @@ bool decode_png(const std::vector<uint8_t>& f, Image& out, std::string& err)
             depth = d[8];
             ctype = d[9];
             interlace = d[12];
+            seen_ihdr = true;
+        } else if (!seen_ihdr) {
+            return err = "first chunk is not IHDR", false;
         } else if (!std::memcmp(type, "PLTE", 4)) {
+            if (len > 768 || len % 3) return err = "bad PLTE", false;
             plte.assign(d, d + len);
         } else if (!std::memcmp(type, "tRNS", 4)) {
+            if (!idat.empty()) return err = "tRNS after IDAT", false;
             trns.assign(d, d + len);
         } else if (!std::memcmp(type, "IDAT", 4)) {
             idat.insert(idat.end(), d, d + len);
         } else if (!std::memcmp(type, "IEND", 4)) {
             break;
+        } else if (!(type[0] & 0x20)) {  // unknown critical chunk
+            return err = std::string("PNG chunk not known: ") + std::string(type, 4), false;
         }
         pos += 12 + len;
     }
     if (w <= 0 || h <= 0 || w > (1 << 24) || h > (1 << 24)) return err = "bad PNG size", false;
-    if (interlace) return err = "interlaced (Adam7) PNG is not supported", false;
+    if (interlace > 1) return err = "bad PNG interlace method", false;
     int nc;
     switch (ctype) {
         case 0: nc = 1; break;
@@ -77,91 +108,127 @@ bool decode_png(const std::vector<uint8_t>& f, Image& out, std::string& err)
     if (!(depth == 1 || depth == 2 || depth == 4 || depth == 8 || depth == 16) ||
         (depth < 8 && ctype != 0 && ctype != 3) || (ctype == 3 && depth == 16))
         return err = "bad PNG bit depth", false;
-    const size_t rowbits = (size_t)w * nc * depth;
-    const size_t rowbytes = (rowbits + 7) / 8;
+    if (ctype == 3 && plte.empty()) return err = "no PLTE", false;
+    const bool key = !trns.empty() && ctype != 3;
+    if (key && (ctype == 4 || ctype == 6)) return err = "tRNS with alpha", false;
+    if (key && trns.size() != (size_t)nc * 2) return err = "bad tRNS length", false;
+    if (ctype == 3 && trns.size() > plte.size() / 3) return err = "bad tRNS length", false;
+    if (idat.empty()) return err = "no IDAT", false;
+
+    // the passes: Adam7 (T.2 / ISO 15948 8.2) or the whole image
+    struct PassGeom {
+        int x0, y0, dx, dy;
+    };
+    const PassGeom adam7[7] = {{0, 0, 8, 8}, {4, 0, 8, 8}, {0, 4, 4, 8}, {2, 0, 4, 4},
+                               {0, 2, 2, 4}, {1, 0, 2, 2}, {0, 1, 1, 2}};
+    const PassGeom whole[1] = {{0, 0, 1, 1}};
+    const PassGeom* passes = interlace ? adam7 : whole;
+    const int npass = interlace ? 7 : 1;
     const int bpp = std::max(1, nc * depth / 8);
-    std::vector<uint8_t> raw((rowbytes + 1) * (size_t)h);
-    uLongf rawlen = (uLongf)raw.size();
-    if (uncompress(raw.data(), &rawlen, idat.data(), (uLong)idat.size()) != Z_OK ||
-        rawlen != raw.size())
-        return err = "PNG inflate failed", false;
-    // unfilter in place
-    std::vector<uint8_t> img(rowbytes * (size_t)h);
-    for (int y = 0; y < h; ++y) {
-        const uint8_t ft = raw[(rowbytes + 1) * y];
-        const uint8_t* src = &raw[(rowbytes + 1) * y + 1];
-        uint8_t* cur = &img[rowbytes * y];
-        const uint8_t* prev = y ? &img[rowbytes * (y - 1)] : nullptr;
-        for (size_t i = 0; i < rowbytes; ++i) {
-            const int a = i >= (size_t)bpp ? cur[i - bpp] : 0;
-            const int b = prev ? prev[i] : 0;
-            const int c = (prev && i >= (size_t)bpp) ? prev[i - bpp] : 0;
-            int v = src[i];
-            switch (ft) {
-                case 0: break;
-                case 1: v += a; break;
-                case 2: v += b; break;
-                case 3: v += (a + b) >> 1; break;
-                case 4: v += paeth(a, b, c); break;
-                default: return err = "bad PNG filter", false;
+    size_t need = 0;
+    for (int k = 0; k < npass; ++k) {
+        const int pw = (w - passes[k].x0 + passes[k].dx - 1) / passes[k].dx;
+        const int ph = (h - passes[k].y0 + passes[k].dy - 1) / passes[k].dy;
+        if (pw > 0 && ph > 0) need += ((size_t)pw * nc * depth + 7) / 8 * ph + ph;
+    }
+    std::vector<uint8_t> raw;
+    if (!inflate_exact(idat, raw, need)) return err = "PNG inflate failed", false;
+
+    // samples as 16-bit values (8-bit and below are 0..255 after scaling; palette: indices)
+    const int scale = ctype == 0 ? (depth == 1 ? 0xFF : depth == 2 ? 0x55 : depth == 4 ? 0x11 : 1) : 1;
+    std::vector<uint16_t> smp((size_t)w * h * nc);
+    size_t rp = 0;
+    std::vector<uint8_t> prev, cur;
+    for (int k = 0; k < npass; ++k) {
+        const PassGeom& g = passes[k];
+        const int pw = (w - g.x0 + g.dx - 1) / g.dx, ph = (h - g.y0 + g.dy - 1) / g.dy;
+        if (pw <= 0 || ph <= 0) continue;
+        const size_t rowbytes = ((size_t)pw * nc * depth + 7) / 8;
+        prev.assign(rowbytes, 0);
+        cur.assign(rowbytes, 0);
+        for (int y = 0; y < ph; ++y) {
+            const uint8_t ft = raw[rp];
+            const uint8_t* src = &raw[rp + 1];
+            rp += rowbytes + 1;
+            for (size_t i = 0; i < rowbytes; ++i) {
+                const int a = i >= (size_t)bpp ? cur[i - bpp] : 0;
+                const int b = prev[i];
+                const int c = i >= (size_t)bpp ? prev[i - bpp] : 0;
+                int v = src[i];
+                switch (ft) {
+                    case 0: break;
+                    case 1: v += a; break;
+                    case 2: v += b; break;
+                    case 3: v += (a + b) >> 1; break;
+                    case 4: v += paeth(a, b, c); break;
+                    default: return err = "bad PNG filter", false;
+                }
+                cur[i] = (uint8_t)v;
             }
-            cur[i] = (uint8_t)v;
+            const int Y = g.y0 + y * g.dy;
+            for (int x = 0; x < pw; ++x) {
+                uint16_t* o = &smp[((size_t)Y * w + g.x0 + (size_t)x * g.dx) * nc];
+                for (int ch = 0; ch < nc; ++ch) {
+                    const size_t e = (size_t)x * nc + ch;
+                    int v;
+                    if (depth == 16) v = cur[2 * e] << 8 | cur[2 * e + 1];
+                    else if (depth == 8) v = cur[e];
+                    else v = ((cur[e * depth / 8] >> (8 - depth - (e * depth) % 8)) & ((1 << depth) - 1)) * scale;
+                    o[ch] = (uint16_t)v;
+                }
+            }
+            std::swap(prev, cur);
         }
     }
+
     out = Image();
     out.w = w;
     out.h = h;
     const size_t npx = (size_t)w * h;
-    if (depth == 16) {
-        out.c = nc;
-        out.is16 = true;
-        out.px16.resize(npx * nc);
-        for (int y = 0; y < h; ++y)
-            for (size_t i = 0; i < (size_t)w * nc; ++i) {
-                const uint8_t* p = &img[rowbytes * y + 2 * i];
-                out.px16[(size_t)y * w * nc + i] = (uint16_t)(p[0] << 8 | p[1]);
-            }
-        return true;
-    }
-    if (ctype == 3) {  // palette: stb expands to RGB, or RGBA when a tRNS chunk is present
+    if (ctype == 3) {  // palette: RGB, or RGBA when a tRNS chunk is present
         const int oc = trns.empty() ? 3 : 4;
         const int np = (int)plte.size() / 3;
         out.c = oc;
         out.px8.resize(npx * oc);
-        for (int y = 0; y < h; ++y)
-            for (int x = 0; x < w; ++x) {
-                const size_t bit = (size_t)x * depth;
-                const int idx = (img[rowbytes * y + bit / 8] >> (8 - depth - bit % 8)) &
-                                ((1 << depth) - 1);
-                if (idx >= np) return err = "PNG palette index out of range", false;
-                uint8_t* o = &out.px8[((size_t)y * w + x) * oc];
-                o[0] = plte[3 * idx];
-                o[1] = plte[3 * idx + 1];
-                o[2] = plte[3 * idx + 2];
-                if (oc == 4) o[3] = idx < (int)trns.size() ? trns[idx] : 255;
-            }
-        return true;
-    }
-    out.c = nc;
-    out.px8.resize(npx * nc);
-    if (depth == 8) {
-        for (int y = 0; y < h; ++y)
-            std::memcpy(&out.px8[(size_t)y * w * nc], &img[rowbytes * y], (size_t)w * nc);
-        return true;
-    }
-    // sub-8-bit gray: scaled to 0..255 (stbi__depth_scale_table {0, 0xff, 0x55, 0, 0x11})
-    const int scale = depth == 1 ? 0xFF : (depth == 2 ? 0x55 : 0x11);
-    for (int y = 0; y < h; ++y)
-        for (int x = 0; x < w; ++x) {
-            const size_t bit = (size_t)x * depth;
-            const int v = (img[rowbytes * y + bit / 8] >> (8 - depth - bit % 8)) &
-                          ((1 << depth) - 1);
-            out.px8[(size_t)y * w + x] = (uint8_t)(v * scale);
+        for (size_t i = 0; i < npx; ++i) {
+            const int idx = smp[i];
+            if (idx >= np) return err = "PNG palette index out of range", false;
+            uint8_t* o = &out.px8[i * oc];
+            o[0] = plte[3 * idx];
+            o[1] = plte[3 * idx + 1];
+            o[2] = plte[3 * idx + 2];
+            if (oc == 4) o[3] = idx < (int)trns.size() ? trns[idx] : 255;
         }
+        return true;
+    }
+    const int oc = nc + (key ? 1 : 0);
+    uint16_t kc[3] = {0, 0, 0};  // the colour key in sample units (scaled like the samples)
+    for (int ch = 0; key && ch < nc; ++ch) {
+        const int v = trns[2 * ch] << 8 | trns[2 * ch + 1];
+        kc[ch] = depth == 16 ? (uint16_t)v : (uint8_t)((v & 255) * (depth < 8 ? scale : 1));
+    }
+    out.c = oc;
+    out.is16 = depth == 16;
+    const uint16_t opaque = depth == 16 ? 65535 : 255;
+    auto emit = [&](auto& dst) {
+        dst.resize(npx * oc);
+        for (size_t i = 0; i < npx; ++i) {
+            const uint16_t* sp = &smp[i * nc];
+            for (int ch = 0; ch < nc; ++ch) dst[i * oc + ch] = (typename std::decay<decltype(dst[0])>::type)sp[ch];
+            if (key) {
+                bool match = true;
+                for (int ch = 0; ch < nc; ++ch) match = match && sp[ch] == kc[ch];
+                dst[i * oc + nc] = match ? 0 : opaque;
+            }
+        }
+    };
+    if (out.is16) emit(out.px16);
+    else emit(out.px8);
     return true;
 }
 
-// Binary PGM (P5) / PPM (P6).
+// Binary PGM (P5) / PPM (P6) as stb_image v2.23 reads them: 8-bit samples as stored (a maxval
+// below 255 is not rescaled); a maxval above 255 fails to load ("PPM image not 8-bit").
 bool decode_pnm(const std::vector<uint8_t>& f, Image& out, std::string& err)
 {
     if (f.size() < 3 || f[0] != 'P' || (f[1] != '5' && f[1] != '6'))
@@ -184,20 +251,15 @@ bool decode_pnm(const std::vector<uint8_t>& f, Image& out, std::string& err)
     ++p;  // single whitespace after maxval
     const int w = (int)vals[0], h = (int)vals[1], nc = f[1] == '5' ? 1 : 3;
     const long maxv = vals[2];
-    if (w <= 0 || h <= 0 || maxv <= 0 || maxv > 65535) return err = "bad PNM header", false;
-    const size_t n = (size_t)w * h * nc, bps = maxv > 255 ? 2 : 1;
-    if (p + n * bps > f.size()) return err = "truncated PNM", false;
+    if (w <= 0 || h <= 0 || maxv <= 0) return err = "bad PNM header", false;
+    if (maxv > 255) return err = "PPM image not 8-bit (max value > 255)", false;
+    const size_t n = (size_t)w * h * nc;
+    if (p + n > f.size()) return err = "truncated PNM", false;
     out = Image();
     out.w = w;
     out.h = h;
     out.c = nc;
-    out.is16 = bps == 2;
-    if (out.is16) {
-        out.px16.resize(n);
-        for (size_t i = 0; i < n; ++i) out.px16[i] = (uint16_t)(f[p + 2 * i] << 8 | f[p + 2 * i + 1]);
-    } else {
-        out.px8.assign(f.begin() + p, f.begin() + p + n);
-    }
+    out.px8.assign(f.begin() + p, f.begin() + p + n);
     return true;
 }
 
@@ -244,15 +306,10 @@ bool write_png(const std::string& fn, const uint8_t* rows, int w, int h, int nc,
 }  // namespace
 
 bool is_16bit(const std::string& fn)
-{
+{  // stbi_is_16_bit (stb_image v2.23): a PNG whose IHDR says 16 bits (PNM is 8-bit only there)
     std::vector<uint8_t> f;
     if (!read_file(fn, f)) return false;
-    if (f.size() >= 33 && !std::memcmp(f.data(), kSig, 8)) return f[24] == 16;
-    Image im;
-    std::string e;
-    if (f.size() > 2 && f[0] == 'P' && (f[1] == '5' || f[1] == '6') && decode_pnm(f, im, e))
-        return im.is16;
-    return false;
+    return f.size() >= 33 && !std::memcmp(f.data(), kSig, 8) && f[24] == 16;
 }
 
 bool load_image(const std::string& fn, Image& out, std::string& err)

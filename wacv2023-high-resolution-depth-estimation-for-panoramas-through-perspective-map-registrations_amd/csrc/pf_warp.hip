@@ -31,6 +31,7 @@
 #include "pf_internal.hpp"
 
 #include <cfloat>
+#include <cstdlib>
 #include <type_traits>
 
 namespace pf {
@@ -310,7 +311,7 @@ __global__ void __launch_bounds__(kWB) k_warp_depth(const TileGeom* __restrict__
                                                     int ph, long long pstride,
                                                     const Resp* __restrict__ resp,
                                                     float* __restrict__ tiles,
-                                                    long long tstride, int batch)
+                                                    long long tstride, int batch, int order)
 {
     __shared__ __attribute__((aligned(16))) float box[2 * kBoxFloats];
     __shared__ RespK rk[kNB * kWarpSlots];  // published by the first barrier inside warp_region
@@ -318,8 +319,8 @@ __global__ void __launch_bounds__(kWB) k_warp_depth(const TileGeom* __restrict__
     // then column): neighbouring boxes' shared rows/columns and a region's entries hit in L2
     const unsigned nchunk = (unsigned)((batch + kNB - 1) / kNB);
     const unsigned lb = xcd_remap(blockIdx.x, gridDim.x);
-    const WarpRegion R = regions[lb / nchunk];
-    const int chunk = (int)(lb % nchunk);
+    const WarpRegion R = regions[order ? lb % (unsigned)nregions : lb / nchunk];
+    const int chunk = (int)(order ? lb / (unsigned)nregions : lb % nchunk);
     const int t = threadIdx.x;
     const int bbeg = chunk * kNB;
     const int nb = min(kNB, batch - bbeg);
@@ -455,8 +456,10 @@ void launch_warp_depth(hipStream_t s, const TileGeom* geom, int ntiles, const Wa
                        int batch)
 {
     const long long n = (long long)nregions * ((batch + kNB - 1) / kNB);
+    static const int order = getenv("PF_WARP_ORDER") ? atoi(getenv("PF_WARP_ORDER")) : 0;
     hipLaunchKernelGGL(k_warp_depth, dim3((unsigned)n), dim3(kWB), 0, s, geom, ntiles, regions,
-                       nregions, entries, pano, pw, ph, pstride, resp, tiles, tstride, batch);
+                       nregions, entries, pano, pw, ph, pstride, resp, tiles, tstride, batch,
+                       order);
 }
 
 }  // namespace pf
