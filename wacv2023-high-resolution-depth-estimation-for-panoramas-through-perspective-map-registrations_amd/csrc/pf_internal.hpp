@@ -74,10 +74,10 @@ struct Resp {
 // kWarpBand rows, then column, and cut into regions of at most kWarpRegionPx pixels whose
 // joint corner footprint (+1 row/column) fits the LDS box of kWarpRows x kWarpPitch floats.
 // Built once per (layout, panorama size) on the host (pf_api.hip build_warp_regions).
-constexpr int kWarpStrip = 32;
+constexpr int kWarpStrip = 16;   // 64 B: the granule the L2 writes back
 constexpr int kWarpBand = 8;        // panorama rows per band (the sort key)
-constexpr int kWarpRows = 14;       // max rows of a staged box
-constexpr int kWarpPitch = 192;     // LDS row pitch of a staged box, floats (a multiple of 64:
+constexpr int kWarpRows = 20;       // max rows of a staged box
+constexpr int kWarpPitch = 128;     // LDS row pitch of a staged box, floats (a multiple of 64:
                                     // c00/c10 and c01/c11 are ds_read2st64 pairs)
 constexpr int kWarpRegionPx = 1024; // max tile pixels per region (4 per thread)
 constexpr int kWarpSlots = 8;       // max distinct tiles per region

@@ -48,6 +48,9 @@
 #ifndef PF_JLAG_PF
 #define PF_JLAG_PF 2  // steps of lead for the input and L row loads (1 or 2)
 #endif
+#ifndef PF_JLREG_T
+#define PF_JLREG_T 5  // passes of depth <= this keep their L ring in registers instead of LDS
+#endif
 
 namespace pf {
 
@@ -140,6 +143,11 @@ struct JLag {
     // ring of R >= 2T+1 rows, R a multiple of 6: the loop body is unrolled over the R/6 groups
     // of 6 steps so every ring slot is a compile-time constant (LDS immediate offsets, no SALU)
     static constexpr int R = (2 * T + 1 + 5) / 6 * 6, NG = R / 6;
+    // Shallow passes (the coarse levels: few waves, latency-bound) keep the L ring in registers
+    // -- every slot index is a compile-time constant of the unrolled step -- so no LDS store /
+    // load latency sits on a step's dependency chain; deep passes keep it in LDS (VGPR budget).
+    static constexpr bool LREG = T <= PF_JLREG_T;
+    Row<C> Lr[LREG ? R : 1];  // LREG: ring slot s = Lr[s]
     Row<C> H[T][3];   // H[t][r % 3] = level t row r
     Row<C> In[NB];    // input row r lands in In[r % NB] (issued at step r + 1 - PF)
     Row<C> Lin[NB];   // L row r lands in Lin[r % NB] (issued at step r - PF), to LDS at step r
@@ -234,6 +242,26 @@ struct JLag {
         if constexpr (C == 2) *reinterpret_cast<float2*>(p) = make_float2(r.v[0], r.v[1]);
         else *reinterpret_cast<float4*>(p) = make_float4(r.v[0], r.v[1], r.v[2], r.v[3]);
     }
+    // the L ring: row k of the group (slot GB + PH) enters; level t reads row k - 2t
+    template <int GB, int PH>
+    __device__ __forceinline__ void ring_put(Row<C> r)
+    {
+        if constexpr (LREG) {
+            if constexpr (FAST) {
+#pragma unroll
+                for (int j = 0; j < C; j++) r.v[j] = __builtin_isfinite(r.v[j]) ? r.v[j] : 0.0f;
+            }
+            Lr[((GB + PH) % R + R) % R] = r;
+        } else {
+            lds_put(lslot<GB, PH>(), r);
+        }
+    }
+    template <int GB, int PH, int TT>
+    __device__ __forceinline__ Row<C> ring_get() const
+    {
+        if constexpr (LREG) return Lr[((GB + PH - 2 * TT) % R + R) % R];
+        else return lds_get(lslot_t<GB, PH>(TT));
+    }
     __device__ __forceinline__ Row<C> lds_get(const float* p) const
     {
         Row<C> r;
@@ -245,6 +273,16 @@ struct JLag {
             r.v[0] = q.x; r.v[1] = q.y; r.v[2] = q.z; r.v[3] = q.w;
         }
         return r;
+    }
+
+    // Lv[t - TA] = L row of level t for t in [TA, TB] (compile-time t)
+    template <int GB, int PH, int TA, int TB>
+    __device__ __forceinline__ void ring_get_range(Row<C>* Lv) const
+    {
+        if constexpr (TA <= TB) {
+            Lv[0] = ring_get<GB, PH, TA>();
+            ring_get_range<GB, PH, TA + 1, TB>(Lv + 1);
+        }
     }
 
     // general form: T*C scalar updates, stage-wise so consecutive VALU instructions belong to
@@ -461,8 +499,7 @@ struct JLag {
 #endif
         {
             Row<C> Lv[T1 - T0];
-#pragma unroll
-            for (int t = T0 + 1; t <= T1; t++) Lv[t - 1 - T0] = lds_get(lslot_t<GB, PH>(t));
+            ring_get_range<GB, PH, T0 + 1, T1>(Lv);
             if constexpr (C == 4) sweep_packed_group4<PH, T0, T1, ROWS>(Lv, nw, k);
             else sweep_packed_group<PH, T0, T1, ROWS>(Lv, nw, k);
         }
@@ -476,7 +513,7 @@ struct JLag {
         H[0][slot(PH, 1)] = In[(PH + NB - 1) % NB];
         // L row k (landed in Lin last step) goes to its ring slot; fetch L row k+PF.  The slot
         // is reused by row k+R > k, after every level has read row k (last read at k + 2T).
-        lds_put(lslot<GB, PH>(), Lin[PH % NB]);
+        ring_put<GB, PH>(Lin[PH % NB]);
 #if PF_JDBG_NOGLOBAL  // profiling only (wrong results): no global loads in the loop
         Lin[(PH + PF) % NB] = H[T - 1][slot(PH, 1)];
         In[(PH + PF - 1) % NB] = H[T - 2][slot(PH, 2)];
@@ -490,8 +527,7 @@ struct JLag {
             sweep_packed<PH, GB, 0, ROWS>(nw, k);
         } else {
             Row<C> Lv[T];
-#pragma unroll
-            for (int t = 1; t <= T; t++) Lv[t - 1] = lds_get(lslot_t<GB, PH>(t));
+            ring_get_range<GB, PH, 1, T>(Lv);
             sweep_general<PH>(Lv, nw);
         }
 #pragma unroll
@@ -613,8 +649,16 @@ __global__ void __launch_bounds__(256, PF_JLAG_WAVES) k_jlag(JacobiPass P)
 #pragma unroll
         for (int j = 0; j < C; j++) { S.In[q].v[j] = 0.0f; S.Lin[q].v[j] = 0.0f; }
     constexpr int R = S_t::R;
-    __shared__ float lds_l[4 * R * 64 * C];  // per-wave private rings, no barriers needed
-    S.lring = lds_l + wave * (R * 64 * C);
+    if constexpr (S_t::LREG) {
+#pragma unroll
+        for (int q = 0; q < R; q++)
+#pragma unroll
+            for (int j = 0; j < C; j++) S.Lr[q].v[j] = 0.0f;
+        S.lring = nullptr;
+    } else {
+        __shared__ float lds_l[4 * R * 64 * C];  // per-wave private rings, no barriers needed
+        S.lring = lds_l + wave * (R * 64 * C);
+    }
     S.lane_c = lane * C;
     // steps k0 .. kend: level 0 needs rows from r0 - T, the last output row r1-1 finishes at
     // step r1 - 1 + 2T; k0 is rounded down to a multiple of 6 so ring slots are static.

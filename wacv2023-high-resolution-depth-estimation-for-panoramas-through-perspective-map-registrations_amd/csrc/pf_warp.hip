@@ -319,7 +319,8 @@ __global__ void __launch_bounds__(kWB) k_warp_depth(const TileGeom* __restrict__
     // then column): neighbouring boxes' shared rows/columns and a region's entries hit in L2
     const unsigned nchunk = (unsigned)((batch + kNB - 1) / kNB);
     const unsigned lb = xcd_remap(blockIdx.x, gridDim.x);
-    const WarpRegion R = regions[order ? lb % (unsigned)nregions : lb / nchunk];
+    // by reference: a private copy of tile[] would be indexed dynamically, i.e. live in scratch
+    const WarpRegion& R = regions[order ? lb % (unsigned)nregions : lb / nchunk];
     const int chunk = (int)(order ? lb / (unsigned)nregions : lb % nchunk);
     const int t = threadIdx.x;
     const int bbeg = chunk * kNB;
@@ -406,7 +407,7 @@ __global__ void __launch_bounds__(kWB) k_warp_entries(const TileGeom* __restrict
                                                       const float2* __restrict__ wfxy, int pw,
                                                       int ph, WarpEntry* __restrict__ entries)
 {
-    const WarpRegion R = regions[blockIdx.x];
+    const WarpRegion& R = regions[blockIdx.x];
     for (int e = threadIdx.x; e < R.n; e += kWB) {
         const uint32_t p = perm[R.e0 + e];
         WarpEntry E{0xFFFFFFFFu, 0u, 0.0f, 0.0f};
