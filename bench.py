@@ -55,6 +55,13 @@ def parse():
                     help="1: software-pipelined steps -- the warp of batch k+1 (second stream) "
                          "runs while batch k is registered and fused; every step still warps, "
                          "registers and fuses one whole batch")
+    ap.add_argument("--backend", choices=("nccl", "gloo"), default="nccl",
+                    help="torch.distributed backend for N > 1: nccl (= RCCL over xGMI, the "
+                         "default) or gloo with host-staged tensors (several ranks sharing one "
+                         "GPU: RCCL refuses a duplicate device)")
+    ap.add_argument("--same-device", action="store_true",
+                    help="every rank on cuda:0 (multi-process rehearsal on a one-GPU box; "
+                         "use with --backend gloo)")
     ap.add_argument("--stand-in", action="store_true",
                     help="test hook (tests/test_bench_dist.py): the launcher, seeding and timing "
                          "path with a CPU stand-in step over gloo; no GPU is touched")
@@ -177,7 +184,7 @@ def run_c5(args, rank, world, local, dev):
             mine = tiles[:, off0:off1]
             fs.warp_depth(gt, mine, resp)
             fs.register(emap, mine, zr, degree=3, apply=False, coeffs=coeffs[t0:t1][None])
-        comm = pf_dist.TorchComm(dist) if world > 1 else None
+        comm = pf_dist.TorchComm(dist, stage_host=args.backend == "gloo") if world > 1 else None
         if args.c5_shard == "rows":
             be = pf_dist.HipRowShardBackend(fz, emap, tiles, coeffs, out_w, zr, out.view(-1))
             pf_dist.fuse_row_sharded(be, nlevels, lay.ntiles, rank, world, comm)
@@ -198,10 +205,22 @@ def run_c5(args, rank, world, local, dev):
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - ts
+    mine_s = elapsed
     if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        t = torch.tensor([elapsed], dtype=torch.float64,
+                         device=dev if args.backend == "nccl" else "cpu")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
+    bit_exact = None
+    if rank == 0:
+        # after the timed steps: the same panorama fused on this GPU alone (every tile warped
+        # and registered here, pf_merge) must equal the sharded result bit for bit
+        full = torch.zeros_like(tiles)
+        fz.warp_depth(gt, full, panofuse.make_responses(resp_all, dev))
+        ref = torch.empty_like(out)
+        fz.merge(emap, full, ref[None], zr, coeffs=torch.zeros_like(coeffs)[None])
+        torch.cuda.synchronize()
+        bit_exact = bool(torch.equal(ref, out))
     if rank == 0:
         nz = int((out != 0).sum().item())
         print(json.dumps({
@@ -217,10 +236,14 @@ def run_c5(args, rank, world, local, dev):
                                       "with halo exchange per pass" if args.c5_shard == "rows"
                                       else "(sum L, n) reduce to rank 0 (RCCL), Jacobi on rank 0"),
                        "parallelism": f"{'row-band' if args.c5_shard == 'rows' else 'tile'}-sharded x{world}"},
-            "nonzero_px": nz}), flush=True)
+            "nonzero_px": nz, "bit_exact_vs_one_gpu": bit_exact,
+            "backend": args.backend if world > 1 else None,
+            "elapsed_rank0_s": mine_s}), flush=True)
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()
+    if rank == 0 and not bit_exact:
+        sys.exit("C5: the sharded result differs from the one-GPU fusion")
 
 
 def rank_seeds(batch, rank):
@@ -285,7 +308,8 @@ def timed_steps(step, sync, args, world, dist, device=None):
     elapsed = mine
     if world > 1:
         import torch
-        t = torch.tensor([mine], dtype=torch.float64, device=device)
+        on_dev = device is not None and dist.get_backend() != "gloo"
+        t = torch.tensor([mine], dtype=torch.float64, device=device if on_dev else "cpu")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
     return mine, elapsed
@@ -334,8 +358,13 @@ def main():
         if world > 1:
             dist.init_process_group("gloo")
         return run_stand_in(args, rank, world)
+    if args.same_device:
+        local = 0
     if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local}"))
+        if args.backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local}"))
+        else:
+            dist.init_process_group("gloo")
     torch.cuda.set_device(local)
     dev = torch.device(f"cuda:{local}")
     if args.mode == "c5":
@@ -362,9 +391,9 @@ def main():
 
     if args.pipeline:
         pstep = pipelined_step(fz, lay, local, dev, gt, emap, resp, tiles, out, coeffs, zr)
-        _, elapsed = timed_steps(pstep, torch.cuda.synchronize, args, world, dist, dev)
+        mine_s, elapsed = timed_steps(pstep, torch.cuda.synchronize, args, world, dist, dev)
     else:
-        _, elapsed = timed_steps(step, torch.cuda.synchronize, args, world, dist, dev)
+        mine_s, elapsed = timed_steps(step, torch.cuda.synchronize, args, world, dist, dev)
     # Per-kernel roofline: the same steps again with the library's hipEvent stage timers on
     # (recorded on the stream the kernels run on).  With the timers on, the library runs each
     # batch unsplit (no half-batch stream overlap), so every stage's time is its own.
@@ -387,6 +416,20 @@ def main():
     metrics_seq_ms = fz.profile_read()["metrics"][0]
     fz.profile(False)
     nprof = max(1, args.prof_steps)
+    # SolveDepthBySmoothing (Depth.cpp:1773-1878, an ablation the reference leaves disabled):
+    # not part of the step; its cost at batch 1 and at the step's batch, for the record.
+    smooth = {}
+    for nb in sorted({1, B}):
+        o_s = torch.empty((nb, out_w // 2, out_w), dtype=torch.int16, device=dev)
+        fz.solve_smoothing(tiles[:nb], o_s, zr, coeffs=coeffs[:nb])  # first call: layout tables
+        torch.cuda.synchronize()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        fz.solve_smoothing(tiles[:nb], o_s, zr, coeffs=coeffs[:nb])
+        e1.record()
+        torch.cuda.synchronize()
+        smooth[f"batch{nb}_ms"] = e0.elapsed_time(e1)
+        del o_s
 
     total_panos = B * world * args.steps
     value = total_panos / elapsed
@@ -399,8 +442,24 @@ def main():
     stages = {k: {"ms_per_step": v[0] / nprof,
                   "GBps": (v[1] / (v[0] * 1e-3) / 1e9) if v[0] > 0 else 0.0,
                   "launches_per_step": v[2] / nprof} for k, v in prof.items()}
-    # sanity: outputs are populated
+    # sanity: outputs are populated, and equal to a fresh one-process fusion of the same batch
     nz = int((out[0].view(torch.int16) != 0).sum().item())
+    bit_exact = None
+    if rank == 0:
+        fref = panofuse.Fuser(local)
+        fref.set_tiles(lay)
+        t_ref = torch.empty_like(tiles)
+        o_ref = torch.empty_like(out)
+        fref.warp_depth(gt, t_ref, resp)
+        fref.merge(emap, t_ref, o_ref, zr, coeffs=torch.empty_like(coeffs))
+        torch.cuda.synchronize()
+        bit_exact = bool(torch.equal(o_ref, out))
+        del fref, t_ref, o_ref
+    per_rank = None
+    if world > 1:  # each rank's seed block and its own time (the line's value uses the MAX)
+        per_rank = [None] * world
+        dist.all_gather_object(per_rank, {"rank": rank, "seed0": seeds[0], "seedN": seeds[-1],
+                                          "elapsed_s": mine_s})
 
     if rank == 0:
         line = {
@@ -475,6 +534,11 @@ def main():
                                                "default, bit-exact means): terms in parallel, "
                                                "one lane per panorama adds them in order"},
             "nonzero_px_pano0": nz,
+            "smoothing_ablation": dict(smooth, note="pf_solve_smoothing (SolveDepthBySmoothing, "
+                                       "500 Gauss-Seidel sweeps near tile edges), outside the step"),
+            "bit_exact_vs_one_process": bit_exact,
+            "backend": args.backend if world > 1 else None,
+            "per_rank": per_rank,
         }
         if not args.no_cpu_baseline:
             line["cpu_baseline"] = cpu_baseline(args.cpu_seconds)
@@ -482,6 +546,8 @@ def main():
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()
+    if rank == 0 and not bit_exact:
+        sys.exit("the fused batch differs from a fresh one-process fusion")
 
 
 if __name__ == "__main__":

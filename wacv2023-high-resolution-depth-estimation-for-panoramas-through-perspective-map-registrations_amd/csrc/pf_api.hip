@@ -69,10 +69,11 @@ struct pf_ctx {
     LevelCache lc;
     bool reg_valid = false;
     uint32_t reg_zr0 = 0, reg_zr1 = 0;
-    // E->P depth warp for one panorama size (pf_warp.hip): per tile pixel the bilinear corner
-    // and (fx, fy) weights, the panorama regions and their pixel entries; built on first use
-    int wmap_pw = 0, wmap_ph = 0, nregions = 0;
-    DevBuf wmap, wfxy, wregion, wperm, wentry;
+    // E->P depth warp for one panorama size (pf_warp.hip): tile patches with their panorama
+    // boxes, per tile pixel the corner index in its box and the (fx, fy) weights; built on
+    // first use
+    int wmap_pw = 0, wmap_ph = 0, npatch = 0;
+    DevBuf wmap, wfxy, wpatch;
     // workspace
     DevBuf buf[3], lnorm, coeffs, lsum_ws, metrics_ws, reg_sums, reg_active;
     // SolveDepthBySmoothing (pf_smooth.hip): boxes, grid tables, per-pixel source and mask
@@ -292,7 +293,7 @@ void pf_destroy(pf_ctx* c)
     (void)hipStreamSynchronize(c->stream);
     DevBuf* all[] = {&c->geom, &c->reg, &c->rcols, &c->rrows, &c->cams, &c->rgb_off,
                      &c->buf[0], &c->buf[1], &c->buf[2], &c->lnorm, &c->coeffs, &c->lsum_ws,
-                     &c->wmap, &c->wfxy, &c->wregion, &c->wperm, &c->wentry, &c->metrics_ws, &c->reg_sums,
+                     &c->wmap, &c->wfxy, &c->wpatch, &c->metrics_ws, &c->reg_sums,
                      &c->reg_active};
     for (DevBuf* b : all) release(*b);
     for (int l = 0; l < 4; l++) {
@@ -480,7 +481,14 @@ int pf_set_tiles(pf_ctx* c, const pf_window* fovs, const pf_window* ranges, int 
     c->lc.out_w = 0;  // boxes and registration grids depend on the ranges: rebuild lazily
     c->reg_valid = false;
     c->wmap_pw = c->wmap_ph = 0;
+    std::vector<WarpPatch> patches;
+    const int pe = warp_patch_edge();
+    for (int i = 0; i < ntiles; i++)
+        for (int y = 0; y < tile_h[i]; y += pe)
+            for (int x = 0; x < tile_w[i]; x += pe) patches.push_back(WarpPatch{i, x, y, 0, 0, 0, 0, 0});
+    c->npatch = (int)patches.size();
     int rc;
+    if ((rc = upload(c, c->wpatch, patches))) return rc;
     if ((rc = upload(c, c->geom, c->geom_h))) return rc;
     if ((rc = upload(c, c->cams, cams))) return rc;
     if ((rc = upload(c, c->rgb_off, rgb_off))) return rc;
@@ -828,8 +836,9 @@ static int jacobi_tcap(const LevelDims& L)
 
 // SRC_SEED passes: ValueAtCoord's index (emap_index) split into its column term x * ec and row
 // term y * ew * ec over the level's grid (the az / zen of grid_tables, then emap_index's fp64
-// expression), cached per (level size, emap size).  Returns PF_OK or the upload's error.
-static int seed_tables(pf_ctx* c, const LevelDims& L, int ew, int eh, int ec, JacobiPass& P)
+// expression), cached per (level size, emap size).  Built by fuse_range before the level's
+// timed Jacobi stage (the upload synchronises the stream); returns PF_OK or the upload's error.
+static int seed_tables(pf_ctx* c, const LevelDims& L, int ew, int eh, int ec)
 {
     const int key[5] = {L.w, L.h, ew, eh, ec};
     if (memcmp(key, c->seed_key, sizeof(key)) != 0) {
@@ -846,8 +855,6 @@ static int seed_tables(pf_ctx* c, const LevelDims& L, int ew, int eh, int ec, Ja
         if ((rc = upload(c, c->seed_ecol, ecol)) || (rc = upload(c, c->seed_erow, erow))) return rc;
         memcpy(c->seed_key, key, sizeof(key));
     }
-    P.ecol = (const int*)c->seed_ecol.p;
-    P.erow = (const int*)c->seed_erow.p;
     return PF_OK;
 }
 
@@ -878,7 +885,12 @@ static float* run_jacobi(pf_ctx* c, const LevelDims& L, int first, const float* 
         }
     }
     JacobiPass P{};
-    if (first == 2 && emap && seed_tables(c, L, ew, eh, ec, P)) return nullptr;
+    if (first == 2 && emap) {  // the tables seed_tables() built for this level and emap
+        const int key[5] = {L.w, L.h, ew, eh, ec};
+        if (memcmp(key, c->seed_key, sizeof(key)) != 0) return nullptr;
+        P.ecol = (const int*)c->seed_ecol.p;
+        P.erow = (const int*)c->seed_erow.p;
+    }
     P.prev = prev; P.pstride = pstride;
     P.emap = emap; P.estride = estride; P.ew = ew; P.eh = eh; P.ec = ec;
     P.cols = cols; P.rows = rows;
@@ -1063,6 +1075,10 @@ static int fuse_range(pf_ctx* c, const float* emap, int ew, int eh, int ec, cons
                 launch_border(c->stream, l == 0 ? nullptr : prev, pst, L, a, b, st,
                               last ? out : nullptr, plane, batch);
             }
+            if (l == 0) {  // outside the timed stage: the first call per emap size uploads
+                int rc;
+                if ((rc = seed_tables(c, L, ew, eh, ec))) return rc;
+            }
             {
                 // 12 B per pixel-update (read b, read L, write b'), SURVEY.md 8d
                 StageTimer t(c, PF_STAGE_JACOBI, B * 12.0 * band * L.iters, L.iters);
@@ -1073,7 +1089,7 @@ static int fuse_range(pf_ctx* c, const float* emap, int ew, int eh, int ec, cons
                                  lc.full[l] ? (const float*)lc.hcol[l].p : nullptr);
                 t.set_launches(passes);  // k_jlag launches (rocprof's count for that kernel)
             }
-            if (!res) return PF_ENOMEM;  // the seed tables' upload failed (message in c->err)
+            if (!res) return fail(c, PF_EINVAL, "level-0 seed tables missing");
         }
         prev = res;
     }
@@ -1100,244 +1116,26 @@ static int fuse_impl(pf_ctx* c, const float* emap, int ew, int eh, int ec, const
                       (float*)c->lnorm.p);
 }
 
-// Once per (layout, panorama size): the depth warp's regions (pf_warp.hip).  Every tile row is
-// cut into aligned strips of kWarpStrip pixels; a strip's footprint is the box of its pixels'
-// bilinear corners (azimuth unwrapped around its first pixel).  Strips are sorted by (band of
-// kWarpBand rows of the footprint's centre, centre column) -- so strips of different tiles that
-// look at the same panorama lines end up together -- and cut greedily into regions of at most
-// kWarpRegionPx pixels and kWarpSlots tiles whose joint footprint, +1 row and column (and the
-// column alignment of quad staging), fits kWarpRows x kWarpPitch.  Inside a region the strips
-// are in layout order.  A strip whose own footprint does not fit goes to a "wide" region (direct
-// gathers).  Regions are ordered by band, then column, so neighbouring boxes, which share
-// lines, are staged by neighbouring blocks.
-// Strip cut: see build_warp_regions.
-static void warp_cut_strips(pf_ctx* c, int pw, const std::vector<uint32_t>& wxy,
-                            std::vector<WarpRegion>& regions, std::vector<uint32_t>& perm,
-                            size_t& nwide)
+// Once per (layout, panorama size): order the warp patches by panorama footprint -- 32-row bands
+// of the box centre, then its azimuth -- instead of tile by tile.  The blocks resident on one XCD
+// then stage overlapping boxes (neighbouring patches of a tile and the overlapping patches of the
+// neighbouring tiles) at about the same time, so a panorama line is fetched from HBM once and
+// re-read from that XCD's L2 instead of once per box that holds it (the boxes hold each panorama
+// pixel ~3 times at the C2 layout).  Patches are self-describing, so the permutation is free.
+static int sort_warp_patches(pf_ctx* c, int pw)
 {
-    const bool quads = (pw & 3) == 0;
-    auto wrap = [pw](int d) {
-        if (d > pw / 2) d -= pw;
-        if (d < -(pw / 2)) d += pw;
-        return d;
-    };
-    struct Strip {
-        int tile, len, xref, umin, umax, ymin, ymax;
-        uint32_t p0;
-        long long key;
-    };
-    std::vector<Strip> strips;
-    strips.reserve(wxy.size() / kWarpStrip + (size_t)c->ntiles * 64);
-    for (int t = 0; t < c->ntiles; t++) {
-        const TileGeom& g = c->geom_h[t];
-        for (int Y = 0; Y < g.h; Y++)
-            for (int X0 = 0; X0 < g.w; X0 += kWarpStrip) {
-                Strip S;
-                S.tile = t;
-                S.len = std::min(kWarpStrip, g.w - X0);
-                S.p0 = (uint32_t)(g.pix_off + (long long)Y * g.w + X0);
-                S.xref = (int)(wxy[S.p0] & 0xFFFFu);
-                S.umin = S.umax = 0;
-                S.ymin = INT32_MAX;
-                S.ymax = INT32_MIN;
-                for (int j = 0; j < S.len; j++) {
-                    const uint32_t m = wxy[S.p0 + j];
-                    const int du = wrap((int)(m & 0xFFFFu) - S.xref), y = (int)(m >> 16);
-                    S.umin = std::min(S.umin, du);
-                    S.umax = std::max(S.umax, du);
-                    S.ymin = std::min(S.ymin, y);
-                    S.ymax = std::max(S.ymax, y);
-                }
-                int xc = S.xref + (S.umin + S.umax) / 2;
-                xc = ((xc % pw) + pw) % pw;
-                S.key = (long long)((S.ymin + S.ymax) / 2 / kWarpBand) * pw + xc;
-                strips.push_back(S);
-            }
-    }
-    std::stable_sort(strips.begin(), strips.end(),
-                     [](const Strip& a, const Strip& b) { return a.key < b.key; });
-    const int slack = quads ? 3 : 0;  // columns added by aligning the box origin to a quad
-    auto fits = [&](int u0, int u1, int y0, int y1) {
-        return u1 - u0 + 2 + slack <= kWarpPitch && y1 - y0 + 2 <= kWarpRows;
-    };
-    std::vector<std::vector<int>> members;  // strip indices per region
-    std::vector<int> wide;
-    size_t k = 0;
-    while (k < strips.size()) {
-        if (!fits(strips[k].umin, strips[k].umax, strips[k].ymin, strips[k].ymax)) {
-            wide.push_back((int)k++);
-            continue;
-        }
-        WarpRegion R{};
-        const int xr = strips[k].xref;
-        int U0 = INT32_MAX, U1 = INT32_MIN, Y0 = INT32_MAX, Y1 = INT32_MIN, px = 0;
-        std::vector<int> mem;
-        while (k < strips.size()) {
-            const Strip& S = strips[k];
-            if (!fits(S.umin, S.umax, S.ymin, S.ymax)) break;  // wide: handled by the outer loop
-            const int off = wrap(S.xref - xr);
-            const int u0 = std::min(U0, off + S.umin), u1 = std::max(U1, off + S.umax);
-            const int y0 = std::min(Y0, S.ymin), y1 = std::max(Y1, S.ymax);
-            if (px + kWarpStrip > kWarpRegionPx || !fits(u0, u1, y0, y1)) break;
-            int s = 0;
-            while (s < R.nslot && R.tile[s] != S.tile) s++;
-            if (s == R.nslot) {
-                if (R.nslot == kWarpSlots) break;
-                R.tile[R.nslot++] = S.tile;
-            }
-            U0 = u0; U1 = u1; Y0 = y0; Y1 = y1;
-            px += kWarpStrip;
-            mem.push_back((int)k++);
-        }
-        std::sort(R.tile, R.tile + R.nslot);  // slot order = tile order (k_warp_entries)
-        int gx0 = ((xr + U0) % pw + pw) % pw;
-        const int a = quads ? (gx0 & 3) : 0;
-        gx0 -= a;
-        const int width = U1 - U0 + 2 + a;
-        R.gx0 = gx0;
-        R.gy0 = Y0;
-        R.bwu = quads ? (width + 3) / 4 : width;
-        R.units = R.bwu * (Y1 - Y0 + 2);
-        regions.push_back(R);
-        members.push_back(std::move(mem));
-    }
-    for (size_t w = 0; w < wide.size(); w += kWarpRegionPx / kWarpStrip) {
-        WarpRegion R{};
-        R.wide = 1;
-        std::vector<int> mem;
-        for (size_t j = w; j < std::min(wide.size(), w + kWarpRegionPx / kWarpStrip); j++) {
-            const int t = strips[wide[j]].tile;
-            int s = 0;
-            while (s < R.nslot && R.tile[s] != t) s++;
-            if (s == R.nslot) {
-                if (R.nslot == kWarpSlots) break;
-                R.tile[R.nslot++] = t;
-            }
-            mem.push_back(wide[j]);
-        }
-        w -= kWarpRegionPx / kWarpStrip - mem.size();  // a slot-limited region ends early
-        std::sort(R.tile, R.tile + R.nslot);
-        regions.push_back(R);
-        members.push_back(std::move(mem));
-    }
-    // entries: each region's strips in layout order, kWarpStrip entries per strip
-    perm.reserve(strips.size() * kWarpStrip);
-    for (size_t r = 0; r < regions.size(); r++) {
-        std::vector<int>& mem = members[r];
-        std::sort(mem.begin(), mem.end(),
-                  [&](int x, int y) { return strips[x].p0 < strips[y].p0; });
-        regions[r].e0 = (int)perm.size();
-        regions[r].n = (int)mem.size() * kWarpStrip;
-        for (int m : mem)
-            for (int j = 0; j < kWarpStrip; j++)
-                perm.push_back(j < strips[m].len ? strips[m].p0 + j : 0xFFFFFFFFu);
-    }
-    nwide = wide.size();
-}
-// Pixel cut (PF_WARP_CUT=pixel): every tile pixel goes to the region of its own corner --
-// bands of kWarpBand rows cut along their columns into regions of at most kWarpRegionPx pixels
-// and an x0 span that fits the box -- via two counting sorts (by band and column, then stably by
-// region, so a region's pixels are in layout order).  Stages each panorama line about once, but a
-// region's tile-row runs start and end anywhere in a 128-B line.
-static void warp_cut_pixels(pf_ctx* c, int pw, int ph, const std::vector<uint32_t>& wxy,
-                            std::vector<WarpRegion>& regions, std::vector<uint32_t>& perm)
-{
-    const long long npix = (long long)wxy.size();
-    const bool quads = (pw & 3) == 0;
-    std::vector<int> tile_of((size_t)npix);
-    for (int t = 0; t < c->ntiles; t++) {
-        const TileGeom& g = c->geom_h[t];
-        std::fill(tile_of.begin() + g.pix_off, tile_of.begin() + g.pix_off + (long long)g.w * g.h,
-                  t);
-    }
-    const int nband = (ph + kWarpBand - 1) / kWarpBand;
-    const size_t nbins = (size_t)nband * pw;
-    std::vector<uint32_t> cnt(nbins + 1, 0);
-    auto key = [&](uint32_t m) { return (size_t)((m >> 16) / kWarpBand) * pw + (m & 0xFFFFu); };
-    for (long long p = 0; p < npix; p++) cnt[key(wxy[p]) + 1]++;
-    for (size_t k = 0; k < nbins; k++) cnt[k + 1] += cnt[k];
-    std::vector<uint32_t> order((size_t)npix);
-    for (long long p = 0; p < npix; p++) order[cnt[key(wxy[p])]++] = (uint32_t)p;
-    const int span = kWarpPitch - 2 - (quads ? 3 : 0);
-    std::vector<uint32_t> rid((size_t)npix);
-    long long j = 0;
-    while (j < npix) {
-        const uint32_t m0 = wxy[order[j]];
-        const int band = (int)((m0 >> 16) / kWarpBand), xa = (int)(m0 & 0xFFFFu);
-        WarpRegion R{};
-        int xb = xa;
-        long long k = j;
-        while (k < npix && k - j < kWarpRegionPx) {
-            const uint32_t m = wxy[order[k]];
-            const int x = (int)(m & 0xFFFFu);
-            if ((int)((m >> 16) / kWarpBand) != band || x - xa > span) break;
-            const int t = tile_of[order[k]];
-            int s = 0;
-            while (s < R.nslot && R.tile[s] != t) s++;
-            if (s == R.nslot) {
-                if (R.nslot == kWarpSlots) break;
-                R.tile[R.nslot++] = t;
-            }
-            xb = x;
-            rid[order[k]] = (uint32_t)regions.size();
-            k++;
-        }
-        std::sort(R.tile, R.tile + R.nslot);
-        R.gy0 = band * kWarpBand;
-        R.gx0 = quads ? (xa & ~3) : xa;
-        const int width = xb + 2 - R.gx0;
-        R.bwu = quads ? (width + 3) / 4 : width;
-        R.units = R.bwu * (kWarpBand + 1);
-        R.n = (int)(k - j);
-        regions.push_back(R);
-        j = k;
-    }
-    std::vector<uint32_t> start(regions.size() + 1, 0);
-    for (long long p = 0; p < npix; p++) start[rid[p] + 1]++;
-    for (size_t r = 0; r < regions.size(); r++) {
-        start[r + 1] += start[r];
-        regions[r].e0 = (int)start[r];
-    }
-    perm.assign((size_t)npix, 0);
-    for (long long p = 0; p < npix; p++) perm[start[rid[p]]++] = (uint32_t)p;
-}
-
-static int build_warp_regions(pf_ctx* c, int pw, int ph, long long npix)
-{
-    std::vector<uint32_t> wxy((size_t)npix);
-    HIPCHK(c, hipMemcpyAsync(wxy.data(), c->wmap.p, sizeof(uint32_t) * npix,
+    std::vector<WarpPatch> p(c->npatch);
+    HIPCHK(c, hipMemcpyAsync(p.data(), c->wpatch.p, sizeof(WarpPatch) * p.size(),
                              hipMemcpyDeviceToHost, c->stream));
     HIPCHK(c, hipStreamSynchronize(c->stream));
-    const bool quads = (pw & 3) == 0;
-    std::vector<WarpRegion> regions;
-    std::vector<uint32_t> perm;
-    size_t nwide = 0;
-    const char* cut = getenv("PF_WARP_CUT");
-    if (cut && !strcmp(cut, "pixel")) warp_cut_pixels(c, pw, ph, wxy, regions, perm);
-    else warp_cut_strips(c, pw, wxy, regions, perm, nwide);
-    if (perm.size() >= (1u << 31))
-        return fail(c, PF_EINVAL, "depth warp: %zu entries (< 2^31)", perm.size());
-    int rc;
-    if ((rc = upload(c, c->wregion, regions))) return rc;
-    if ((rc = upload(c, c->wperm, perm))) return rc;
-    if ((rc = ensure(c, c->wentry, sizeof(WarpEntry) * perm.size()))) return rc;
-    c->nregions = (int)regions.size();
-    if (getenv("PF_WARP_STATS")) {
-        double boxf = 0;
-        int maxslot = 0;
-        for (const WarpRegion& R : regions) {
-            boxf += (double)R.units * (quads ? 4 : 1);
-            maxslot = std::max(maxslot, R.nslot);
-        }
-        fprintf(stderr, "[pf warp] %d regions (%zu wide strips), %.1f px/region, staged %.3f x "
-                "the panorama, max %d tiles/region\n", c->nregions, nwide,
-                (double)npix / regions.size(), boxf / ((double)pw * ph), maxslot);
-    }
-    launch_warp_entries(c->stream, (const TileGeom*)c->geom.p, (const WarpRegion*)c->wregion.p,
-                        c->nregions, (const uint32_t*)c->wperm.p, (const uint32_t*)c->wmap.p,
-                        (const float*)c->wfxy.p, pw, ph, (WarpEntry*)c->wentry.p);
-    HIPCHK(c, hipGetLastError());
-    return PF_OK;
+    auto key = [pw](const WarpPatch& w) {
+        const long long band = (w.gy0 + w.bh / 2) / 32;
+        const long long col = (w.gx0 + w.bw / 2) % pw;
+        return band * 65536 + col;
+    };
+    std::stable_sort(p.begin(), p.end(),
+                     [&](const WarpPatch& a, const WarpPatch& b) { return key(a) < key(b); });
+    return upload(c, c->wpatch, p);
 }
 
 extern "C" {
@@ -1475,17 +1273,18 @@ int pf_warp_depth(pf_ctx* c, const float* pano, int pw, int ph, int batch,
     if (c->wmap_pw != pw || c->wmap_ph != ph) {
         if ((rc = ensure(c, c->wmap, sizeof(uint32_t) * npix))) return rc;
         if ((rc = ensure(c, c->wfxy, sizeof(float) * 2 * npix))) return rc;
-        launch_warp_coords(c->stream, (const TileGeom*)c->geom.p, c->ntiles, c->npix_max, pw, ph,
-                           (uint32_t*)c->wmap.p, (float*)c->wfxy.p);
+        launch_warp_prepare(c->stream, (const TileGeom*)c->geom.p, c->ntiles, c->npix_max,
+                            (WarpPatch*)c->wpatch.p, c->npatch, pw, ph, (uint32_t*)c->wmap.p,
+                            (float*)c->wfxy.p);
         HIPCHK(c, hipGetLastError());
-        if ((rc = build_warp_regions(c, pw, ph, npix))) return rc;
+        if ((rc = sort_warp_patches(c, pw))) return rc;
         c->wmap_pw = pw;
         c->wmap_ph = ph;
     }
     StageTimer t(c, PF_STAGE_WARP, batch * (4.0 * pw * ph + 4.0 * (double)npix), 1);
     launch_warp_depth(c->stream, (const TileGeom*)c->geom.p, c->ntiles,
-                      (const WarpRegion*)c->wregion.p, c->nregions,
-                      (const WarpEntry*)c->wentry.p, pano, pw, ph, (long long)pw * ph,
+                      (const WarpPatch*)c->wpatch.p, c->npatch, (const uint32_t*)c->wmap.p,
+                      (const float*)c->wfxy.p, pano, pw, ph, (long long)pw * ph,
                       (const Resp*)resp, tiles, c->tile_elems, batch);
     HIPCHK(c, hipGetLastError());
     return PF_OK;
@@ -1699,7 +1498,11 @@ int pf_fuse_band_pass(pf_ctx* c, const float* emap, int ew, int eh, int ec, cons
                               4 * c->num_cu, tune.step_overhead, tune.lone_cycles, tune.c4_eff);
     const long long st = (long long)L.w * L.h;
     JacobiPass P{};
-    if (src_mode == 2 && (rc = seed_tables(c, L, ew, eh, ec, P))) return rc;
+    if (src_mode == 2) {
+        if ((rc = seed_tables(c, L, ew, eh, ec))) return rc;
+        P.ecol = (const int*)c->seed_ecol.p;
+        P.erow = (const int*)c->seed_erow.p;
+    }
     P.prev = prev; P.pstride = 0;
     P.emap = emap; P.estride = 0; P.ew = ew; P.eh = eh; P.ec = ec;
     P.cols = (const GridCol*)lc.cols[level].p; P.rows = (const GridRow*)lc.rows[level].p;

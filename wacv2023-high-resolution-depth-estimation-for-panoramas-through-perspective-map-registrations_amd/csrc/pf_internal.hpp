@@ -68,32 +68,12 @@ struct Resp {
     uint32_t seed, pad;
 };
 
-// E->P depth warp (pf_warp.hip).  The tiles are cut into strips of kWarpStrip consecutive pixels
-// of one tile row (aligned: a strip's stores are whole 128-B lines) and the strips are grouped,
-// whichever tile they belong to, into regions of the panorama: strips sorted by band of
-// kWarpBand rows, then column, and cut into regions of at most kWarpRegionPx pixels whose
-// joint corner footprint (+1 row/column) fits the LDS box of kWarpRows x kWarpPitch floats.
-// Built once per (layout, panorama size) on the host (pf_api.hip build_warp_regions).
-constexpr int kWarpStrip = 16;   // 64 B: the granule the L2 writes back
-constexpr int kWarpBand = 8;        // panorama rows per band (the sort key)
-constexpr int kWarpRows = 20;       // max rows of a staged box
-constexpr int kWarpPitch = 128;     // LDS row pitch of a staged box, floats (a multiple of 64:
-                                    // c00/c10 and c01/c11 are ds_read2st64 pairs)
-constexpr int kWarpRegionPx = 1024; // max tile pixels per region (4 per thread)
-constexpr int kWarpSlots = 8;       // max distinct tiles per region
-struct WarpRegion {
-    int gx0, gy0;   // box origin: column (a multiple of 4 for quad staging), row
-    int bwu, units; // staging units per box row, units in the box (units: floats or quads)
-    int e0, n;      // first entry, entry count (a multiple of kWarpStrip)
-    int nslot;
-    int wide;       // strips too wide for a box: direct corner gathers, no staging
-    int tile[kWarpSlots];  // layout tile of each slot
-};
-struct WarpEntry {
-    uint32_t i;   // pixel index inside its tile | slot << 24; 0xFFFFFFFF: no pixel (strip tail)
-    uint32_t ls;  // LDS index of corner (x0, y0) in the box; wide regions: panorama index of the
-                  // corner | (x1 != x0) << 31 | (y1 != y0) << 30
-    float fx, fy;
+// One square patch of a tile for the E->P depth warp (pf_warp.hip): its tile pixels and the
+// azimuth-unwrapped panorama box their bilinear corners fall in (filled on the device).
+struct WarpPatch {
+    int tile, X0, Y0;
+    int gx0, gy0, bw, bh;  // box origin (column mod pw, row) and size, +1 row/column
+    int wide;              // box larger than the LDS staging capacity: direct gathers
 };
 
 struct LevelDims {
@@ -241,15 +221,14 @@ void launch_register_joint(hipStream_t s, const double* sums, const int* active,
                            int batch, int degree, int solver, float* coeffs, double* coeffs64);
 void launch_apply_cubic(hipStream_t s, const TileGeom* geom, int ntiles, long long tile_elems,
                         float* tiles, long long tstride, const float* coeffs, int batch);
-void launch_warp_coords(hipStream_t s, const TileGeom* geom, int ntiles, long long npix_max,
-                        int pw, int ph, uint32_t* wxy, float* wfxy);
-void launch_warp_entries(hipStream_t s, const TileGeom* geom, const WarpRegion* regions,
-                         int nregions, const uint32_t* perm, const uint32_t* wxy,
-                         const float* wfxy, int pw, int ph, WarpEntry* entries);
-void launch_warp_depth(hipStream_t s, const TileGeom* geom, int ntiles, const WarpRegion* regions,
-                       int nregions, const WarpEntry* entries, const float* pano, int pw, int ph,
-                       long long pstride, const Resp* resp, float* tiles, long long tstride,
-                       int batch);
+int warp_patch_edge();
+void launch_warp_prepare(hipStream_t s, const TileGeom* geom, int ntiles, long long npix_max,
+                         WarpPatch* patches, int npatch, int pw, int ph, uint32_t* wloc,
+                         float* wfxy);
+void launch_warp_depth(hipStream_t s, const TileGeom* geom, int ntiles, const WarpPatch* patches,
+                       int npatch, const uint32_t* wloc, const float* wfxy, const float* pano,
+                       int pw, int ph, long long pstride, const Resp* resp, float* tiles,
+                       long long tstride, int batch);
 void launch_warp_rgb(hipStream_t s, const RgbCam* cams, const TileGeom* geom, int ntiles,
                      long long npix_total, const long long* pix_prefix,
                      const long long* rgb_off, const uint8_t* pano, int pw, int ph,

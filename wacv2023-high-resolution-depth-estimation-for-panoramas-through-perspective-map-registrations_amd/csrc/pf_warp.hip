@@ -1,49 +1,56 @@
-// pf_warp.hip -- E->P depth warp as a region-staged gather for gfx950.
+// pf_warp.hip -- E->P depth warp as an LDS-staged gather for gfx950.
 //
 // For every tile pixel (X, Y) the reference mapping is ToSphericalCoord (Depth.cpp:157-166):
 // corner0 + hedge*x + vedge*y -> WorldToSpherical (Depth.cpp:2960-2971) -> a bilinear sample of
 // the panorama at ValueAtCoord's pixel convention (az/2pi*(pw-1), zen/pi*(ph-1)).  That mapping
-// depends only on the layout and the panorama size, so it is evaluated once and cached by the
-// context, and the per-call kernel does no trigonometry:
+// depends only on the layout and the panorama size, so it is evaluated once (three small
+// passes, cached by the context) and the per-call kernel does no trigonometry:
 //
-//  1. k_warp_coords:  per tile pixel the bilinear corner (x0, y0) and weights (fx, fy).
-//  2. the host cuts every tile row into aligned strips of kWarpStrip pixels and groups the
-//     strips of all tiles by where their corners fall in the panorama: sorted by band of
-//     kWarpBand rows, then column, and cut into regions of at most kWarpRegionPx pixels whose
-//     joint corner footprint fits one LDS box (pf_api.hip build_warp_regions).
-//  3. k_warp_entries: per region its pixels' 16-B entries, strip by strip.
+//  1. k_warp_coords: per tile pixel the bilinear corner (x0, y0) and weights (fx, fy).
+//  2. k_patch_box:   tiles are cut into 32x32-pixel patches; per patch the panorama footprint
+//                    (an azimuth-unwrapped box, <= kCap floats, or "wide").
+//  3. k_warp_local:  per tile pixel the corner's index inside its patch's footprint box (or the
+//                    global index with edge flags for a wide patch).
 //
-// k_warp_depth: one block per (region, chunk of kNB panoramas).  Per panorama the block stages
-// the region's box from HBM into LDS with coalesced 16-B row loads, then every pixel reads its
-// four corners from LDS.  Input-driven: the strips of overlapping tiles that look at the same
-// part of the panorama share one staged box, so each panorama line is fetched about once per
-// launch (plus the boxes' overlap, ~7-15 %), where the round-2 patch-per-tile boxes fetched each
-// line ~1.8x; and a wave's two strips are two whole 128-B lines of output.  The chunks of one
-// region are adjacent in the grid, so a region's entries come from HBM once and from L2 for
-// the other chunks.  Strips whose own footprint is too wide for a box (near the poles) form
-// "wide" regions served by direct corner gathers.
+// k_warp_depth: one block per (patch, chunk of kNB panoramas).  Per panorama the block copies the
+// footprint box from HBM into LDS with plain coalesced row loads (double-buffered: the loads for
+// panorama q+1 are in flight while panorama q is interpolated), then every pixel reads its four
+// corners from LDS.  The box is ~0.4x the panorama's bytes per panorama (vs ~4 scattered corner
+// loads per tile pixel from L2 in a direct gather), so the kernel is bound by the tile writes.
 //
 // Edge rule: the reference clamps x1 = min(x0+1, pw-1), y1 = min(y0+1, ph-1).  x0 == pw-1 only
 // when px == pw-1 exactly (az < 2*MYPI), i.e. fx == 0, and likewise y0 == ph-1 means fy == 0; the
-// neighbour's weight is then exactly zero, so the box may hold any finite value there (the next
-// row's first pixel, or 0 past the panorama through the buffer range check).  Inputs are depth
-// maps, finite by contract.
+// neighbour's weight is then exactly zero, so the box may hold any finite value there (the box
+// wraps in azimuth and clamps rows).  Inputs are depth maps, finite by contract.
 #include "pf_internal.hpp"
 
 #include <cfloat>
-#include <cstdlib>
 #include <type_traits>
 
 namespace pf {
 
-static constexpr int kWB = 256;                          // threads per block
-static constexpr int kPx = kWarpRegionPx / kWB;          // pixels per thread
-static constexpr int kBoxRows = kWarpRows;
-static constexpr int kBoxFloats = kBoxRows * kWarpPitch;  // LDS floats per staged box
+static constexpr int kWB = 256;                         // threads per block
+static constexpr int kPatch = 32;                       // patch edge in tile pixels
+static constexpr int kPx = kPatch * kPatch / kWB;       // pixels per thread
+#ifndef PF_WARP_CAP
+#define PF_WARP_CAP 4096
+#endif
+static constexpr int kCap = PF_WARP_CAP;                // LDS floats per staged footprint
+static constexpr int kSlots = kCap / kWB;               // staging loads per thread
 #ifndef PF_WARP_BATCH
 #define PF_WARP_BATCH 16
 #endif
-static constexpr int kNB = PF_WARP_BATCH;                // panoramas per block
+static constexpr int kNB = PF_WARP_BATCH;               // panoramas per block
+// Wider memory operations, measured on MI355X at C3 (tools/warp_probe.py, round 2) and not kept:
+// 16-B staging loads of quad-aligned boxes 0.596 ms, a thread's pixels in one row with 16-B
+// stores 0.600 ms, both 0.637 ms, against 0.586 ms for 4-B loads and stores -- the kernel is not
+// bound by its memory instruction count.
+#ifndef PF_WARP_V4
+#define PF_WARP_V4 0     // quad-aligned footprint boxes staged with 16-B loads (pw % 4 == 0)
+#endif
+#ifndef PF_WARP_ROWPX
+#define PF_WARP_ROWPX 0  // a thread's pixels consecutive in one row: one 16-B store per panorama
+#endif
 
 __device__ __forceinline__ void world_to_sph(float p0, float p1, float p2, float& az,
                                              float& zen)
@@ -115,6 +122,98 @@ __global__ void __launch_bounds__(kWB) k_warp_coords(const TileGeom* __restrict_
     wfxy[g.pix_off + i] = make_float2(fx, fy);
 }
 
+__device__ __forceinline__ int patch_pixel(const WarpPatch& P, const TileGeom& g, int t, int k,
+                                           int& i)
+{  // thread t, slot k -> tile pixel index i; returns 0 outside the tile.  A thread owns kPx
+   // consecutive pixels of one patch row (one 16-B store per panorama), a wave 8 whole rows.
+    static_assert(kPx == 4 && kPatch == 32, "4 pixels per thread, 8 threads per patch row");
+#if PF_WARP_ROWPX
+    const int X = P.X0 + 4 * (t & 7) + k, Y = P.Y0 + (t >> 3);
+#else  // a wave covers 2 rows per slot, slots 8 rows apart
+    const int X = P.X0 + (t & (kPatch - 1)), Y = P.Y0 + t / kPatch + k * (kWB / kPatch);
+#endif
+    i = Y * g.w + X;
+    return X < g.w && Y < g.h;
+}
+
+__device__ __forceinline__ int wrap_du(int d, int pw)
+{
+    if (d > pw / 2) d -= pw;
+    if (d < -(pw / 2)) d += pw;
+    return d;
+}
+
+// Pass 2: per patch the azimuth-unwrapped footprint box of all its corners (+1 row/column).
+__global__ void __launch_bounds__(kWB) k_patch_box(const TileGeom* __restrict__ geom,
+                                                   WarpPatch* __restrict__ patches, int pw,
+                                                   const uint32_t* __restrict__ wxy)
+{
+    __shared__ int red[4];
+    WarpPatch P = patches[blockIdx.x];
+    const TileGeom& g = geom[P.tile];
+    const int t = threadIdx.x;
+    const int ref = (int)(wxy[g.pix_off + P.Y0 * g.w + P.X0] & 0xFFFFu);
+    if (t == 0) { red[0] = INT32_MAX; red[1] = INT32_MIN; red[2] = INT32_MAX; red[3] = INT32_MIN; }
+    __syncthreads();
+    int umin = INT32_MAX, umax = INT32_MIN, ymin = INT32_MAX, ymax = INT32_MIN;
+#pragma unroll
+    for (int k = 0; k < kPx; k++) {
+        int i;
+        if (!patch_pixel(P, g, t, k, i)) continue;
+        const uint32_t m = wxy[g.pix_off + i];
+        const int du = wrap_du((int)(m & 0xFFFFu) - ref, pw), y = (int)(m >> 16);
+        umin = min(umin, du); umax = max(umax, du);
+        ymin = min(ymin, y); ymax = max(ymax, y);
+    }
+    atomicMin(&red[0], umin); atomicMax(&red[1], umax);
+    atomicMin(&red[2], ymin); atomicMax(&red[3], ymax);
+    __syncthreads();
+    if (t == 0) {
+        int gx0 = ref + red[0];
+        gx0 = gx0 < 0 ? gx0 + pw : (gx0 >= pw ? gx0 - pw : gx0);
+        int bw = red[1] - red[0] + 2;
+        if (PF_WARP_V4 && (pw & 3) == 0) {  // 16-B staging loads: origin and width in quads
+            const int a = gx0 & 3;
+            gx0 -= a;
+            bw = (bw + a + 3) & ~3;
+        }
+        P.gx0 = gx0;
+        P.gy0 = red[2];
+        P.bw = bw;
+        P.bh = red[3] - red[2] + 2;
+        P.wide = (P.bw * P.bh > kCap || P.bw > pw / 2) ? 1 : 0;
+        patches[blockIdx.x] = P;
+    }
+}
+
+// Pass 3: per tile pixel the corner index inside its patch's box (or, for a wide patch, the
+// global index | (x1 != x0) << 31 | (y1 != y0) << 30).  In place over wxy.
+__global__ void __launch_bounds__(kWB) k_warp_local(const TileGeom* __restrict__ geom,
+                                                    const WarpPatch* __restrict__ patches,
+                                                    int pw, int ph, uint32_t* __restrict__ wxy)
+{
+    const WarpPatch P = patches[blockIdx.x];
+    const TileGeom& g = geom[P.tile];
+    const int t = threadIdx.x;
+#pragma unroll
+    for (int k = 0; k < kPx; k++) {
+        int i;
+        if (!patch_pixel(P, g, t, k, i)) continue;
+        const uint32_t m = wxy[g.pix_off + i];
+        const int x0 = (int)(m & 0xFFFFu), y0 = (int)(m >> 16);
+        uint32_t o;
+        if (P.wide) {
+            o = (uint32_t)(y0 * pw + x0) | (x0 < pw - 1 ? 1u << 31 : 0u) |
+                (y0 < ph - 1 ? 1u << 30 : 0u);
+        } else {
+            int d = x0 - P.gx0;
+            if (d < 0) d += pw;
+            o = (uint32_t)((y0 - P.gy0) * P.bw + d);
+        }
+        wxy[g.pix_off + i] = o;
+    }
+}
+
 // Per-panorama response of one tile with its noise key mix32(seed), staged in LDS at block start
 // (a scalar load per panorama inside the loop would expose its latency on lgkmcnt with the LDS
 // reads).  The seed is unique per (panorama, layout-wide tile): pf_synth.responses folds the tile
@@ -180,42 +279,45 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc(const void* base, uint32_
 }
 
 struct WarpLanes {  // one thread's kPx pixels, all panorama-invariant
-    uint32_t la[kPx];   // LDS float index of corner (x0, y0) in the box
+    uint32_t la[kPx];   // LDS float index of corner (x0, y0) in the parity-interleaved box (x2)
     uint32_t oo[kPx];   // byte offset of the pixel inside one panorama's tile block; past the
-                        // block (a dropped buffer store) for lanes without a pixel
+                        // block (a dropped buffer store) for lanes outside the tile
     uint32_t hp[kPx];   // mix32(pixel index): the per-pixel half of the noise hash
-    uint32_t rs[kPx];   // byte offset of the pixel's slot in one panorama's response row
     f2 wx[kPx], wy[kPx];  // (1-fx, fx), (1-fy, fy)
+    bool ok[kPx];
+    bool full;  // the kPx pixels are inside the tile and contiguous (one channel): 16-B store
 };
 
+// LDS-staged interpolation of kNB panoramas for a box of at most NS*256 staging units (floats,
+// or with V4 column quads: 16-B loads of a box whose origin and width are whole quads, which
+// k_patch_box guarantees when pw % 4 == 0).  The box is double-buffered with the two parities
+// interleaved (element e of parity PA at box[2e + PA]), so a pixel's c00/c01 (and c10/c11) are
+// one ds_read2_b32 with immediate offsets in both parities.  Every staging load is issued
+// unconditionally (slots past the box reload a valid unit, panoramas past the chunk reload the
+// last one), so the loads for panorama q+2 go out before panorama q is interpolated and the wait
+// for panorama q+1's loads -- an in-order vmcnt -- never covers them.  A thread's four pixels
+// are consecutive in one tile row: one 16-B store per panorama when they are all inside.
 typedef uint32_t u4v __attribute__((ext_vector_type(4)));
-
-// Stage the region box of kNB panoramas through LDS (double-buffered) and interpolate every
-// pixel of the region for each.  U = floats per staging unit (4: 16-B loads of a box whose
-// origin and row width are whole quads, pw % 4 == 0; 1 otherwise); NS = staging units per
-// thread.  Every staging load is issued unconditionally (slots past the box reload a valid unit,
-// panoramas past the chunk reload the last one), so the loads for panorama q+2 are in flight
-// while panorama q is interpolated.
-template <int NS, int U, bool RESP>
-__device__ __forceinline__ void warp_region(float* box, const RespK* rk, const WarpRegion& R,
+template <int NS, bool RESP, bool V4>
+__device__ __forceinline__ void warp_staged(float* box, const RespK* rk, const WarpPatch& P,
                                             int t, const WarpLanes& W,
-                                            const float* __restrict__ pano, long long pstride,
-                                            int pw, int ph, float* __restrict__ tiles,
+                                            const float* __restrict__ pano, int pw, int ph,
+                                            long long pstride, float* __restrict__ tiles,
                                             long long tstride, int bbeg, int nb)
 {
+    constexpr int U = V4 ? 4 : 1;  // floats per staging unit
+    const int bw2 = 2 * P.bw, bwu = P.bw / U, units = bwu * P.bh;
     uint32_t goff[NS];  // unit e = t + 256*s of the box -> panorama byte offset
-    uint32_t loff[NS];  // -> LDS float index
 #pragma unroll
     for (int s = 0; s < NS; s++) {
         int e = t + s * kWB;
-        e = e < R.units ? e : R.units - 1;
-        const int r = e / R.bwu, c = (e - r * R.bwu) * U;
-        int row = R.gy0 + r;
-        row = row < ph ? row : ph - 1;  // only rows of zero-weight corners are clamped
-        int col = R.gx0 + c;
-        col = col < pw ? col : col - pw;  // the box wraps in azimuth (quads never straddle)
+        e = e < units ? e : units - 1;
+        const int r = e / bwu, c = (e - r * bwu) * U;
+        int row = P.gy0 + r;
+        row = row < ph ? row : ph - 1;
+        int col = P.gx0 + c;
+        col = col < pw ? col : col - pw;
         goff[s] = (uint32_t)(row * pw + col) * 4u;
-        loff[s] = (uint32_t)(r * kWarpPitch + c);
     }
     float stg[2][NS][U];
     const uint32_t pbytes = (uint32_t)(pstride * 4);
@@ -223,7 +325,7 @@ __device__ __forceinline__ void warp_region(float* box, const RespK* rk, const W
         const auto pr = rsrc(pano + (long long)(bbeg + (q < nb ? q : nb - 1)) * pstride, pbytes);
 #pragma unroll
         for (int s = 0; s < NS; s++) {
-            if constexpr (U == 4) {
+            if constexpr (V4) {
                 const u4v v = __builtin_amdgcn_raw_buffer_load_b128(pr, (int)goff[s], 0, 0);
 #pragma unroll
                 for (int j = 0; j < 4; j++) dst[s][j] = __uint_as_float(v[j]);
@@ -232,23 +334,26 @@ __device__ __forceinline__ void warp_region(float* box, const RespK* rk, const W
             }
         }
     };
-    auto put = [&](float* bx, const float (*src)[U]) {
+    auto put = [&](int pa, const float (*src)[U]) {
 #pragma unroll
-        for (int s = 0; s < NS; s++) {
-            if constexpr (U == 4) {
-                *(float4*)(bx + loff[s]) = make_float4(src[s][0], src[s][1], src[s][2], src[s][3]);
-            } else {
-                bx[loff[s]] = src[s][0];
-            }
-        }
+        for (int s = 0; s < NS; s++)
+#pragma unroll
+            for (int j = 0; j < U; j++) box[2 * ((t + s * kWB) * U + j) + pa] = src[s][j];
     };
     auto iter = [&](auto parity, int q) {
         constexpr int PA = decltype(parity)::value;
-        fetch(stg[PA], q + 2);  // panorama q was put into buffer PA last iteration: reuse stg[PA]
-        const float* L = box + PA * kBoxFloats;
+        fetch(stg[PA], q + 2);  // panorama q was put into parity PA last iteration: reuse stg[PA]
+        const float* L = box + PA;
         const int b = bbeg + q;
         const auto orr = rsrc(tiles + b * tstride, (uint32_t)(tstride * 4));
-        const char* rq = (const char*)(rk + q * kWarpSlots);
+        f2 al{}, ka{}, be{}, si{};
+        uint32_t key = 0;
+        if (RESP) {
+            const RespK r = rk[q];
+            al = f2{r.alpha, r.alpha}; ka = f2{r.kappa, r.kappa};
+            be = f2{r.beta, r.beta}; si = f2{r.sigma, r.sigma};
+            key = r.key;
+        }
         float out[kPx];
 #pragma unroll
         for (int k = 0; k < kPx; k += 2) {
@@ -256,32 +361,37 @@ __device__ __forceinline__ void warp_region(float* box, const RespK* rk, const W
 #pragma unroll
             for (int j = 0; j < 2; j++) {
                 const float* c = L + W.la[k + j];
-                v[j] = bilinear(f2{c[0], c[1]}, f2{c[kWarpPitch], c[kWarpPitch + 1]},
-                                W.wx[k + j], W.wy[k + j]);
+                v[j] = bilinear(f2{c[0], c[2]}, f2{c[bw2], c[bw2 + 2]}, W.wx[k + j],
+                                W.wy[k + j]);
             }
             if (RESP) {
-                const RespK r0 = *(const RespK*)(rq + W.rs[k]);
-                const RespK r1 = *(const RespK*)(rq + W.rs[k + 1]);
-                const f2 u = f2{noise_top24(W.hp[k], r0.key), noise_top24(W.hp[k + 1], r1.key)};
+                const f2 u = f2{noise_top24(W.hp[k], key), noise_top24(W.hp[k + 1], key)};
                 const f2 nz = __builtin_elementwise_fma(u, f2{0x1p-23f, 0x1p-23f},
                                                         f2{-1.0f, -1.0f});
-                f2 tt = f2{r0.alpha, r1.alpha} * v;
-                tt = tt + (f2{r0.kappa, r1.kappa} * v) * v;
-                tt = tt + f2{r0.beta, r1.beta};
-                v = pk_add_clamp01(tt, f2{r0.sigma, r1.sigma} * nz);
+                f2 tt = al * v;
+                tt = tt + (ka * v) * v;
+                tt = tt + be;
+                v = pk_add_clamp01(tt, si * nz);
             }
             out[k] = v[0];
             out[k + 1] = v[1];
         }
+        if (W.full) {
+            const u4v o = {__float_as_uint(out[0]), __float_as_uint(out[1]),
+                           __float_as_uint(out[2]), __float_as_uint(out[3])};
+            __builtin_amdgcn_raw_buffer_store_b128(o, orr, (int)W.oo[0], 0, 0);
+        } else {
 #pragma unroll
-        for (int k = 0; k < kPx; k++)
-            __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(out[k]), orr, (int)W.oo[k], 0, 0);
-        put(box + (1 - PA) * kBoxFloats, stg[1 - PA]);  // panorama q+1 (past the chunk: unread)
+            for (int k = 0; k < kPx; k++)
+                __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(out[k]), orr, (int)W.oo[k],
+                                                      0, 0);
+        }
+        put(1 - PA, stg[1 - PA]);  // panorama q+1 (a duplicate past the chunk: unread)
         __syncthreads();
     };
     fetch(stg[0], 0);
     fetch(stg[1], 1);
-    put(box, stg[0]);
+    put(0, stg[0]);
     __syncthreads();
     for (int q = 0; q < nb; q += 2) {
         iter(std::integral_constant<int, 0>{}, q);
@@ -289,84 +399,72 @@ __device__ __forceinline__ void warp_region(float* box, const RespK* rk, const W
     }
 }
 
-template <int NS, int U>
-__device__ __forceinline__ void warp_region_sel(bool resp, float* box, const RespK* rk,
-                                                const WarpRegion& R, int t, const WarpLanes& W,
-                                                const float* pano, long long pstride, int pw,
-                                                int ph, float* tiles, long long tstride, int bbeg,
-                                                int nb)
+template <int NS, bool V4>
+__device__ __forceinline__ void warp_staged_sel(bool resp, float* box, const RespK* rk,
+                                                const WarpPatch& P, int t, const WarpLanes& W,
+                                                const float* pano, int pw, int ph,
+                                                long long pstride, float* tiles,
+                                                long long tstride, int bbeg, int nb)
 {
-    if (resp) warp_region<NS, U, true>(box, rk, R, t, W, pano, pstride, pw, ph, tiles, tstride,
-                                       bbeg, nb);
-    else warp_region<NS, U, false>(box, rk, R, t, W, pano, pstride, pw, ph, tiles, tstride, bbeg,
-                                   nb);
+    if (resp) warp_staged<NS, true, V4>(box, rk, P, t, W, pano, pw, ph, pstride, tiles, tstride,
+                                        bbeg, nb);
+    else warp_staged<NS, false, V4>(box, rk, P, t, W, pano, pw, ph, pstride, tiles, tstride,
+                                    bbeg, nb);
 }
 
 __global__ void __launch_bounds__(kWB) k_warp_depth(const TileGeom* __restrict__ geom,
                                                     int ntiles,
-                                                    const WarpRegion* __restrict__ regions,
-                                                    int nregions,
-                                                    const WarpEntry* __restrict__ entries,
+                                                    const WarpPatch* __restrict__ patches,
+                                                    int npatch, const uint32_t* __restrict__ wloc,
+                                                    const float2* __restrict__ wfxy,
                                                     const float* __restrict__ pano, int pw,
                                                     int ph, long long pstride,
                                                     const Resp* __restrict__ resp,
                                                     float* __restrict__ tiles,
-                                                    long long tstride, int batch, int order)
+                                                    long long tstride, int batch)
 {
-    __shared__ __attribute__((aligned(16))) float box[2 * kBoxFloats];
-    __shared__ RespK rk[kNB * kWarpSlots];  // published by the first barrier inside warp_region
-    // the chunks of one region are adjacent, XCD-contiguous runs of regions (sorted by band,
-    // then column): neighbouring boxes' shared rows/columns and a region's entries hit in L2
-    const unsigned nchunk = (unsigned)((batch + kNB - 1) / kNB);
+    __shared__ float box[2 * kCap];
+    // XCD-contiguous runs of patches; the host sorts the patches by panorama footprint, so the
+    // blocks resident on one XCD stage overlapping boxes and re-read each other's lines from L2
     const unsigned lb = xcd_remap(blockIdx.x, gridDim.x);
-    // by reference: a private copy of tile[] would be indexed dynamically, i.e. live in scratch
-    const WarpRegion& R = regions[order ? lb % (unsigned)nregions : lb / nchunk];
-    const int chunk = (int)(order ? lb / (unsigned)nregions : lb % nchunk);
+    const int pid = (int)(lb % (unsigned)npatch);
+    const int chunk = (int)(lb / (unsigned)npatch);
+    const WarpPatch P = patches[pid];
+    const TileGeom& g = geom[P.tile];
     const int t = threadIdx.x;
     const int bbeg = chunk * kNB;
     const int nb = min(kNB, batch - bbeg);
 
     WarpLanes W;
-    int slot[kPx];
-    bool ok[kPx];
 #pragma unroll
     for (int k = 0; k < kPx; k++) {
-        const int e = t + k * kWB;
+        int i;
+        W.ok[k] = patch_pixel(P, g, t, k, i);
         W.la[k] = 0; W.wx[k] = f2{1.0f, 0.0f}; W.wy[k] = f2{1.0f, 0.0f};
-        W.hp[k] = 0; W.rs[k] = 0; W.oo[k] = 0xFFFFFFF0u;
-        slot[k] = 0;
-        ok[k] = false;
-        if (e < R.n) {
-            const WarpEntry E = entries[R.e0 + e];
-            if (E.i != 0xFFFFFFFFu) {
-                const uint32_t i = E.i & 0xFFFFFFu;
-                slot[k] = (int)(E.i >> 24);
-                ok[k] = true;
-                const TileGeom& g = geom[R.tile[slot[k]]];
-                W.la[k] = E.ls;
-                W.oo[k] = (uint32_t)(g.off + (long long)i * g.c) * 4u;
-                W.hp[k] = mix32(i);
-                W.rs[k] = (uint32_t)(slot[k] * sizeof(RespK));
-                W.wx[k] = f2{1.0f - E.fx, E.fx};
-                W.wy[k] = f2{1.0f - E.fy, E.fy};
-            }
+        W.hp[k] = mix32((uint32_t)i);
+        W.oo[k] = W.ok[k] ? (uint32_t)(g.off + (long long)i * g.c) * 4u : 0xFFFFFFF0u;
+        if (W.ok[k]) {
+            W.la[k] = wloc[g.pix_off + i];
+            const float2 f = wfxy[g.pix_off + i];
+            W.wx[k] = f2{1.0f - f.x, f.x};
+            W.wy[k] = f2{1.0f - f.y, f.y};
         }
     }
 
-    if (R.wide) {  // footprints too wide for a box (near a pole): direct corner gathers
+    if (P.wide) {  // footprint too large for LDS (near a pole): direct corner gathers
         for (int q = 0; q < nb; q++) {
             const int b = bbeg + q;
             const float* pp = pano + b * pstride;
+            const RespK r = resp_key(resp, b, ntiles, P.tile);
             float* out = tiles + b * tstride;
 #pragma unroll
             for (int k = 0; k < kPx; k++) {
-                if (!ok[k]) continue;
+                if (!W.ok[k]) continue;
                 const uint32_t o00 = W.la[k] & 0x3FFFFFFFu, dx = W.la[k] >> 31;
                 const uint32_t o10 = o00 + (((W.la[k] >> 30) & 1u) ? (uint32_t)pw : 0u);
                 float v = bilinear(f2{pp[o00], pp[o00 + dx]}, f2{pp[o10], pp[o10 + dx]},
                                    W.wx[k], W.wy[k]);
                 if (resp) {
-                    const RespK r = resp_key(resp, b, ntiles, R.tile[slot[k]]);
                     const float nz = __builtin_fmaf(noise_top24(W.hp[k], r.key), 0x1p-23f, -1.0f);
                     float tt = r.alpha * v;
                     tt = tt + (r.kappa * v) * v;
@@ -380,87 +478,55 @@ __global__ void __launch_bounds__(kWB) k_warp_depth(const TileGeom* __restrict__
         return;
     }
 
-    if (t < nb * R.nslot) {
-        const int q = t / R.nslot, s = t - q * R.nslot;
-        rk[q * kWarpSlots + s] = resp_key(resp, bbeg + q, ntiles, R.tile[s]);
-    }
+    W.full = PF_WARP_ROWPX && W.ok[0] && W.ok[kPx - 1] && g.c == 1;
+#pragma unroll
+    for (int k = 0; k < kPx; k++) W.la[k] *= 2;  // parity-interleaved box
+    __shared__ RespK rk[kNB];  // published by the first barrier inside warp_staged
+    if (t < nb) rk[t] = resp_key(resp, bbeg + t, ntiles, P.tile);
     const bool rs = resp != nullptr;
-    if ((pw & 3) == 0) {  // quad-aligned boxes: 16-B staging loads
-        if (R.units <= kWB) warp_region_sel<1, 4>(rs, box, rk, R, t, W, pano, pstride, pw, ph,
-                                                  tiles, tstride, bbeg, nb);
-        else warp_region_sel<(kBoxFloats / 4 + kWB - 1) / kWB, 4>(
-            rs, box, rk, R, t, W, pano, pstride, pw, ph, tiles, tstride, bbeg, nb);
+    if (PF_WARP_V4 && (pw & 3) == 0) {  // quad-aligned boxes (k_patch_box): 16-B staging loads
+        const int nq = (P.bw * P.bh / 4 + kWB - 1) / kWB;  // uniform: loads per thread
+        if (nq <= 1) warp_staged_sel<1, true>(rs, box, rk, P, t, W, pano, pw, ph, pstride, tiles,
+                                              tstride, bbeg, nb);
+        else if (nq <= 2) warp_staged_sel<2, true>(rs, box, rk, P, t, W, pano, pw, ph, pstride,
+                                                   tiles, tstride, bbeg, nb);
+        else warp_staged_sel<kSlots / 4, true>(rs, box, rk, P, t, W, pano, pw, ph, pstride,
+                                               tiles, tstride, bbeg, nb);
     } else {
-        if (R.units <= 4 * kWB) warp_region_sel<4, 1>(rs, box, rk, R, t, W, pano, pstride, pw, ph,
-                                                      tiles, tstride, bbeg, nb);
-        else warp_region_sel<(kBoxFloats + kWB - 1) / kWB, 1>(rs, box, rk, R, t, W, pano, pstride,
-                                                              pw, ph, tiles, tstride, bbeg, nb);
-    }
-}
-
-// Per region its pixels' entries (perm: the region's tile pixels as layout-wide pixel indices,
-// strip by strip, 0xFFFFFFFF past a strip's end) with the corner's index in the region's box.
-__global__ void __launch_bounds__(kWB) k_warp_entries(const TileGeom* __restrict__ geom,
-                                                      const WarpRegion* __restrict__ regions,
-                                                      const uint32_t* __restrict__ perm,
-                                                      const uint32_t* __restrict__ wxy,
-                                                      const float2* __restrict__ wfxy, int pw,
-                                                      int ph, WarpEntry* __restrict__ entries)
-{
-    const WarpRegion& R = regions[blockIdx.x];
-    for (int e = threadIdx.x; e < R.n; e += kWB) {
-        const uint32_t p = perm[R.e0 + e];
-        WarpEntry E{0xFFFFFFFFu, 0u, 0.0f, 0.0f};
-        if (p != 0xFFFFFFFFu) {
-            int slot = 0;
-            for (int s = 1; s < R.nslot; s++)
-                if ((long long)p >= geom[R.tile[s]].pix_off) slot = s;  // slots in tile order
-            const TileGeom& g = geom[R.tile[slot]];
-            const uint32_t m = wxy[p];
-            const int x0 = (int)(m & 0xFFFFu), y0 = (int)(m >> 16);
-            const float2 f = wfxy[p];
-            E.i = (p - (uint32_t)g.pix_off) | ((uint32_t)slot << 24);
-            if (R.wide) {
-                E.ls = (uint32_t)(y0 * pw + x0) | (x0 < pw - 1 ? 1u << 31 : 0u) |
-                       (y0 < ph - 1 ? 1u << 30 : 0u);
-            } else {
-                int dx = x0 - R.gx0;
-                if (dx < 0) dx += pw;
-                E.ls = (uint32_t)((y0 - R.gy0) * kWarpPitch + dx);
-            }
-            E.fx = f.x;
-            E.fy = f.y;
-        }
-        entries[R.e0 + e] = E;
+        const int ns = (P.bw * P.bh + kWB - 1) / kWB;  // uniform: staging loads per thread
+        if (ns <= 4) warp_staged_sel<4, false>(rs, box, rk, P, t, W, pano, pw, ph, pstride,
+                                               tiles, tstride, bbeg, nb);
+        else if (ns <= 8) warp_staged_sel<8, false>(rs, box, rk, P, t, W, pano, pw, ph, pstride,
+                                                    tiles, tstride, bbeg, nb);
+        else warp_staged_sel<kSlots, false>(rs, box, rk, P, t, W, pano, pw, ph, pstride, tiles,
+                                            tstride, bbeg, nb);
     }
 }
 
 // ---------------------------------------------------------------------------------------------
-void launch_warp_coords(hipStream_t s, const TileGeom* geom, int ntiles, long long npix_max,
-                        int pw, int ph, uint32_t* wxy, float* wfxy)
+void launch_warp_prepare(hipStream_t s, const TileGeom* geom, int ntiles, long long npix_max,
+                         WarpPatch* patches, int npatch, int pw, int ph, uint32_t* wloc,
+                         float* wfxy)
 {
     dim3 g1((unsigned)((npix_max + kWB - 1) / kWB), ntiles);
-    hipLaunchKernelGGL(k_warp_coords, g1, dim3(kWB), 0, s, geom, pw, ph, wxy, (float2*)wfxy);
+    hipLaunchKernelGGL(k_warp_coords, g1, dim3(kWB), 0, s, geom, pw, ph, wloc, (float2*)wfxy);
+    hipLaunchKernelGGL(k_patch_box, dim3(npatch), dim3(kWB), 0, s, geom, patches, pw,
+                       (const uint32_t*)wloc);
+    hipLaunchKernelGGL(k_warp_local, dim3(npatch), dim3(kWB), 0, s, geom,
+                       (const WarpPatch*)patches, pw, ph, wloc);
 }
 
-void launch_warp_entries(hipStream_t s, const TileGeom* geom, const WarpRegion* regions,
-                         int nregions, const uint32_t* perm, const uint32_t* wxy,
-                         const float* wfxy, int pw, int ph, WarpEntry* entries)
-{
-    hipLaunchKernelGGL(k_warp_entries, dim3((unsigned)nregions), dim3(kWB), 0, s, geom, regions,
-                       perm, wxy, (const float2*)wfxy, pw, ph, entries);
-}
+int warp_patch_edge() { return kPatch; }
 
-void launch_warp_depth(hipStream_t s, const TileGeom* geom, int ntiles, const WarpRegion* regions,
-                       int nregions, const WarpEntry* entries, const float* pano, int pw, int ph,
-                       long long pstride, const Resp* resp, float* tiles, long long tstride,
-                       int batch)
+void launch_warp_depth(hipStream_t s, const TileGeom* geom, int ntiles, const WarpPatch* patches,
+                       int npatch, const uint32_t* wloc, const float* wfxy, const float* pano,
+                       int pw, int ph, long long pstride, const Resp* resp, float* tiles,
+                       long long tstride, int batch)
 {
-    const long long n = (long long)nregions * ((batch + kNB - 1) / kNB);
-    static const int order = getenv("PF_WARP_ORDER") ? atoi(getenv("PF_WARP_ORDER")) : 0;
-    hipLaunchKernelGGL(k_warp_depth, dim3((unsigned)n), dim3(kWB), 0, s, geom, ntiles, regions,
-                       nregions, entries, pano, pw, ph, pstride, resp, tiles, tstride, batch,
-                       order);
+    const long long n = (long long)npatch * ((batch + kNB - 1) / kNB);
+    hipLaunchKernelGGL(k_warp_depth, dim3((unsigned)n), dim3(kWB), 0, s, geom, ntiles, patches,
+                       npatch, wloc, (const float2*)wfxy, pano, pw, ph, pstride, resp, tiles,
+                       tstride, batch);
 }
 
 }  // namespace pf

@@ -122,31 +122,63 @@ def fuse_tile_sharded(backend, nlevels, ntiles, rank, world, comm=None):
 # so every rank holds the full buffer the next level upsamples; the u16 bands likewise.
 
 class TorchComm:
-    """The collectives fuse_row_sharded needs, over torch.distributed (RCCL on the GPU box,
-    gloo on CPU)."""
+    """The collectives fuse_row_sharded / fuse_tile_sharded need, over torch.distributed (RCCL
+    on the GPU box, gloo on CPU).  stage_host=True runs every collective on host copies of
+    device tensors (gloo with GPU data: several ranks sharing one GPU, where RCCL refuses a
+    duplicate device) -- same values, the copies are exact."""
 
-    def __init__(self, dist, group=None):
-        self.dist, self.group = dist, group
+    def __init__(self, dist, group=None, stage_host=False):
+        self.dist, self.group, self.stage = dist, group, stage_host
+
+    def _host(self, t):
+        return t.cpu() if self.stage and t.device.type != "cpu" else t
+
+    def _back(self, h, t):
+        if h is not t:
+            t.copy_(h)
 
     def all_reduce_sum(self, t):
-        self.dist.all_reduce(t, op=self.dist.ReduceOp.SUM, group=self.group)
+        h = self._host(t)
+        self.dist.all_reduce(h, op=self.dist.ReduceOp.SUM, group=self.group)
+        self._back(h, t)
 
     def reduce_sum(self, t, dst):
-        self.dist.reduce(t, dst=dst, op=self.dist.ReduceOp.SUM, group=self.group)
+        h = self._host(t)
+        self.dist.reduce(h, dst=dst, op=self.dist.ReduceOp.SUM, group=self.group)
+        self._back(h, t)
 
     def exchange(self, sends, recvs):
         """sends: [(peer, tensor)], recvs: [(peer, tensor)]; point-to-point, all at once."""
-        ops = [self.dist.P2POp(self.dist.isend, t, peer, group=self.group) for peer, t in sends]
-        ops += [self.dist.P2POp(self.dist.irecv, t, peer, group=self.group) for peer, t in recvs]
+        hs = [(peer, self._host(t)) for peer, t in sends]
+        hr = [(peer, self._host(t), t) for peer, t in recvs]
+        ops = [self.dist.P2POp(self.dist.isend, t, peer, group=self.group) for peer, t in hs]
+        ops += [self.dist.P2POp(self.dist.irecv, h, peer, group=self.group) for peer, h, _ in hr]
         if ops:
             for req in self.dist.batch_isend_irecv(ops):
                 req.wait()
+        for _, h, t in hr:
+            self._back(h, t)
 
     def broadcast(self, t, src):
         import torch
         if t.dtype == torch.int16:  # the u16 result: as bytes (gloo has no 16-bit integers)
             t = t.view(torch.uint8)
-        self.dist.broadcast(t, src=src, group=self.group)
+        h = self._host(t)
+        self.dist.broadcast(h, src=src, group=self.group)
+        self._back(h, t)
+
+    def agree(self, values, src=0, device=None):
+        """Rank `src`'s list of small ints on every rank (the pass plan of a level: every rank
+        must run the same passes, or the halo exchanges would not pair up)."""
+        import torch
+        dev = device if (device is not None and not self.stage) else "cpu"
+        n = torch.tensor([len(values)], dtype=torch.int64, device=dev)
+        self.dist.broadcast(n, src=src, group=self.group)
+        v = torch.zeros(int(n.item()), dtype=torch.int64, device=dev)
+        if len(values) == v.numel():
+            v.copy_(torch.tensor(values, dtype=torch.int64))
+        self.dist.broadcast(v, src=src, group=self.group)
+        return [int(x) for x in v.tolist()]
 
 
 def band_rows(h0, h1, rank, world):
@@ -188,6 +220,10 @@ def fuse_row_sharded(backend, nlevels, ntiles, rank, world, comm=None):
         w, h, h0, h1 = backend.dims(level)
         r0, r1 = band_rows(h0, h1, rank, world)
         plan = backend.plan(level, world)
+        if world > 1 and hasattr(comm, "agree"):
+            # one plan for all ranks: rank 0's (the plan depends on per-process state -- CU
+            # count, occupancy, PF_J* overrides -- and mismatched passes would hang the exchanges)
+            plan = comm.agree(plan, 0, getattr(backend, "device", None))
         if world > 1 and (h1 - h0 + 1) // world < max(plan) + 1:
             raise ValueError(f"level {level}: {h1 - h0 + 1} band rows over {world} ranks leave "
                              f"bands thinner than the {max(plan) + 1}-row halo")
@@ -236,6 +272,10 @@ class HipRowShardBackend:
     def dims(self, level):
         w, h, h0, h1 = self.levels[level][:4]
         return w, h, h0, h1
+
+    @property
+    def device(self):
+        return self.tiles.device
 
     def plane(self, level):
         import torch
