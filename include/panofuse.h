@@ -192,6 +192,20 @@ int pf_fuse_band_pass(pf_ctx* ctx, const float* emap, int ew, int eh, int ec, co
 int pf_profile_enable(pf_ctx* ctx, int on);
 int pf_profile_read(pf_ctx* ctx, double* ms, double* bytes, long long* launches);
 
+/* ---- Jacobi engine selection (no reference counterpart; every engine is bit-identical) ----
+ * mode 1 (default; the environment variable PF_JRES=0 changes the default to 0): levels of
+ * width 256 or 512 with the separable-coverage certificate run all their sweeps in one resident
+ * launch, in row_blocks blocks per panorama (0: chosen by the cost model); mode 0: the
+ * streaming temporally blocked passes everywhere. */
+int pf_set_jacobi_engine(pf_ctx* ctx, int mode, int row_blocks);
+
+/* ---- resident level kernel health (no reference counterpart) ----
+ * The coarse fusion level runs all its sweeps in one launch whose row blocks trade halo rows
+ * through device memory (pf_jres.hip).  Its waits are bounded: a wait that times out is counted
+ * here instead of hanging the device (the level's result is then invalid).  Synchronises the
+ * context stream; returns the count since the context was created (>= 0) or an error code. */
+int pf_jres_errors(pf_ctx* ctx);
+
 /* ---- parity probes (bit-exact index maps) ----
  * For level `level` of out_w: per covered pixel and tap k (5 taps in std::map order), the
  * linear tile index (Y*W+X)*C of the tap for the first covering tile, -1 elsewhere.

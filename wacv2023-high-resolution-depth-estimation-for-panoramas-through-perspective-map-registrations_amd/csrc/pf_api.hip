@@ -80,6 +80,12 @@ struct pf_ctx {
     DevBuf sm_box, sm_cols, sm_rows, sm_src, sm_mask;
     // level-0 seed index tables of the streaming Jacobi (run_jacobi), keyed by level and emap
     DevBuf seed_ecol, seed_erow;
+    // resident level kernel (pf_jres.hip): hand-off rows, and the sync words ([0] ticket
+    // counter, [1] spin timeouts, [2..] one flag per row block); tickets and flags are
+    // monotone across launches (jres_tk, jres_fb), so nothing is reset between launches
+    DevBuf jres_x, jres_sync;
+    uint32_t jres_tk = 0, jres_fb = 1;
+    int jres_mode = -1, jres_nb = 0;  // pf_set_jacobi_engine (-1: not set, PF_JRES decides)
     int seed_key[5] = {0, 0, 0, 0, 0};
     // stage profiling
     struct Span {
@@ -294,7 +300,8 @@ void pf_destroy(pf_ctx* c)
     DevBuf* all[] = {&c->geom, &c->reg, &c->rcols, &c->rrows, &c->cams, &c->rgb_off,
                      &c->buf[0], &c->buf[1], &c->buf[2], &c->lnorm, &c->coeffs, &c->lsum_ws,
                      &c->wmap, &c->wfxy, &c->wpatch, &c->metrics_ws, &c->reg_sums,
-                     &c->reg_active};
+                     &c->reg_active, &c->sm_box, &c->sm_cols, &c->sm_rows, &c->sm_src,
+                     &c->sm_mask, &c->seed_ecol, &c->seed_erow, &c->jres_x, &c->jres_sync};
     for (DevBuf* b : all) release(*b);
     for (int l = 0; l < 4; l++) {
         release(c->lc.box[l]);
@@ -321,6 +328,25 @@ void pf_destroy(pf_ctx* c)
 }
 
 const char* pf_last_error(const pf_ctx* c) { return c ? c->err.c_str() : "null context"; }
+
+int pf_set_jacobi_engine(pf_ctx* c, int mode, int row_blocks)
+{
+    if (!c || mode < 0 || mode > 1 || row_blocks < 0) return PF_EINVAL;
+    c->jres_mode = mode;
+    c->jres_nb = row_blocks;
+    return PF_OK;
+}
+
+int pf_jres_errors(pf_ctx* c)
+{
+    if (!c) return PF_EINVAL;
+    HIPCHK(c, hipSetDevice(c->device));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    if (!c->jres_sync.p) return 0;
+    uint32_t n = 0;
+    HIPCHK(c, hipMemcpy(&n, (const uint32_t*)c->jres_sync.p + 1, sizeof(n), hipMemcpyDeviceToHost));
+    return (int)(n & 0x7FFFFFFF);
+}
 
 int pf_set_solver(pf_ctx* c, int solver)
 {
@@ -858,13 +884,127 @@ static int seed_tables(pf_ctx* c, const LevelDims& L, int ew, int eh, int ec)
     return PF_OK;
 }
 
+// The resident level kernel (pf_jres.hip): one launch for all of a level's sweeps, for the
+// widths it is built for (a wave holds whole rows) and levels with the packed-form certificate.
+// nb row blocks per panorama of `core` rows; every K sweeps the blocks trade K halo rows.
+struct JresPlan {
+    bool on = false;
+    int nb = 0, core = 0, K = 0, rounds = 0;
+};
+
+static JresPlan jres_plan(pf_ctx* c, const LevelDims& L, int batch, bool fast)
+{
+    JresPlan jp;
+    static const char* env = getenv("PF_JRES");  // "0": streaming passes only (A/B runs)
+    const int mode = c->jres_mode >= 0 ? c->jres_mode : (env && atoi(env) == 0 ? 0 : 1);
+    if (mode == 0 || !fast || batch < 1) return jp;
+    const int rs = jres_rows_per_wave(L.w);
+    if (rs <= 0 || L.iters < 1) return jp;
+    static int bpc = -1;
+    if (bpc < 0) bpc = jres_blocks_per_cu(512);
+    if (bpc < 1) return jp;
+    const int rows = 16 * rs;  // region rows of one workgroup
+    const int band = L.h1 - L.h0 + 1;
+    // cost in sweep units: the blocks run in ceil(blocks / resident) rounds of residency, each
+    // sweep costs one unit (fixed region size), each K-sweep hand-off ~2.5 units (measured
+    // hand-off latency on MI355X is 2-3 us against ~1.2 us per sweep)
+    static const double xcost = getenv("PF_JRES_X") ? atof(getenv("PF_JRES_X")) : 2.5;
+    static const int nb_env = getenv("PF_JRES_NB") ? atoi(getenv("PF_JRES_NB")) : 0;
+    const int nb_force = c->jres_nb > 0 ? c->jres_nb : nb_env;
+    double best = 1e300;
+    for (int nb = 1; nb <= band && nb <= 64; nb++) {
+        if (nb_force > 0 && nb != nb_force) continue;
+        const int core = (band + nb - 1) / nb;
+        if ((band + core - 1) / core != nb) continue;
+        int K;
+        if (nb == 1) {
+            if (core > rows) continue;
+            K = L.iters;
+        } else {
+            K = (rows - core) / 2;
+            if (K > core) K = core;
+            if (K > L.iters) K = L.iters;
+            if (K < 1) continue;
+        }
+        const int rounds = (L.iters + K - 1) / K;
+        const long long resident = (long long)c->num_cu * bpc;
+        const long long waves = ((long long)batch * nb + resident - 1) / resident;
+        const double cost = (double)waves * (L.iters + (rounds - 1) * xcost);
+        if (cost < best) {
+            best = cost;
+            jp.on = true;
+            jp.nb = nb;
+            jp.core = core;
+            jp.K = K;
+            jp.rounds = rounds;
+        }
+    }
+    return jp;
+}
+
+// The resident kernel's buffers (outside the timed stage: a first allocation synchronises).
+static int jres_prepare(pf_ctx* c, const LevelDims& L, int batch, const JresPlan& jp)
+{
+    int rc;
+    const size_t xb = sizeof(float) * (size_t)batch * jp.nb * 4 * (size_t)jp.K * L.w;
+    if ((rc = ensure(c, c->jres_x, xb))) return rc;
+    const size_t sb = sizeof(uint32_t) * (2 + (size_t)batch * jp.nb);
+    if (c->jres_sync.bytes < sb) {
+        if ((rc = ensure(c, c->jres_sync, sb))) return rc;
+        HIPCHK(c, hipMemsetAsync(c->jres_sync.p, 0, sb, c->stream));
+        c->jres_tk = 0;
+        c->jres_fb = 1;
+    }
+    return PF_OK;
+}
+
 static float* run_jacobi(pf_ctx* c, const LevelDims& L, int first, const float* emap, int ew,
                          int eh, int ec, long long estride, const GridCol* cols,
                          const GridRow* rows, const float* prev, long long pstride,
                          const float* lnorm, float* a, float* b, uint16_t* out,
-                         long long ostride, int batch, int* npasses, const float* hcol)
+                         long long ostride, int batch, int* npasses, const float* hcol,
+                         const JresPlan* jp = nullptr)
 {
     static const JacobiTuning tune = jacobi_tuning();
+    if (jp && jp->on) {
+        JresArgs A{};
+        A.src_mode = first;
+        if (first == 2) {
+            const int key[5] = {L.w, L.h, ew, eh, ec};
+            if (!emap || memcmp(key, c->seed_key, sizeof(key)) != 0) return nullptr;
+            A.ecol = (const int*)c->seed_ecol.p;
+            A.erow = (const int*)c->seed_erow.p;
+        }
+        const long long st = (long long)L.w * L.h;
+        A.src = a; A.sstride = st;
+        A.prev = prev; A.pstride = pstride;
+        A.emap = emap; A.estride = estride;
+        A.lnorm = lnorm; A.lstride = st;
+        A.hcol = hcol;
+        float* dst = first == 0 ? b : a;
+        A.dst = dst; A.dstride = st;
+        A.out = out; A.ostride = ostride;
+        A.w = L.w; A.h = L.h; A.h0 = L.h0; A.h1 = L.h1; A.iters = L.iters; A.batch = batch;
+        A.nb = jp->nb; A.core = jp->core; A.K = jp->K;
+        uint32_t* sync = (uint32_t*)c->jres_sync.p;
+        A.xbuf = (float*)c->jres_x.p;
+        A.ticket = sync;
+        A.err = sync + 1;
+        A.flags = sync + 2;
+        static const int dbg = getenv("PF_JRES_DBG") ? atoi(getenv("PF_JRES_DBG")) : 0;
+        A.dbg = dbg;
+        A.tbase = c->jres_tk;
+        A.fbase = c->jres_fb;
+        c->jres_tk += (uint32_t)(batch * jp->nb);
+        c->jres_fb += (uint32_t)(jp->rounds + 1);
+        static const bool show = getenv("PF_JPLAN") != nullptr;
+        if (show)
+            fprintf(stderr, "jacobi plan %dx%d band %d iters %d batch %d resident: nb %d core %d K %d rounds %d\n",
+                    L.w, L.h, L.h1 - L.h0 + 1, L.iters, batch, jp->nb, jp->core, jp->K, jp->rounds);
+        launch_jres(c->stream, A);
+        if (npasses) *npasses = 1;
+        return dst;
+    }
     static const bool slow = getenv("PF_JSLOW") != nullptr;  // force the general (scalar) form
     const long long st = (long long)L.w * L.h;
     // packed form: the level's separable-coverage certificate (pf_jacobi.hip)
@@ -1079,6 +1219,11 @@ static int fuse_range(pf_ctx* c, const float* emap, int ew, int eh, int ec, cons
                 int rc;
                 if ((rc = seed_tables(c, L, ew, eh, ec))) return rc;
             }
+            const JresPlan jp = jres_plan(c, L, batch, lc.full[l]);
+            if (jp.on) {  // outside the timed stage too (first allocation synchronises)
+                int rc;
+                if ((rc = jres_prepare(c, L, batch, jp))) return rc;
+            }
             {
                 // 12 B per pixel-update (read b, read L, write b'), SURVEY.md 8d
                 StageTimer t(c, PF_STAGE_JACOBI, B * 12.0 * band * L.iters, L.iters);
@@ -1086,7 +1231,7 @@ static int fuse_range(pf_ctx* c, const float* emap, int ew, int eh, int ec, cons
                 res = run_jacobi(c, L, l == 0 ? 2 : 1, emap, ew, eh, ec, estride, cols, rows,
                                  prev, pst, (const float*)lnorm_l, a, b, last ? out : nullptr,
                                  plane, batch, &passes,
-                                 lc.full[l] ? (const float*)lc.hcol[l].p : nullptr);
+                                 lc.full[l] ? (const float*)lc.hcol[l].p : nullptr, &jp);
                 t.set_launches(passes);  // k_jlag launches (rocprof's count for that kernel)
             }
             if (!res) return fail(c, PF_EINVAL, "level-0 seed tables missing");

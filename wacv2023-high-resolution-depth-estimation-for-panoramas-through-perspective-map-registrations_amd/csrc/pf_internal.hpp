@@ -164,6 +164,29 @@ struct JacobiPass {
     const float* hcol;  // packed form: per column 0.5 (covered) or 0 (un-windowed), w entries
 };
 
+// The resident level kernel (pf_jres.hip): all of a level's sweeps in one launch.
+struct JresArgs {
+    const float* src; long long sstride;    // src_mode 0: buffer
+    const float* prev; long long pstride;   // src_mode 1: nearest upsample of the previous level
+    const float* emap; long long estride;   // src_mode 2: level-0 seed through ecol / erow
+    const int* ecol; const int* erow;
+    const float* lnorm; long long lstride;
+    const float* hcol;                      // separable-coverage certificate (packed form)
+    float* dst; long long dstride;
+    uint16_t* out; long long ostride;       // non-null: store the u16 quantisation instead
+    int w, h, h0, h1, iters, batch, src_mode;
+    int nb, core, K;       // row blocks per panorama, core rows per block, sweeps per round
+    float* xbuf;           // hand-off rows [batch][nb][2 parity][2 edge][K][w]
+    uint32_t* flags;       // [batch][nb] last round published (monotone across launches)
+    uint32_t* ticket;      // workgroup ticket counter (monotone across launches)
+    uint32_t* err;         // spin timeouts (pf_jres_errors)
+    uint32_t tbase, fbase; // this launch's first ticket / flag base
+    int dbg;               // profiling only (wrong results): 1 = no hand-offs, 2 = no LDS edges
+};
+int jres_rows_per_wave(int w);
+int jres_blocks_per_cu(int w);
+void launch_jres(hipStream_t s, const JresArgs& A);
+
 // ------------------------------------------------------------------------------------------
 // Kernel launchers (pf_kernels.hip, pf_jacobi.hip).  All are asynchronous on `stream`.
 void launch_tapmap(hipStream_t s, const TileGeom* geom, const TapBox* tb, int ntiles,

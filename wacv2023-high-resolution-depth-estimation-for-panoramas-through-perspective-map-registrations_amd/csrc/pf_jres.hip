@@ -1,0 +1,410 @@
+// pf_jres.hip -- resident damped Jacobi for the coarse fusion level: ONE launch runs all of the
+// level's sweeps (Depth.cpp:1649-1718; 200 at level 0).
+//
+// Why: the level-0 band of a C3 panorama is 512 x 185 pixels.  The streaming engine
+// (pf_jacobi.hip) covers it with ~2 waves per SIMD and pays 40 launches, each with its 3T-1
+// fill/drain steps per row chunk and its load latency (0.92-0.99 ms per 64 panoramas, 0.11 of
+// the VALU roof).  Here the level stays on chip for all its sweeps:
+//
+//  * A workgroup (16 waves) owns a block of band rows of one panorama: `core` rows plus K halo
+//    rows on each side, 16*RS rows in all, at CPL = w/64 columns per lane -- a wave holds RS
+//    whole rows (its lanes side by side across the row), so every horizontal neighbour is in the
+//    lane's own registers except one per row end, which crosses one lane by DPP.  The levels
+//    b and L live in VGPRs for the whole launch (L is read from HBM once, not once per pass).
+//  * Vertical neighbours across waves go through LDS: after every sweep each wave writes its
+//    first and last row (double-buffered by sweep parity, so one workgroup barrier per sweep).
+//  * Blocks of one panorama exchange K rows with their neighbours every K sweeps (a "round"):
+//    after k sweeps of a round the rows within k of a block edge are stale, so after K sweeps
+//    exactly the core is current, and the neighbours' cores refresh the halos.  The hand-off is
+//    the write-through form of MI355X_MICROARCH.md (inter-workgroup visibility): sc1 row stores,
+//    every storing wave's vmcnt(0), a workgroup barrier, one sc1 flag store; the consumer polls
+//    the flag with one lane's sc1 load, joins a barrier, then reads the rows with sc1 loads.
+//  * Deadlock freedom without co-residency: a workgroup takes its (panorama, block) from a
+//    ticket counter when it STARTS, so the blocks holding tickets are running, groups are filled
+//    in ticket order, and at most one group of a launch is incomplete at any time; every other
+//    running group finishes on its own.  A launch needs only `nb` workgroups resident at once
+//    (checked on the host), however many other kernels share the chip.  Spins are bounded: a
+//    timeout counts into an error word (pf_jres_errors) instead of hanging the GPU.
+//
+// Arithmetic: the packed form of pf_jacobi.hip (JLag::sweep_packed_group), bit-identical to the
+// reference's fp32 operand order: Lcur = ((((W*q) + N*q) + C) + S*q) + E*q with q = -1/4 (every
+// product by q is exact, so the adds fold into FMAs that round where the reference rounds),
+// t = b + (L - Lcur)*H, b' = clamp01(t*(1-1e-4) + b*1e-4), H = 0.5 on windowed pixels and 0 on
+// un-windowed ones (the host's separable-coverage certificate; column 0 is never windowed, so the
+// west tap of column 0 is never needed).  The east tap of column w-1 is pixel (0, Y+1): the
+// reference's linear buffer[yy*width + xx] addressing.
+#include "pf_internal.hpp"
+
+namespace pf {
+
+namespace {
+
+typedef float f2 __attribute__((ext_vector_type(2)));
+typedef uint32_t u4v __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ float dpp_shr(float v)
+{  // lane i <- lane i-1 (wave_shr:1), lane 0 <- 0
+    return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0x138, 0xF, 0xF, true));
+}
+__device__ __forceinline__ float dpp_rol(float v)
+{  // lane i <- lane (i+1) mod 64 (wave_rol:1)
+    return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0x134, 0xF, 0xF, false));
+}
+__device__ __forceinline__ f2 pk_add_clamp01(f2 a, f2 b)
+{
+    f2 r;
+    asm("v_pk_add_f32 %0, %1, %2 clamp" : "=v"(r) : "v"(a), "v"(b));
+    return r;
+}
+__device__ __forceinline__ float add_scalar(float a, float b)
+{
+    float r;
+    asm("v_add_f32 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+    return r;
+}
+__device__ __forceinline__ float fma_scalar(float a, float b, float c)
+{
+    float r;
+    asm("v_fma_f32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+    return r;
+}
+
+// sc1 (write-through / L2-bypassing) buffer accesses for the inter-workgroup row hand-off
+constexpr int kSC1 = 16;
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc(const void* base, uint32_t bytes)
+{
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), 0, (int)bytes, 0x00020000);
+}
+
+}  // namespace
+
+template <int CPL, int RS, int SRC, bool OUT16>
+struct JRes {
+    static constexpr int NP = CPL / 2;  // column pairs per lane
+    static constexpr int NW = 16;       // waves per workgroup
+    f2 b[RS][NP];   // the level, rows wv*RS + r of the block's region
+    f2 L[RS][NP];   // targets (sanitised: non-finite -> 0)
+    f2 hc[NP];      // H of the lane's columns
+    float vq;       // -1/4 in a VGPR
+    int lane, wv;
+
+    // new values of row R (in place) from N = the old row above and S = the row below (old);
+    // on return N holds row R's old value (the next row's N).  EDGE: H = 0.
+    template <int R, bool EDGE>
+    __device__ __forceinline__ void row(f2* N, const f2* S)
+    {
+        const f2 q = {-0.25f, -0.25f};
+        const f2 reg = {(float)1e-4, (float)1e-4};
+        const f2 reg_ = {1 - (float)1e-4, 1 - (float)1e-4};
+        f2* c = b[R];
+        // east tap of the lane's last column: the next lane's first column of this row; for
+        // lane 63 (column w-1) lane 0's first column of the row below -- pixel (0, Y+1)
+        const float xr = lane == 0 ? S[0].x : c[0].x;
+        const float e_last = dpp_rol(xr);
+        f2 cur[NP];
+#pragma unroll
+        for (int k = 0; k < NP; k++) {
+            // W + N (the W*q + N*q of the reference, scaled by q below)
+            const float wx = k == 0 ? dpp_shr(c[NP - 1].y) : c[k - 1].y;
+            cur[k].x = (k == 0) ? (wx + N[k].x) : add_scalar(wx, N[k].x);
+            cur[k].y = add_scalar(c[k].x, N[k].y);
+        }
+#pragma unroll
+        for (int k = 0; k < NP; k++) cur[k] = __builtin_elementwise_fma(cur[k], q, c[k]);
+#pragma unroll
+        for (int k = 0; k < NP; k++) cur[k] = __builtin_elementwise_fma(S[k], q, cur[k]);
+#pragma unroll
+        for (int k = 0; k < NP; k++) {
+            cur[k].x = fma_scalar(c[k].y, vq, cur[k].x);
+            const float ey = k == NP - 1 ? e_last : c[k + 1].x;
+            cur[k].y = fma_scalar(ey, vq, cur[k].y);
+        }
+#pragma unroll
+        for (int k = 0; k < NP; k++) {
+            N[k] = c[k];
+            if constexpr (EDGE) {
+                // un-windowed row (h0 or h1): t = b exactly
+                c[k] = pk_add_clamp01(c[k] * reg_, c[k] * reg);
+            } else {
+                const f2 t = __builtin_elementwise_fma(L[R][k] - cur[k], hc[k], c[k]);
+                c[k] = pk_add_clamp01(t * reg_, c[k] * reg);
+            }
+        }
+    }
+
+    // one sweep over the wave's rows, top to bottom (up = the row above, then each row's old
+    // value for the next; the row below the last comes from LDS, read just before it is
+    // needed).  HAS_EDGE: this wave holds row h0 or h1 (bit r of em), which only two waves of a
+    // panorama do, so the others run the branch-free body.
+    template <int R, bool HAS_EDGE>
+    __device__ __forceinline__ void rows_from(f2* up, const float* dn_lds, uint32_t em)
+    {
+        if constexpr (R < RS) {
+            if constexpr (R + 1 < RS) {
+                if (HAS_EDGE && (em & (1u << R))) row<R, true>(up, b[R + 1]);
+                else row<R, false>(up, b[R + 1]);
+                rows_from<R + 1, HAS_EDGE>(up, dn_lds, em);
+            } else {
+                f2 dn[NP];
+#pragma unroll
+                for (int k = 0; k < NP; k++)
+                    dn[k] = dn_lds ? *reinterpret_cast<const f2*>(dn_lds + 2 * k) : f2{0.0f, 0.0f};
+                if (HAS_EDGE && (em & (1u << R))) row<R, true>(up, dn);
+                else row<R, false>(up, dn);
+            }
+        }
+    }
+};
+
+
+
+template <int CPL, int RS, int SRC, bool OUT16>
+__global__ void __launch_bounds__(1024) k_jres(JresArgs A)
+{
+    using S_t = JRes<CPL, RS, SRC, OUT16>;
+    constexpr int NP = S_t::NP, NW = S_t::NW;
+    __shared__ float lds_edge[2][2][NW][64 * CPL];  // [sweep parity][0 top / 1 bottom][wave]
+    __shared__ uint32_t lds_ticket;
+    const int tid = threadIdx.x;
+    S_t S;
+    S.lane = tid & 63;
+    S.wv = __builtin_amdgcn_readfirstlane(tid >> 6);
+    S.vq = -0.25f;
+    asm volatile("" : "+v"(S.vq));
+    const int lane = S.lane, wv = S.wv;
+    if (tid == 0) lds_ticket = __hip_atomic_fetch_add(A.ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __syncthreads();
+    const uint32_t t = __builtin_amdgcn_readfirstlane(lds_ticket - A.tbase);
+    const int p = (int)(t / (uint32_t)A.nb), j = (int)(t % (uint32_t)A.nb);
+    const int w = A.w;
+    const int c0 = A.h0 + j * A.core;
+    const int c1 = min(c0 + A.core, A.h1 + 1);
+    const int K = A.K;
+    const int rs = j == 0 ? A.h0 : c0 - K;                       // region's first row
+    const int re = j == A.nb - 1 ? A.h1 + 1 : min(c1 + K, A.h1 + 1);  // one past its last row
+    const int x0 = lane * CPL;
+
+    // ---- initial state of the region, targets, H
+    {
+        const float* lp = A.lnorm + p * A.lstride;
+#pragma unroll
+        for (int k = 0; k < NP; k++) {
+            S.hc[k].x = A.hcol[x0 + 2 * k];
+            S.hc[k].y = A.hcol[x0 + 2 * k + 1];
+        }
+#pragma unroll
+        for (int r = 0; r < RS; r++) {
+            const int Y = rs + wv * RS + r;
+            const bool live = Y < re;
+#pragma unroll
+            for (int k = 0; k < NP; k++) {
+                float v0 = 0.0f, v1 = 0.0f, l0 = 0.0f, l1 = 0.0f;
+                if (live) {
+                    const int x = x0 + 2 * k;
+                    if constexpr (SRC == 2) {  // level-0 seed (Depth.cpp:1442-1465)
+                        const float* ep = A.emap + p * A.estride + A.erow[Y + 1];
+                        v0 = ep[A.ecol[x + 1]];
+                        v1 = ep[A.ecol[x + 2]];
+                    } else if constexpr (SRC == 1) {  // nearest upsample (Depth.cpp:1467-1485)
+                        v0 = v1 = A.prev[p * A.pstride + (long long)(Y >> 1) * (w >> 1) + (x >> 1)];
+                    } else {
+                        const float2 q = *reinterpret_cast<const float2*>(A.src + p * A.sstride + (long long)Y * w + x);
+                        v0 = q.x;
+                        v1 = q.y;
+                    }
+                    const float2 lq = *reinterpret_cast<const float2*>(lp + (long long)Y * w + x);
+                    l0 = __builtin_isfinite(lq.x) ? lq.x : 0.0f;
+                    l1 = __builtin_isfinite(lq.y) ? lq.y : 0.0f;
+                }
+                S.b[r][k] = f2{v0, v1};
+                S.L[r][k] = f2{l0, l1};
+            }
+        }
+    }
+    // rows h0 / h1 of this wave: un-windowed (their update ignores the neighbours)
+    uint32_t em = 0;
+#pragma unroll
+    for (int r = 0; r < RS; r++) {
+        const int Y = rs + wv * RS + r;
+        if (Y == A.h0 || Y == A.h1) em |= 1u << r;
+    }
+    em = __builtin_amdgcn_readfirstlane(em);
+
+    const auto put_edges = [&](int pb) {
+        float* top = &lds_edge[pb][0][wv][x0];
+        float* bot = &lds_edge[pb][1][wv][x0];
+#pragma unroll
+        for (int k = 0; k < NP; k++) {
+            *reinterpret_cast<f2*>(top + 2 * k) = S.b[0][k];
+            *reinterpret_cast<f2*>(bot + 2 * k) = S.b[RS - 1][k];
+        }
+    };
+
+    const long long xplane = (long long)K * w;  // floats of one published edge
+    float* const xb = A.xbuf;
+    int s = 0, round = 0;
+    while (true) {
+        const int n = min(K, A.iters - s);
+        put_edges(0);
+        __syncthreads();
+        if (A.dbg & 2) {
+            for (int i = 0; i < n; i++) {
+                f2 up[NP];
+#pragma unroll
+                for (int k = 0; k < NP; k++) up[k] = S.b[RS - 1][k];
+                const float* dn = &lds_edge[0][0][wv][x0];
+                if (em) S.template rows_from<0, true>(up, dn, em);
+                else S.template rows_from<0, false>(up, dn, em);
+            }
+        } else {
+        for (int i = 0; i < n; i++) {
+            const int cb = i & 1;
+            f2 up[NP];
+#pragma unroll
+            for (int k = 0; k < NP; k++)
+                up[k] = wv > 0 ? *reinterpret_cast<const f2*>(&lds_edge[cb][1][wv > 0 ? wv - 1 : 0][x0 + 2 * k]) : f2{0.0f, 0.0f};
+            const float* dn = wv < NW - 1 ? &lds_edge[cb][0][wv < NW - 1 ? wv + 1 : 0][x0] : nullptr;
+            if (em) S.template rows_from<0, true>(up, dn, em);
+            else S.template rows_from<0, false>(up, dn, em);
+            put_edges(cb ^ 1);
+            __syncthreads();
+        }
+        }
+        s += n;
+        round++;
+        if (s >= A.iters) break;
+        if (A.dbg & 1) continue;
+
+        // ---- hand-off: publish the core's first / last K rows, take the neighbours'
+        const int par = round & 1;
+        float* mine = xb + ((long long)(p * A.nb + j) * 2 + par) * 2 * xplane;
+        const auto mr = rsrc(mine, (uint32_t)(sizeof(float) * xplane * 2));
+#pragma unroll
+        for (int r = 0; r < RS; r++) {
+            const int Y = rs + wv * RS + r;
+            // a row can be in both published sets when core < 2K
+#pragma unroll
+            for (int e = 0; e < 2; e++) {
+                const bool pub = e == 0 ? (j > 0 && Y >= c0 && Y < c0 + K)
+                                        : (j < A.nb - 1 && Y >= c1 - K && Y < c1);
+                if (!pub) continue;  // wave-uniform
+                const int yo = e == 0 ? Y - c0 : Y - (c1 - K);
+                const int off = (int)(sizeof(float) * (e * xplane + (long long)yo * w + x0));
+#pragma unroll
+                for (int k = 0; k < NP; k += 2) {
+                    u4v v;
+                    v[0] = __float_as_uint(S.b[r][k].x);
+                    v[1] = __float_as_uint(S.b[r][k].y);
+                    v[2] = __float_as_uint(S.b[r][k + 1].x);
+                    v[3] = __float_as_uint(S.b[r][k + 1].y);
+                    __builtin_amdgcn_raw_buffer_store_b128(v, mr, off + 8 * k, 0, kSC1);
+                }
+            }
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        const uint32_t want = A.fbase + (uint32_t)round;
+        if (tid == 0) {
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            __hip_atomic_store(&A.flags[p * A.nb + j], want, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            // wait for the neighbours' rows of this round (bounded: a timeout is counted, never hangs)
+            for (int nbj = j - 1; nbj <= j + 1; nbj += 2) {
+                if (nbj < 0 || nbj >= A.nb) continue;
+                uint32_t* f = &A.flags[p * A.nb + nbj];
+                int spins = 0;
+                while ((int)(__hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) - want) < 0) {
+                    __builtin_amdgcn_s_sleep(2);
+                    if (++spins > (1 << 24)) {
+                        __hip_atomic_fetch_add(A.err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                        break;
+                    }
+                }
+            }
+        }
+        __syncthreads();
+#pragma unroll
+        for (int r = 0; r < RS; r++) {
+            const int Y = rs + wv * RS + r;
+            int src_j = -1, e = 0, yo = 0;
+            if (j > 0 && Y >= c0 - K && Y < c0) { src_j = j - 1; e = 1; yo = Y - (c0 - K); }
+            else if (j < A.nb - 1 && Y >= c1 && Y < re) { src_j = j + 1; e = 0; yo = Y - c1; }
+            if (src_j >= 0) {  // wave-uniform
+                const float* theirs = xb + ((long long)(p * A.nb + src_j) * 2 + par) * 2 * xplane;
+                const auto tr = rsrc(theirs, (uint32_t)(sizeof(float) * xplane * 2));
+                const int off = (int)(sizeof(float) * (e * xplane + (long long)yo * w + x0));
+#pragma unroll
+                for (int k = 0; k < NP; k += 2) {
+                    const u4v v = __builtin_amdgcn_raw_buffer_load_b128(tr, off + 8 * k, 0, kSC1);
+                    S.b[r][k] = f2{__uint_as_float(v[0]), __uint_as_float(v[1])};
+                    S.b[r][k + 1] = f2{__uint_as_float(v[2]), __uint_as_float(v[3])};
+                }
+            }
+        }
+    }
+
+    // ---- the core rows of the finished level
+#pragma unroll
+    for (int r = 0; r < RS; r++) {
+        const int Y = rs + wv * RS + r;
+        if (Y < c0 || Y >= c1) continue;  // wave-uniform
+        const long long o = (long long)Y * w + x0;
+        if constexpr (OUT16) {
+            uint16_t* op = A.out + p * A.ostride + o;
+#pragma unroll
+            for (int k = 0; k < NP; k++) {
+                // quantise (Depth.cpp:1721-1736); b is already in [0, 1], truncating cast
+                const uint32_t q0 = (uint32_t)(S.b[r][k].x * 65535.0f);
+                const uint32_t q1 = (uint32_t)(S.b[r][k].y * 65535.0f);
+                *reinterpret_cast<uint32_t*>(op + 2 * k) = q0 | (q1 << 16);
+            }
+        } else {
+            float* dp = A.dst + p * A.dstride + o;
+#pragma unroll
+            for (int k = 0; k < NP; k += 2)
+                *reinterpret_cast<float4*>(dp + 2 * k) =
+                    make_float4(S.b[r][k].x, S.b[r][k].y, S.b[r][k + 1].x, S.b[r][k + 1].y);
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------------------------
+// Host side.
+template <int CPL, int RS, int SRC, bool OUT16>
+static void launch_t(hipStream_t s, const JresArgs& A, int grid)
+{
+    hipLaunchKernelGGL((k_jres<CPL, RS, SRC, OUT16>), dim3(grid), dim3(1024), 0, s, A);
+}
+template <int CPL, int RS>
+static void launch_cr(hipStream_t s, const JresArgs& A, int grid, int src_mode, bool out16)
+{
+    if (out16) {
+        if (src_mode == 2) launch_t<CPL, RS, 2, true>(s, A, grid);
+        else if (src_mode == 1) launch_t<CPL, RS, 1, true>(s, A, grid);
+        else launch_t<CPL, RS, 0, true>(s, A, grid);
+    } else {
+        if (src_mode == 2) launch_t<CPL, RS, 2, false>(s, A, grid);
+        else if (src_mode == 1) launch_t<CPL, RS, 1, false>(s, A, grid);
+        else launch_t<CPL, RS, 0, false>(s, A, grid);
+    }
+}
+
+// rows per wave of the resident kernel at this width (0: not supported)
+int jres_rows_per_wave(int w) { return w == 512 ? 4 : (w == 256 ? 8 : 0); }
+
+void launch_jres(hipStream_t s, const JresArgs& A)
+{
+    const int grid = A.nb * A.batch;
+    if (A.w == 512) launch_cr<8, 4>(s, A, grid, A.src_mode, A.out != nullptr);
+    else if (A.w == 256) launch_cr<4, 8>(s, A, grid, A.src_mode, A.out != nullptr);
+}
+
+int jres_blocks_per_cu(int w)
+{
+    int nb = 0;
+    const void* f = w == 256 ? reinterpret_cast<const void*>(k_jres<4, 8, 0, false>)
+                             : reinterpret_cast<const void*>(k_jres<8, 4, 0, false>);
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, f, 1024, 0) != hipSuccess) nb = 0;
+    return nb;
+}
+
+}  // namespace pf

@@ -27,6 +27,7 @@ EXPORTS = [
     "pf_depth_transform", "pf_register_joint", "pf_set_solver", "pf_fuse_normalize",
     "pf_fuse_border", "pf_fuse_band_plan", "pf_fuse_band_pass", "pf_fuse_multicover",
     "pf_fuse_multicover_patch", "pf_solve_smoothing", "pf_set_metrics_order",
+    "pf_jres_errors", "pf_set_jacobi_engine",
 ]
 METRICS_ORDERS = {"tree": 0, "sequential": 1}  # PF_METRICS_*; "sequential" = the reference's
 SOLVERS = {"normal": 0, "lm": 1}  # PF_SOLVER_*; "lm" = the reference's Ceres LM (default)
@@ -99,6 +100,8 @@ def load():
     L.pf_fuse_band_pass.argtypes = [vp, vp, ip, ip, ip, vp, vp, ip, vp, vp, vp, ip, ip, fp, fp,
                                     ip, ip, ip, ip]
     L.pf_profile_enable.argtypes = [vp, ip]
+    L.pf_jres_errors.argtypes = [vp]
+    L.pf_set_jacobi_engine.argtypes = [vp, ip, ip]
     L.pf_profile_read.argtypes = [vp, C.POINTER(C.c_double), C.POINTER(C.c_double),
                                   C.POINTER(C.c_longlong)]
     for name in EXPORTS:
@@ -364,6 +367,19 @@ class Fuser:
 
     def synchronize(self):
         self._check(self.L.pf_synchronize(self.h))
+
+    def set_jacobi_engine(self, resident=True, row_blocks=0):
+        """Jacobi engine of the fusion levels: the resident one-launch kernel where it applies
+        (default) or the streaming passes; row_blocks forces its blocks per panorama."""
+        self._check(self.L.pf_set_jacobi_engine(self.h, 1 if resident else 0, int(row_blocks)))
+
+    def jres_errors(self):
+        """Timed-out hand-off waits of the resident level kernel so far (0 = every resident
+        level result is valid); synchronises."""
+        n = self.L.pf_jres_errors(self.h)
+        if n < 0:
+            self._check(n)
+        return n
 
 
 def make_responses(params, device):
