@@ -20,5 +20,5 @@ PY
 run default PF_JPLAN=1 || exit 1
 grep "resident" $OUT/default.log | sort | uniq -c
 for v in ${VARIANTS:-dbg1:PF_JRES_DBG=1 dbg2:PF_JRES_DBG=2 dbg3:PF_JRES_DBG=3 nb3:PF_JRES_NB=3 nb5:PF_JRES_NB=5 nb6:PF_JRES_NB=6}; do
-  run ${v%%:*} ${v#*:} || exit 1
+  run ${v%%:*} $(echo ${v#*:} | tr "," " ") || exit 1
 done

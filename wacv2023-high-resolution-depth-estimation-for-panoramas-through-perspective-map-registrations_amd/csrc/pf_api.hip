@@ -898,12 +898,11 @@ static JresPlan jres_plan(pf_ctx* c, const LevelDims& L, int batch, bool fast)
     static const char* env = getenv("PF_JRES");  // "0": streaming passes only (A/B runs)
     const int mode = c->jres_mode >= 0 ? c->jres_mode : (env && atoi(env) == 0 ? 0 : 1);
     if (mode == 0 || !fast || batch < 1) return jp;
-    const int rs = jres_rows_per_wave(L.w);
-    if (rs <= 0 || L.iters < 1) return jp;
+    const int rows = jres_region_rows(L.w);  // region rows of one workgroup
+    if (rows <= 0 || L.iters < 1) return jp;
     static int bpc = -1;
     if (bpc < 0) bpc = jres_blocks_per_cu(512);
     if (bpc < 1) return jp;
-    const int rows = 16 * rs;  // region rows of one workgroup
     const int band = L.h1 - L.h0 + 1;
     // cost in sweep units: the blocks run in ceil(blocks / resident) rounds of residency, each
     // sweep costs one unit (fixed region size), each K-sweep hand-off ~2.5 units (measured

@@ -181,9 +181,10 @@ struct JresArgs {
     uint32_t* ticket;      // workgroup ticket counter (monotone across launches)
     uint32_t* err;         // spin timeouts (pf_jres_errors)
     uint32_t tbase, fbase; // this launch's first ticket / flag base
-    int dbg;               // profiling only (wrong results): 1 = no hand-offs, 2 = no LDS edges
+    int dbg;               // profiling only (wrong results): 1 = no hand-offs
 };
-int jres_rows_per_wave(int w);
+int jres_region_rows(int w);
+int jres_threads();
 int jres_blocks_per_cu(int w);
 void launch_jres(hipStream_t s, const JresArgs& A);
 

@@ -78,10 +78,10 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc(const void* base, uint32_
 
 }  // namespace
 
-template <int CPL, int RS, int SRC, bool OUT16>
+template <int CPL, int RS, int NWV, int SRC, bool OUT16>
 struct JRes {
     static constexpr int NP = CPL / 2;  // column pairs per lane
-    static constexpr int NW = 16;       // waves per workgroup
+    static constexpr int NW = NWV;      // waves per workgroup
     f2 b[RS][NP];   // the level, rows wv*RS + r of the block's region
     f2 L[RS][NP];   // targets (sanitised: non-finite -> 0)
     f2 hc[NP];      // H of the lane's columns
@@ -158,10 +158,10 @@ struct JRes {
 
 
 
-template <int CPL, int RS, int SRC, bool OUT16>
-__global__ void __launch_bounds__(1024) k_jres(JresArgs A)
+template <int CPL, int RS, int NWV, int SRC, bool OUT16>
+__global__ void __launch_bounds__(64 * NWV) k_jres(JresArgs A)
 {
-    using S_t = JRes<CPL, RS, SRC, OUT16>;
+    using S_t = JRes<CPL, RS, NWV, SRC, OUT16>;
     constexpr int NP = S_t::NP, NW = S_t::NW;
     __shared__ float lds_edge[2][2][NW][64 * CPL];  // [sweep parity][0 top / 1 bottom][wave]
     __shared__ uint32_t lds_ticket;
@@ -247,16 +247,6 @@ __global__ void __launch_bounds__(1024) k_jres(JresArgs A)
         const int n = min(K, A.iters - s);
         put_edges(0);
         __syncthreads();
-        if (A.dbg & 2) {
-            for (int i = 0; i < n; i++) {
-                f2 up[NP];
-#pragma unroll
-                for (int k = 0; k < NP; k++) up[k] = S.b[RS - 1][k];
-                const float* dn = &lds_edge[0][0][wv][x0];
-                if (em) S.template rows_from<0, true>(up, dn, em);
-                else S.template rows_from<0, false>(up, dn, em);
-            }
-        } else {
         for (int i = 0; i < n; i++) {
             const int cb = i & 1;
             f2 up[NP];
@@ -269,13 +259,16 @@ __global__ void __launch_bounds__(1024) k_jres(JresArgs A)
             put_edges(cb ^ 1);
             __syncthreads();
         }
-        }
         s += n;
         round++;
         if (s >= A.iters) break;
         if (A.dbg & 1) continue;
 
         // ---- hand-off: publish the core's first / last K rows, take the neighbours'
+        // (the lane offset is re-materialised here so that the per-row offsets below are not
+        // hoisted out of the round loop, where they would sit in VGPRs through the sweeps)
+        int xl = x0;
+        asm volatile("" : "+v"(xl));
         const int par = round & 1;
         float* mine = xb + ((long long)(p * A.nb + j) * 2 + par) * 2 * xplane;
         const auto mr = rsrc(mine, (uint32_t)(sizeof(float) * xplane * 2));
@@ -289,7 +282,7 @@ __global__ void __launch_bounds__(1024) k_jres(JresArgs A)
                                         : (j < A.nb - 1 && Y >= c1 - K && Y < c1);
                 if (!pub) continue;  // wave-uniform
                 const int yo = e == 0 ? Y - c0 : Y - (c1 - K);
-                const int off = (int)(sizeof(float) * (e * xplane + (long long)yo * w + x0));
+                const int off = (int)(sizeof(float) * (e * xplane + (long long)yo * w + xl));
 #pragma unroll
                 for (int k = 0; k < NP; k += 2) {
                     u4v v;
@@ -331,7 +324,7 @@ __global__ void __launch_bounds__(1024) k_jres(JresArgs A)
             if (src_j >= 0) {  // wave-uniform
                 const float* theirs = xb + ((long long)(p * A.nb + src_j) * 2 + par) * 2 * xplane;
                 const auto tr = rsrc(theirs, (uint32_t)(sizeof(float) * xplane * 2));
-                const int off = (int)(sizeof(float) * (e * xplane + (long long)yo * w + x0));
+                const int off = (int)(sizeof(float) * (e * xplane + (long long)yo * w + xl));
 #pragma unroll
                 for (int k = 0; k < NP; k += 2) {
                     const u4v v = __builtin_amdgcn_raw_buffer_load_b128(tr, off + 8 * k, 0, kSC1);
@@ -369,41 +362,52 @@ __global__ void __launch_bounds__(1024) k_jres(JresArgs A)
 
 // ---------------------------------------------------------------------------------------------
 // Host side.
-template <int CPL, int RS, int SRC, bool OUT16>
+template <int CPL, int RS, int NWV, int SRC, bool OUT16>
 static void launch_t(hipStream_t s, const JresArgs& A, int grid)
 {
-    hipLaunchKernelGGL((k_jres<CPL, RS, SRC, OUT16>), dim3(grid), dim3(1024), 0, s, A);
+    hipLaunchKernelGGL((k_jres<CPL, RS, NWV, SRC, OUT16>), dim3(grid), dim3(64 * NWV), 0, s, A);
 }
-template <int CPL, int RS>
+template <int CPL, int RS, int NWV>
 static void launch_cr(hipStream_t s, const JresArgs& A, int grid, int src_mode, bool out16)
 {
     if (out16) {
-        if (src_mode == 2) launch_t<CPL, RS, 2, true>(s, A, grid);
-        else if (src_mode == 1) launch_t<CPL, RS, 1, true>(s, A, grid);
-        else launch_t<CPL, RS, 0, true>(s, A, grid);
+        if (src_mode == 2) launch_t<CPL, RS, NWV, 2, true>(s, A, grid);
+        else if (src_mode == 1) launch_t<CPL, RS, NWV, 1, true>(s, A, grid);
+        else launch_t<CPL, RS, NWV, 0, true>(s, A, grid);
     } else {
-        if (src_mode == 2) launch_t<CPL, RS, 2, false>(s, A, grid);
-        else if (src_mode == 1) launch_t<CPL, RS, 1, false>(s, A, grid);
-        else launch_t<CPL, RS, 0, false>(s, A, grid);
+        if (src_mode == 2) launch_t<CPL, RS, NWV, 2, false>(s, A, grid);
+        else if (src_mode == 1) launch_t<CPL, RS, NWV, 1, false>(s, A, grid);
+        else launch_t<CPL, RS, NWV, 0, false>(s, A, grid);
     }
 }
 
-// rows per wave of the resident kernel at this width (0: not supported)
-int jres_rows_per_wave(int w) { return w == 512 ? 4 : (w == 256 ? 8 : 0); }
+// Workgroup shape: PF_JRES_WAVES waves of 64-row regions -- 8 waves of 8 rows (default: two
+// waves per SIMD at <= 256 VGPRs, a third of the CU's register file left to co-resident
+// kernels such as the side-stream target gathers and the pipelined warp) or 16 waves of 4 rows
+// (one workgroup fills the CU's registers).
+#ifndef PF_JRES_WAVES
+#define PF_JRES_WAVES 8
+#endif
+static constexpr int kJW = PF_JRES_WAVES;
+static constexpr int kRS512 = 64 / kJW, kRS256 = 128 / kJW;
+
+// region rows of the resident kernel's workgroup at this width (0: not supported)
+int jres_region_rows(int w) { return w == 512 ? 64 : (w == 256 ? 128 : 0); }
+int jres_threads() { return 64 * kJW; }
 
 void launch_jres(hipStream_t s, const JresArgs& A)
 {
     const int grid = A.nb * A.batch;
-    if (A.w == 512) launch_cr<8, 4>(s, A, grid, A.src_mode, A.out != nullptr);
-    else if (A.w == 256) launch_cr<4, 8>(s, A, grid, A.src_mode, A.out != nullptr);
+    if (A.w == 512) launch_cr<8, kRS512, kJW>(s, A, grid, A.src_mode, A.out != nullptr);
+    else if (A.w == 256) launch_cr<4, kRS256, kJW>(s, A, grid, A.src_mode, A.out != nullptr);
 }
 
 int jres_blocks_per_cu(int w)
 {
     int nb = 0;
-    const void* f = w == 256 ? reinterpret_cast<const void*>(k_jres<4, 8, 0, false>)
-                             : reinterpret_cast<const void*>(k_jres<8, 4, 0, false>);
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, f, 1024, 0) != hipSuccess) nb = 0;
+    const void* f = w == 256 ? reinterpret_cast<const void*>(k_jres<4, kRS256, kJW, 0, false>)
+                             : reinterpret_cast<const void*>(k_jres<8, kRS512, kJW, 0, false>);
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, f, 64 * kJW, 0) != hipSuccess) nb = 0;
     return nb;
 }
 
