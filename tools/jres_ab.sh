@@ -9,7 +9,7 @@ export TMPDIR=/tmp
 OUT=gpurun_out/jres_ab${TAG:-}
 mkdir -p $OUT
 W16=$PWD/tools/ubench/bin/w16/libpanofuse.so
-for r in 1 2; do
+for r in 1 2 3; do
   for m in stream w8 w16; do
     case $m in
       stream) envs="PF_JRES=0" ;;
@@ -20,4 +20,4 @@ for r in 1 2; do
     tail -1 $OUT/b_${m}_$r.log | python3 -c 'import json,sys; d=json.loads(sys.stdin.read()); print("'$m' round '$r'", round(d["value"]), "pano/s", round(d["ms_per_step"], 3), "ms", {k: round(v["ms_per_step"], 3) for k, v in d["stages"].items()})'
   done
 done
-VARIANTS="noside:PF_NOSIDE=1 noside_dbg1:PF_NOSIDE=1,PF_JRES_DBG=1 w16:PANOFUSE_LIB=$W16 w16_noside:PANOFUSE_LIB=$W16,PF_NOSIDE=1" TAG=_ab bash tools/jres_probe.sh
+VARIANTS="noside:PF_NOSIDE=1 noside_dbg1:PF_NOSIDE=1,PF_JRES_DBG=1 w16:PANOFUSE_LIB=$W16 w16_noside:PANOFUSE_LIB=$W16,PF_NOSIDE=1 w16_dbg1:PANOFUSE_LIB=$W16,PF_NOSIDE=1,PF_JRES_DBG=1" TAG=_ab bash tools/jres_probe.sh

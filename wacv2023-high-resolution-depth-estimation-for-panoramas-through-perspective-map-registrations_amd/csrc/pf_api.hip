@@ -945,7 +945,8 @@ static JresPlan jres_plan(pf_ctx* c, const LevelDims& L, int batch, bool fast)
 static int jres_prepare(pf_ctx* c, const LevelDims& L, int batch, const JresPlan& jp)
 {
     int rc;
-    const size_t xb = sizeof(float) * (size_t)batch * jp.nb * 4 * (size_t)jp.K * L.w;
+    const size_t xb = sizeof(float) * jres_words_per_value() * (size_t)batch * jp.nb * 4 *
+                      (size_t)jp.K * L.w;
     if ((rc = ensure(c, c->jres_x, xb))) return rc;
     const size_t sb = sizeof(uint32_t) * (2 + (size_t)batch * jp.nb);
     if (c->jres_sync.bytes < sb) {

@@ -181,10 +181,11 @@ struct JresArgs {
     uint32_t* ticket;      // workgroup ticket counter (monotone across launches)
     uint32_t* err;         // spin timeouts (pf_jres_errors)
     uint32_t tbase, fbase; // this launch's first ticket / flag base
-    int dbg;               // profiling only (wrong results): 1 = no hand-offs
+    int dbg;               // profiling only (wrong results): 1 no hand-offs, 4 no rows, 8 no barriers
 };
 int jres_region_rows(int w);
 int jres_threads();
+int jres_words_per_value();  // 2: the hand-off rows travel as {value, tag} granules
 int jres_blocks_per_cu(int w);
 void launch_jres(hipStream_t s, const JresArgs& A);
 

@@ -69,6 +69,10 @@ __device__ __forceinline__ float fma_scalar(float a, float b, float c)
     return r;
 }
 
+#ifndef PF_JRES_GRANULE
+#define PF_JRES_GRANULE 0  // hand-off by data-tagged granules (measured 2x slower: 32-KB edges)
+#endif
+
 // sc1 (write-through / L2-bypassing) buffer accesses for the inter-workgroup row hand-off
 constexpr int kSC1 = 16;
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc(const void* base, uint32_t bytes)
@@ -132,38 +136,47 @@ struct JRes {
         }
     }
 
-    // one sweep over the wave's rows, top to bottom (up = the row above, then each row's old
-    // value for the next; the row below the last comes from LDS, read just before it is
-    // needed).  HAS_EDGE: this wave holds row h0 or h1 (bit r of em), which only two waves of a
-    // panorama do, so the others run the branch-free body.
+    // one sweep over the wave's rows.  The rows that need the neighbour waves' edge rows (row 0:
+    // the row above, from LDS; row RS-1: the row below) go last, so the LDS reads issued at the
+    // start of the sweep land while rows 1..RS-2 are computed: rows 1..RS-1 top to bottom (n =
+    // old row 0, then each row's old value for the next), then row 0 with S = old row 1 (kept).
+    // HAS_EDGE: this wave holds row h0 or h1 (bit r of em), which only two waves of a panorama
+    // do, so the others run the branch-free body.
     template <int R, bool HAS_EDGE>
-    __device__ __forceinline__ void rows_from(f2* up, const float* dn_lds, uint32_t em)
+    __device__ __forceinline__ void rows_mid(f2* n, const f2* dn, uint32_t em)
     {
         if constexpr (R < RS) {
-            if constexpr (R + 1 < RS) {
-                if (HAS_EDGE && (em & (1u << R))) row<R, true>(up, b[R + 1]);
-                else row<R, false>(up, b[R + 1]);
-                rows_from<R + 1, HAS_EDGE>(up, dn_lds, em);
-            } else {
-                f2 dn[NP];
-#pragma unroll
-                for (int k = 0; k < NP; k++)
-                    dn[k] = dn_lds ? *reinterpret_cast<const f2*>(dn_lds + 2 * k) : f2{0.0f, 0.0f};
-                if (HAS_EDGE && (em & (1u << R))) row<R, true>(up, dn);
-                else row<R, false>(up, dn);
-            }
+            const f2* S = R + 1 < RS ? b[R + 1 < RS ? R + 1 : 0] : dn;
+            if (HAS_EDGE && (em & (1u << R))) row<R, true>(n, S);
+            else row<R, false>(n, S);
+            rows_mid<R + 1, HAS_EDGE>(n, dn, em);
         }
     }
+    template <bool HAS_EDGE>
+    __device__ __forceinline__ void sweep(const f2* up_lds, const f2* dn_lds, uint32_t em)
+    {
+        f2 up[NP], dn[NP], s1[NP], n[NP];
+#pragma unroll
+        for (int k = 0; k < NP; k++) {
+            up[k] = up_lds ? up_lds[64 * k] : f2{0.0f, 0.0f};
+            dn[k] = dn_lds ? dn_lds[64 * k] : f2{0.0f, 0.0f};
+            s1[k] = b[RS > 1 ? 1 : 0][k];
+            n[k] = b[0][k];
+        }
+        if constexpr (RS > 1) rows_mid<1, HAS_EDGE>(n, dn, em);
+        if (HAS_EDGE && (em & 1u)) row<0, true>(up, RS > 1 ? s1 : dn);
+        else row<0, false>(up, RS > 1 ? s1 : dn);
+    }
 };
-
-
 
 template <int CPL, int RS, int NWV, int SRC, bool OUT16>
 __global__ void __launch_bounds__(64 * NWV) k_jres(JresArgs A)
 {
     using S_t = JRes<CPL, RS, NWV, SRC, OUT16>;
     constexpr int NP = S_t::NP, NW = S_t::NW;
-    __shared__ float lds_edge[2][2][NW][64 * CPL];  // [sweep parity][0 top / 1 bottom][wave]
+    // [sweep parity][0 top / 1 bottom][wave][column pair k][lane]: a lane's pair k of a wave's
+    // first / last row; lane-minor, so the 8-B accesses of a wave are conflict-free
+    __shared__ f2 lds_edge[2][2][NW][NP][64];
     __shared__ uint32_t lds_ticket;
     const int tid = threadIdx.x;
     S_t S;
@@ -183,6 +196,7 @@ __global__ void __launch_bounds__(64 * NWV) k_jres(JresArgs A)
     const int rs = j == 0 ? A.h0 : c0 - K;                       // region's first row
     const int re = j == A.nb - 1 ? A.h1 + 1 : min(c1 + K, A.h1 + 1);  // one past its last row
     const int x0 = lane * CPL;
+    const int qc0 = c0 - rs, qc1 = c1 - rs;  // the core in region rows
 
     // ---- initial state of the region, targets, H
     {
@@ -231,12 +245,10 @@ __global__ void __launch_bounds__(64 * NWV) k_jres(JresArgs A)
     em = __builtin_amdgcn_readfirstlane(em);
 
     const auto put_edges = [&](int pb) {
-        float* top = &lds_edge[pb][0][wv][x0];
-        float* bot = &lds_edge[pb][1][wv][x0];
 #pragma unroll
         for (int k = 0; k < NP; k++) {
-            *reinterpret_cast<f2*>(top + 2 * k) = S.b[0][k];
-            *reinterpret_cast<f2*>(bot + 2 * k) = S.b[RS - 1][k];
+            lds_edge[pb][0][wv][k][lane] = S.b[0][k];
+            lds_edge[pb][1][wv][k][lane] = S.b[RS - 1][k];
         }
     };
 
@@ -249,15 +261,22 @@ __global__ void __launch_bounds__(64 * NWV) k_jres(JresArgs A)
         __syncthreads();
         for (int i = 0; i < n; i++) {
             const int cb = i & 1;
-            f2 up[NP];
-#pragma unroll
-            for (int k = 0; k < NP; k++)
-                up[k] = wv > 0 ? *reinterpret_cast<const f2*>(&lds_edge[cb][1][wv > 0 ? wv - 1 : 0][x0 + 2 * k]) : f2{0.0f, 0.0f};
-            const float* dn = wv < NW - 1 ? &lds_edge[cb][0][wv < NW - 1 ? wv + 1 : 0][x0] : nullptr;
-            if (em) S.template rows_from<0, true>(up, dn, em);
-            else S.template rows_from<0, false>(up, dn, em);
-            put_edges(cb ^ 1);
-            __syncthreads();
+            const f2* up = wv > 0 ? &lds_edge[cb][1][wv > 0 ? wv - 1 : 0][0][lane] : nullptr;
+            const f2* dn = wv < NW - 1 ? &lds_edge[cb][0][wv < NW - 1 ? wv + 1 : 0][0][lane] : nullptr;
+            // Dependency cone: sweep i of the round only needs the rows within n-1-i of the core;
+            // a wave whose rows all lie outside it skips the sweep (its rows feed only rows that
+            // are no longer needed, and the hand-off refreshes them before the next round).
+            const int reach = n - 1 - i;
+            const bool skip = (j > 0 && wv * RS + RS - 1 < qc0 - reach) ||
+                              (j < A.nb - 1 && wv * RS >= qc1 + reach);
+            if (!(A.dbg & 4) && !skip) {
+                if (em) S.template sweep<true>(up, dn, em);
+                else S.template sweep<false>(up, dn, em);
+            }
+            if (!(A.dbg & 8)) {
+                put_edges(cb ^ 1);
+                __syncthreads();
+            }
         }
         s += n;
         round++;
@@ -270,6 +289,62 @@ __global__ void __launch_bounds__(64 * NWV) k_jres(JresArgs A)
         int xl = x0;
         asm volatile("" : "+v"(xl));
         const int par = round & 1;
+        const uint32_t want = A.fbase + (uint32_t)round;
+#if PF_JRES_GRANULE
+        // Data-tagged granules (MI355X_MICROARCH.md, handoff-1to1): every float travels as one
+        // 8-B {value, round tag} granule, stored write-through (sc1) with no wait and no flag;
+        // the consumer waves re-read their rows (sc1) until every tag is this round's.  Parity
+        // slots: a block overwrites slot (round & 1) only after taking its neighbours' rows of
+        // the round in between, which they publish after reading this slot.
+        uint32_t* const gb = reinterpret_cast<uint32_t*>(xb);
+        const long long gplane = 2 * xplane;  // uint32 words of one published edge
+        const uint32_t gbytes = (uint32_t)(sizeof(uint32_t) * gplane * 2);
+        const auto mr = rsrc(gb + ((long long)(p * A.nb + j) * 2 + par) * 2 * gplane, gbytes);
+#pragma unroll
+        for (int r = 0; r < RS; r++) {
+            const int Y = rs + wv * RS + r;
+#pragma unroll
+            for (int e = 0; e < 2; e++) {  // a row can be in both published sets when core < 2K
+                const bool pub = e == 0 ? (j > 0 && Y >= c0 && Y < c0 + K)
+                                        : (j < A.nb - 1 && Y >= c1 - K && Y < c1);
+                if (!pub) continue;  // wave-uniform
+                const int yo = e == 0 ? Y - c0 : Y - (c1 - K);
+                const int off = (int)(sizeof(uint32_t) * (e * gplane + 2 * ((long long)yo * w + xl)));
+#pragma unroll
+                for (int k = 0; k < NP; k++) {
+                    const u4v v = {__float_as_uint(S.b[r][k].x), want, __float_as_uint(S.b[r][k].y), want};
+                    __builtin_amdgcn_raw_buffer_store_b128(v, mr, off + 16 * k, 0, kSC1);
+                }
+            }
+        }
+#pragma unroll
+        for (int r = 0; r < RS; r++) {
+            const int Y = rs + wv * RS + r;
+            int src_j = -1, e = 0, yo = 0;
+            if (j > 0 && Y >= c0 - K && Y < c0) { src_j = j - 1; e = 1; yo = Y - (c0 - K); }
+            else if (j < A.nb - 1 && Y >= c1 && Y < re) { src_j = j + 1; e = 0; yo = Y - c1; }
+            if (src_j >= 0) {  // wave-uniform
+                const auto tr = rsrc(gb + ((long long)(p * A.nb + src_j) * 2 + par) * 2 * gplane, gbytes);
+                const int off = (int)(sizeof(uint32_t) * (e * gplane + 2 * ((long long)yo * w + xl)));
+                int spins = 0;
+                while (true) {
+                    bool ok = true;
+#pragma unroll
+                    for (int k = 0; k < NP; k++) {
+                        const u4v v = __builtin_amdgcn_raw_buffer_load_b128(tr, off + 16 * k, 0, kSC1);
+                        S.b[r][k] = f2{__uint_as_float(v[0]), __uint_as_float(v[2])};
+                        ok = ok && v[1] == want && v[3] == want;
+                    }
+                    if (__builtin_amdgcn_ballot_w64(!ok) == 0) break;  // every lane's granules current
+                    __builtin_amdgcn_s_sleep(1);
+                    if (++spins > (1 << 22)) {  // bounded: counted, never hangs
+                        if (lane == 0) __hip_atomic_fetch_add(A.err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                        break;
+                    }
+                }
+            }
+        }
+#else
         float* mine = xb + ((long long)(p * A.nb + j) * 2 + par) * 2 * xplane;
         const auto mr = rsrc(mine, (uint32_t)(sizeof(float) * xplane * 2));
 #pragma unroll
@@ -296,7 +371,6 @@ __global__ void __launch_bounds__(64 * NWV) k_jres(JresArgs A)
         }
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
-        const uint32_t want = A.fbase + (uint32_t)round;
         if (tid == 0) {
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             __hip_atomic_store(&A.flags[p * A.nb + j], want, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -333,6 +407,7 @@ __global__ void __launch_bounds__(64 * NWV) k_jres(JresArgs A)
                 }
             }
         }
+#endif
     }
 
     // ---- the core rows of the finished level
@@ -381,14 +456,16 @@ static void launch_cr(hipStream_t s, const JresArgs& A, int grid, int src_mode, 
     }
 }
 
-// Workgroup shape: PF_JRES_WAVES waves of 64-row regions -- 8 waves of 8 rows (default: two
-// waves per SIMD at <= 256 VGPRs, a third of the CU's register file left to co-resident
-// kernels such as the side-stream target gathers and the pipelined warp) or 16 waves of 4 rows
-// (one workgroup fills the CU's registers).
+// Workgroup shape: PF_JRES_WAVES waves over a 64-row region -- 16 waves of 4 rows (default: one
+// workgroup per CU at <= 128 VGPRs) or 8 waves of 8 rows (two waves per SIMD at <= 256 VGPRs,
+// leaving a sixth of the register file to co-resident kernels).  Measured in the pipelined C3
+// step on MI355X (tools/jres_ab.sh, three alternating rounds): 13.64-13.97k panoramas/s for 16
+// waves, 13.66-13.76k for 8, 12.89-13.02k for the streaming passes.
 #ifndef PF_JRES_WAVES
-#define PF_JRES_WAVES 8
+#define PF_JRES_WAVES 16
 #endif
 static constexpr int kJW = PF_JRES_WAVES;
+int jres_words_per_value() { return PF_JRES_GRANULE ? 2 : 1; }
 static constexpr int kRS512 = 64 / kJW, kRS256 = 128 / kJW;
 
 // region rows of the resident kernel's workgroup at this width (0: not supported)

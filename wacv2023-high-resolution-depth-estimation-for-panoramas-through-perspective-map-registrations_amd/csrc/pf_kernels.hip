@@ -542,7 +542,10 @@ __global__ void __launch_bounds__(kRegLanes) k_register(
     const int* __restrict__ active)
 {
     __shared__ double part[kRegSums][kRegLanes];
-    const int p = blockIdx.x, b = blockIdx.y, l = threadIdx.x;
+    // one linear grid, XCD-contiguous: the tiles of one panorama run on one XCD, so its emap is
+    // fetched into one L2 (the samples of neighbouring tiles overlap in the emap)
+    const unsigned lb = xcd_remap(blockIdx.x, gridDim.x);
+    const int p = (int)(lb % (unsigned)ntiles), b = (int)(lb / (unsigned)ntiles), l = threadIdx.x;
     if (active && !active[p]) return;  // joint solve: an inactive tile is neither read nor solved
     const TileGeom g = geom[p];
     const RegGrid rg = grids[p];
@@ -836,7 +839,7 @@ void launch_register(hipStream_t s, const TileGeom* geom, const RegGrid* grids,
                      long long tstride, int degree, int solver, float* coeffs, double* coeffs64,
                      int batch, double* sums, const int* active)
 {
-    dim3 grid(ntiles, batch);
+    dim3 grid((unsigned)(ntiles * batch));
     hipLaunchKernelGGL(k_register, grid, dim3(kRegLanes), 0, s, geom, grids, rcols, rrows,
                        ntiles, emap, ew, eh, ec, estride, tiles, tstride, degree, solver, coeffs,
                        coeffs64, sums, active);
