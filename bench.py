@@ -134,6 +134,30 @@ def pmc_traffic(family):
         return None
 
 
+def _pmc_record(family):
+    try:
+        with open(os.path.join(ROOT, "profiles", "pmc_traffic.json")) as f:
+            return json.load(f).get(family)
+    except (OSError, ValueError):
+        return None
+
+
+def jacobi_traffic_per_step(launches_per_step):
+    """PMC HBM bytes of one step's Jacobi stage: the streaming passes (k_jlag) plus, where the
+    resident level kernel ran, its one launch per fusion (k_jres).  The PMC run's k_jres dispatch
+    count is its fusion count, which scales k_jlag's total to one step."""
+    rl, rr = _pmc_record("pf::k_jlag"), _pmc_record("pf::k_jres")
+    try:
+        if rr and rl:
+            return (float(rl["traffic_B"]) * float(rl["dispatches"]) / float(rr["dispatches"])
+                    + float(rr["traffic_B"]))
+        if rl:
+            return float(rl["traffic_B"]) * launches_per_step
+    except (KeyError, ValueError, ZeroDivisionError):
+        pass
+    return None
+
+
 def _metrics_traffic():
     """PMC HBM bytes of one pf_error_metrics call (align_way 1): 3 k_med_hist + k_err_sums."""
     h, e = pmc_traffic("pf::k_med_hist"), pmc_traffic("pf::k_err_sums")
@@ -436,7 +460,7 @@ def main():
     jms, jbytes, jlaunch = prof["jacobi"]
     achieved = jbytes / (jms * 1e-3) / 1e9 if jms > 0 else 0.0
     jtf = jbytes / 12.0 * 14.0 / (jms * 1e-3) / 1e12 if jms > 0 else 0.0
-    jtraffic = pmc_traffic("pf::k_jlag")
+    jtraffic = jacobi_traffic_per_step(jlaunch / nprof if nprof else 0)  # B per step
     wms, wbytes, wlaunch = prof["warp"]  # read 4 B/pano pixel + write 4 B/tile pixel (8d)
     wach = wbytes / (wms * 1e-3) / 1e9 if wms > 0 else 0.0
     stages = {k: {"ms_per_step": v[0] / nprof,
@@ -483,31 +507,38 @@ def main():
                        "pipeline": ("warp of batch k+1 on a second stream during the "
                                     "registration + fusion of batch k" if args.pipeline
                                     else "off")},
-            # Headline: the dominant kernel (k_jlag, the temporally blocked Jacobi) against its
-            # real roof, VALU issue: algorithmic FLOP = 14 fp32 operations per pixel-update as the
-            # reference writes them (Depth.cpp:1680-1717: 4 mul + 4 add for Lcur; sub, mul, add;
-            # 2 mul, add for b'), per average launch, over the hipEvent launch time, against the
-            # vector FP32 peak (MI355X_MICROARCH.md).  `traffic` is the HBM bytes per launch
-            # measured by the rocprofv3 PMC passes (profiles/pmc_traffic.json).
+            # Headline: the dominant stage -- the Jacobi sweeps of one step, i.e. the resident
+            # level-0 kernel (k_jres, all 200 sweeps in one launch) and the temporally blocked
+            # passes of the finer levels (k_jlag) -- against its real roof, VALU issue:
+            # algorithmic FLOP = 14 fp32 operations per pixel-update as the reference writes them
+            # (Depth.cpp:1680-1717: 4 mul + 4 add for Lcur; sub, mul, add; 2 mul, add for b'),
+            # per step, over the stage's hipEvent time, against the vector FP32 peak
+            # (MI355X_MICROARCH.md).  `traffic` is the stage's HBM bytes per step measured by the
+            # rocprofv3 PMC passes (profiles/pmc_traffic.json).
             "roofline": {"bound": "valu", "achieved": jtf, "peak": VALU_PEAK_TF,
                          "unit": "TFLOP/s", "frac": jtf / VALU_PEAK_TF,
-                         "traffic": pmc_traffic("pf::k_jlag"),
-                         "kernel": "k_jlag (all Jacobi passes of the levels, aggregated)",
+                         "traffic": jtraffic,
+                         "traffic_unit": "B per step (all Jacobi launches of the step)",
+                         "kernel": "Jacobi stage: k_jres (level 0, resident) + k_jlag passes "
+                                   "(levels 1-2), aggregated per step",
                          "flop_per_update": 14,
-                         "avg_launch_us": (jms / jlaunch * 1e3) if jlaunch else None,
-                         "flop_per_launch": (jbytes / 12.0 * 14.0 / jlaunch) if jlaunch else None,
+                         "launches_per_step": (jlaunch / nprof) if nprof else None,
+                         "ms_per_step": jms / nprof if nprof else None,
+                         "flop_per_step": jbytes / 12.0 * 14.0 / nprof if nprof else None,
                          "updates_per_step": jbytes / 12.0 / nprof,
-                         "traffic_source": "profiles/pmc_traffic.json (FETCH_SIZE + WRITE_SIZE, "
-                                           "B per launch, averaged over every k_jlag dispatch)"},
-            # the same kernel on the HBM roof with its MEASURED traffic (temporal blocking moves
-            # T sweeps per pass through HBM once), and the 12 B/update algorithmic rate of
-            # SURVEY.md 8d as an "effective" bandwidth (> peak by construction: not a fraction)
+                         "traffic_source": "profiles/pmc_traffic.json (FETCH_SIZE + WRITE_SIZE "
+                                           "per launch of k_jlag and k_jres, scaled to one step)"},
+            # the same stage on the HBM roof with its MEASURED traffic (temporal blocking moves
+            # T sweeps per pass through HBM once; the resident kernel reads the level once), and
+            # the 12 B/update algorithmic rate of SURVEY.md 8d as an "effective" bandwidth (>
+            # peak by construction: not a fraction)
             "roofline_hbm": {"bound": "hbm", "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                             "achieved": (jtraffic / (jms / jlaunch * 1e-3) / 1e9)
-                             if (jtraffic and jlaunch) else None,
-                             "frac": (jtraffic / (jms / jlaunch * 1e-3) / 1e9 / HBM_PEAK_GBS)
-                             if (jtraffic and jlaunch) else None,
-                             "kernel": "k_jlag", "basis": "measured PMC bytes per launch"},
+                             "achieved": (jtraffic / (jms / nprof * 1e-3) / 1e9)
+                             if (jtraffic and nprof and jms > 0) else None,
+                             "frac": (jtraffic / (jms / nprof * 1e-3) / 1e9 / HBM_PEAK_GBS)
+                             if (jtraffic and nprof and jms > 0) else None,
+                             "kernel": "Jacobi stage (k_jres + k_jlag)",
+                             "basis": "measured PMC bytes per step"},
             "effective_hbm": {"achieved": achieved, "unit": "GB/s",
                               "basis": "12 B per pixel-update (SURVEY.md 8d) / Jacobi time; "
                                        "temporal blocking keeps T-1 of every T sweeps on chip"},
