@@ -1,5 +1,6 @@
 """Per-level Jacobi time from a rocprofv3 kernel trace (tools/ktrace_levels.py run_kernel_trace.csv):
-groups k_jlag / k_jpipe dispatches of the last bench step by grid width and sums their durations."""
+groups k_jres / k_jlag / k_jpipe dispatches of the last bench step by kernel and grid width and
+sums their durations."""
 import collections
 import csv
 import sys
@@ -11,7 +12,7 @@ step = rows[warps[-2]:warps[-1]] if len(warps) > 1 else rows
 acc = collections.OrderedDict()
 for r in step:
     n = r["Kernel_Name"]
-    if "k_jlag" not in n and "k_jpipe" not in n:
+    if "k_jlag" not in n and "k_jpipe" not in n and "k_jres" not in n:
         continue
     key = (n.split("(")[0].replace("void pf::", "")[:34], r["Grid_Size_X"])
     d = (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1000.0
