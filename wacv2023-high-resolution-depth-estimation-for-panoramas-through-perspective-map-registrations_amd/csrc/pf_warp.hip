@@ -48,6 +48,12 @@ static constexpr int kNB = PF_WARP_BATCH;               // panoramas per block
 #ifndef PF_WARP_V4
 #define PF_WARP_V4 0     // quad-aligned footprint boxes staged with 16-B loads (pw % 4 == 0)
 #endif
+#ifndef PF_WARP_SPLIT
+// the two staging parities in separate LDS halves (consecutive lanes read/write consecutive
+// dwords: conflict-free) instead of interleaved (stride-2 dwords: 2-way bank conflicts, 64% of
+// the kernel's LDS-active cycles on MI355X, tools/warp_sq.sh)
+#define PF_WARP_SPLIT 1
+#endif
 #ifndef PF_WARP_ROWPX
 #define PF_WARP_ROWPX 0  // a thread's pixels consecutive in one row: one 16-B store per panorama
 #endif
@@ -338,12 +344,15 @@ __device__ __forceinline__ void warp_staged(float* box, const RespK* rk, const W
 #pragma unroll
         for (int s = 0; s < NS; s++)
 #pragma unroll
-            for (int j = 0; j < U; j++) box[2 * ((t + s * kWB) * U + j) + pa] = src[s][j];
+            for (int j = 0; j < U; j++) {
+                if constexpr (PF_WARP_SPLIT) box[pa * kCap + (t + s * kWB) * U + j] = src[s][j];
+                else box[2 * ((t + s * kWB) * U + j) + pa] = src[s][j];
+            }
     };
     auto iter = [&](auto parity, int q) {
         constexpr int PA = decltype(parity)::value;
         fetch(stg[PA], q + 2);  // panorama q was put into parity PA last iteration: reuse stg[PA]
-        const float* L = box + PA;
+        const float* L = PF_WARP_SPLIT ? box + PA * kCap : box + PA;
         const int b = bbeg + q;
         const auto orr = rsrc(tiles + b * tstride, (uint32_t)(tstride * 4));
         f2 al{}, ka{}, be{}, si{};
@@ -361,8 +370,12 @@ __device__ __forceinline__ void warp_staged(float* box, const RespK* rk, const W
 #pragma unroll
             for (int j = 0; j < 2; j++) {
                 const float* c = L + W.la[k + j];
-                v[j] = bilinear(f2{c[0], c[2]}, f2{c[bw2], c[bw2 + 2]}, W.wx[k + j],
-                                W.wy[k + j]);
+                if constexpr (PF_WARP_SPLIT)
+                    v[j] = bilinear(f2{c[0], c[1]}, f2{c[P.bw], c[P.bw + 1]}, W.wx[k + j],
+                                    W.wy[k + j]);
+                else
+                    v[j] = bilinear(f2{c[0], c[2]}, f2{c[bw2], c[bw2 + 2]}, W.wx[k + j],
+                                    W.wy[k + j]);
             }
             if (RESP) {
                 const f2 u = f2{noise_top24(W.hp[k], key), noise_top24(W.hp[k + 1], key)};
@@ -480,7 +493,7 @@ __global__ void __launch_bounds__(kWB) k_warp_depth(const TileGeom* __restrict__
 
     W.full = PF_WARP_ROWPX && W.ok[0] && W.ok[kPx - 1] && g.c == 1;
 #pragma unroll
-    for (int k = 0; k < kPx; k++) W.la[k] *= 2;  // parity-interleaved box
+    for (int k = 0; k < kPx; k++) W.la[k] *= PF_WARP_SPLIT ? 1 : 2;  // parity-interleaved box
     __shared__ RespK rk[kNB];  // published by the first barrier inside warp_staged
     if (t < nb) rk[t] = resp_key(resp, bbeg + t, ntiles, P.tile);
     const bool rs = resp != nullptr;
