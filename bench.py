@@ -277,6 +277,14 @@ def rank_seeds(batch, rank):
     return pf_dist.panorama_block(batch, rank)
 
 
+# pipelined steps: the next batch's warp waits for this level of the current fusion (-1: only for
+# the fusion that last read its buffer).  Level 0 (default): the memory-bound warp runs beside
+# the finer levels' streaming passes instead of contending with the resident level-0 kernel,
+# which fills every CU -- measured on MI355X (tools/warp_after_ab.sh, three alternating rounds):
+# 14.12-14.28k panoramas/s against 13.51-14.02k (-1) and 13.94-14.32k (1).
+WARP_AFTER_LEVEL = int(os.environ.get("PF_WARP_AFTER", "0"))
+
+
 def pipelined_step(fz, lay, local, dev, gt, emap, resp, tiles, out, coeffs, zr):
     """The software-pipelined bench step: step k registers and fuses the tiles warped during step
     k-1 (buffer k % 2) on the main stream while a second stream (its own context) warps batch k+1
@@ -305,6 +313,8 @@ def pipelined_step(fz, lay, local, dev, gt, emap, resp, tiles, out, coeffs, zr):
         fused.record(main)
         if st["fused"] is not None:
             sw.wait_event(st["fused"])  # the fusion of step k-1 read nxt
+        if WARP_AFTER_LEVEL >= 0:  # start the warp beside the finer levels of this fusion
+            fz.stream_wait_level(WARP_AFTER_LEVEL, sw)
         fw.warp_depth(gt, nxt, resp)
         warped = torch.cuda.Event()
         warped.record(sw)
@@ -504,9 +514,13 @@ def main():
                                    f"20 tiles of 512x512 (5x4 layout), 512x256 baseline",
                        "global_batch": B * world, "out": "2048x1024", "tiles": "20x512x512",
                        "parallelism": f"dp{world} (panorama sharding, no collective)",
-                       "pipeline": ("warp of batch k+1 on a second stream during the "
-                                    "registration + fusion of batch k" if args.pipeline
-                                    else "off")},
+                       "pipeline": ("warp of batch k+1 on a second stream beside the fusion "
+                                    "of batch k, from the end of its level-0 sweeps"
+                                    if args.pipeline else "off"),
+                       "layout_caches": "tap maps, warp corner tables and level tables are "
+                                        "built once per layout and panorama size, outside the "
+                                        "timed steps (every step re-warps, re-registers and "
+                                        "re-fuses the whole batch)"},
             # Headline: the dominant stage -- the Jacobi sweeps of one step, i.e. the resident
             # level-0 kernel (k_jres, all 200 sweeps in one launch) and the temporally blocked
             # passes of the finer levels (k_jlag) -- against its real roof, VALU issue:

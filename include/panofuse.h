@@ -192,6 +192,13 @@ int pf_fuse_band_pass(pf_ctx* ctx, const float* emap, int ew, int eh, int ec, co
 int pf_profile_enable(pf_ctx* ctx, int on);
 int pf_profile_read(pf_ctx* ctx, double* ms, double* bytes, long long* launches);
 
+/* ---- cross-stream ordering (no reference counterpart) ----
+ * Makes `hip_stream` (another stream on the same device) wait until level `level` of the
+ * context's most recently enqueued fusion (pf_fuse / pf_merge) has finished its sweeps, e.g. to
+ * start memory-bound work beside the finer levels instead of beside the coarse one.  Returns
+ * PF_EINVAL if no fusion with that many levels was enqueued on this context. */
+int pf_stream_wait_level(pf_ctx* ctx, int level, void* hip_stream);
+
 /* ---- Jacobi engine selection (no reference counterpart; every engine is bit-identical) ----
  * mode 1 (default; the environment variable PF_JRES=0 changes the default to 0): levels of
  * width 256 or 512 with the separable-coverage certificate run all their sweeps in one resident

@@ -100,6 +100,9 @@ struct pf_ctx {
     // side stream for the finer levels' target planes (fuse_range), created on first use
     hipStream_t aux = nullptr;
     hipEvent_t ev_fork = nullptr, ev_tgt[4] = {};
+    // end of each level's sweeps in the last fusion (pf_stream_wait_level), created on first use
+    hipEvent_t ev_level[4] = {};
+    int nlev_recorded = 0;
 };
 
 namespace {
@@ -324,10 +327,19 @@ void pf_destroy(pf_ctx* c)
         (void)hipEventDestroy(c->ev_fork);
         for (hipEvent_t e : c->ev_tgt) (void)hipEventDestroy(e);
     }
+    for (hipEvent_t e : c->ev_level)
+        if (e) (void)hipEventDestroy(e);
     delete c;
 }
 
 const char* pf_last_error(const pf_ctx* c) { return c ? c->err.c_str() : "null context"; }
+
+int pf_stream_wait_level(pf_ctx* c, int level, void* hip_stream)
+{
+    if (!c || level < 0 || level >= c->nlev_recorded || !c->ev_level[level]) return PF_EINVAL;
+    HIPCHK(c, hipStreamWaitEvent((hipStream_t)hip_stream, c->ev_level[level], 0));
+    return PF_OK;
+}
 
 int pf_set_jacobi_engine(pf_ctx* c, int mode, int row_blocks)
 {
@@ -948,7 +960,7 @@ static int jres_prepare(pf_ctx* c, const LevelDims& L, int batch, const JresPlan
     const size_t xb = sizeof(float) * jres_words_per_value() * (size_t)batch * jp.nb * 4 *
                       (size_t)jp.K * L.w;
     if ((rc = ensure(c, c->jres_x, xb))) return rc;
-    const size_t sb = sizeof(uint32_t) * (2 + (size_t)batch * jp.nb);
+    const size_t sb = sizeof(uint32_t) * (2 + (size_t)batch * jp.nb * jres_flags_per_block(jp.K));
     if (c->jres_sync.bytes < sb) {
         if ((rc = ensure(c, c->jres_sync, sb))) return rc;
         HIPCHK(c, hipMemsetAsync(c->jres_sync.p, 0, sb, c->stream));
@@ -1237,7 +1249,10 @@ static int fuse_range(pf_ctx* c, const float* emap, int ew, int eh, int ec, cons
             if (!res) return fail(c, PF_EINVAL, "level-0 seed tables missing");
         }
         prev = res;
+        if (!c->ev_level[l]) HIPCHK(c, hipEventCreateWithFlags(&c->ev_level[l], hipEventDisableTiming));
+        HIPCHK(c, hipEventRecord(c->ev_level[l], c->stream));
     }
+    c->nlev_recorded = lc.nlevels;
     HIPCHK(c, hipGetLastError());
     return PF_OK;
 }

@@ -185,7 +185,8 @@ struct JresArgs {
 };
 int jres_region_rows(int w);
 int jres_threads();
-int jres_words_per_value();  // 2: the hand-off rows travel as {value, tag} granules
+int jres_words_per_value();
+int jres_flags_per_block(int K);  // 2: the hand-off rows travel as {value, tag} granules
 int jres_blocks_per_cu(int w);
 void launch_jres(hipStream_t s, const JresArgs& A);
 

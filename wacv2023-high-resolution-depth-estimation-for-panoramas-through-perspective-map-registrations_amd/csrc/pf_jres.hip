@@ -69,6 +69,9 @@ __device__ __forceinline__ float fma_scalar(float a, float b, float c)
     return r;
 }
 
+#ifndef PF_JRES_LDSFLAG
+#define PF_JRES_LDSFLAG 0  // barrier-free sweeps + per-row hand-off flags (measured: same time as barriers)
+#endif
 #ifndef PF_JRES_GRANULE
 #define PF_JRES_GRANULE 0  // hand-off by data-tagged granules (measured 2x slower: 32-KB edges)
 #endif
@@ -254,6 +257,155 @@ __global__ void __launch_bounds__(64 * NWV) k_jres(JresArgs A)
 
     const long long xplane = (long long)K * w;  // floats of one published edge
     float* const xb = A.xbuf;
+#if PF_JRES_LDSFLAG
+    // Barrier-free sweeps: wave w starts sweep s+1 once its neighbour waves have published their
+    // edge rows of state s (an LDS flag per wave), so a wave runs at most one sweep ahead of its
+    // neighbours and, while the halo waves wait for a hand-off, the waves further in keep
+    // sweeping (a wave d waves from the halo can run d sweeps ahead).  Edge rows of state s sit in
+    // buffer s & 1: wave w overwrites buffer s & 1 only after its neighbours published state s+1,
+    // i.e. after they read state s-1 from it.  The hand-off is per row: each published row
+    // carries its own flag (one sc1 store after the storing wave's vmcnt(0)); a halo wave polls
+    // the flags of its own rows only.  No workgroup barrier after the start.
+    __shared__ int eflag[NW];
+    auto publish_edges = [&](int st) {
+        put_edges(st & 1);
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        if (lane == 0) *reinterpret_cast<volatile int*>(&eflag[wv]) = st;
+    };
+    auto wait_edges = [&](int nbw, int st) {
+        int spins = 0;
+        while (*reinterpret_cast<volatile int*>(&eflag[nbw]) < st) {
+            __builtin_amdgcn_s_sleep(0);
+            if (++spins > (1 << 26)) {
+                if (lane == 0) __hip_atomic_fetch_add(A.err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                break;
+            }
+        }
+        asm volatile("" ::: "memory");  // the edge reads below stay after the flag read
+    };
+    // halo rows of this wave (refreshed from the neighbour blocks after every round), as bits
+    uint32_t halo = 0;
+#pragma unroll
+    for (int r = 0; r < RS; r++) {
+        const int Y = rs + wv * RS + r;
+        if ((j > 0 && Y >= c0 - K && Y < c0) || (j < A.nb - 1 && Y >= c1 && Y < re)) halo |= 1u << r;
+    }
+    halo = __builtin_amdgcn_readfirstlane(halo);
+    uint32_t* const gflag = A.flags;  // [batch][nb][2 edge][K] per published row
+    publish_edges(0);
+    __syncthreads();  // every wave's state-0 edges and flag in place
+    int s = 0, round = 0;
+    while (true) {
+        const int n = min(K, A.iters - s);
+        for (int i = 0; i < n; i++) {
+            if (wv > 0) wait_edges(wv - 1, s);
+            if (wv < NW - 1) wait_edges(wv + 1, s);
+            const int cb = s & 1;
+            const f2* up = wv > 0 ? &lds_edge[cb][1][wv > 0 ? wv - 1 : 0][0][lane] : nullptr;
+            const f2* dn = wv < NW - 1 ? &lds_edge[cb][0][wv < NW - 1 ? wv + 1 : 0][0][lane] : nullptr;
+            const int reach = n - 1 - i;
+            const bool skip = (j > 0 && wv * RS + RS - 1 < qc0 - reach) ||
+                              (j < A.nb - 1 && wv * RS >= qc1 + reach);
+            if (!(A.dbg & 4) && !skip) {
+                if (em) S.template sweep<true>(up, dn, em);
+                else S.template sweep<false>(up, dn, em);
+            }
+            s++;
+            // a halo wave publishes its end-of-round edges after the hand-off refreshed its rows
+            if (!(i == n - 1 && halo && s < A.iters)) publish_edges(s);
+        }
+        round++;
+        if (s >= A.iters) break;
+        if (A.dbg & 1) {
+            if (halo) publish_edges(s);
+            continue;
+        }
+        int xl = x0;
+        asm volatile("" : "+v"(xl));
+        const int par = round & 1;
+        const uint32_t want = A.fbase + (uint32_t)round;
+        // publish: this wave's core rows that a neighbour block needs (sc1 stores, drained, then
+        // one sc1 flag per row)
+        {
+            float* mine = xb + ((long long)(p * A.nb + j) * 2 + par) * 2 * xplane;
+            const auto mr = rsrc(mine, (uint32_t)(sizeof(float) * xplane * 2));
+            uint32_t pubm = 0;  // bit 2r+e: row r published in edge set e
+#pragma unroll
+            for (int r = 0; r < RS; r++) {
+                const int Y = rs + wv * RS + r;
+#pragma unroll
+                for (int e = 0; e < 2; e++) {
+                    const bool pub = e == 0 ? (j > 0 && Y >= c0 && Y < c0 + K)
+                                            : (j < A.nb - 1 && Y >= c1 - K && Y < c1);
+                    if (!pub) continue;  // wave-uniform
+                    pubm |= 1u << (2 * r + e);
+                    const int yo = e == 0 ? Y - c0 : Y - (c1 - K);
+                    const int off = (int)(sizeof(float) * (e * xplane + (long long)yo * w + xl));
+#pragma unroll
+                    for (int k = 0; k < NP; k += 2) {
+                        u4v v;
+                        v[0] = __float_as_uint(S.b[r][k].x);
+                        v[1] = __float_as_uint(S.b[r][k].y);
+                        v[2] = __float_as_uint(S.b[r][k + 1].x);
+                        v[3] = __float_as_uint(S.b[r][k + 1].y);
+                        __builtin_amdgcn_raw_buffer_store_b128(v, mr, off + 8 * k, 0, kSC1);
+                    }
+                }
+            }
+            if (pubm) {
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                // lane 2r+e flags row r of edge set e
+                if (lane < 2 * RS && ((pubm >> lane) & 1u)) {
+                    const int r = lane >> 1, e = lane & 1;
+                    const int Y = rs + wv * RS + r;
+                    const int yo = e == 0 ? Y - c0 : Y - (c1 - K);
+                    __hip_atomic_store(&gflag[((long long)(p * A.nb + j) * 2 + e) * K + yo], want,
+                                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                }
+            }
+        }
+        if (halo) {
+            // poll the flags of this wave's halo rows (lane r: row r), then load them
+            int spins = 0;
+            while (true) {
+                bool ok = true;
+                if (lane < RS && ((halo >> lane) & 1u)) {
+                    const int Y = rs + wv * RS + lane;
+                    const bool top = j > 0 && Y < c0;
+                    const int sj = top ? j - 1 : j + 1, e = top ? 1 : 0;
+                    const int yo = top ? Y - (c0 - K) : Y - c1;
+                    const uint32_t f = __hip_atomic_load(&gflag[((long long)(p * A.nb + sj) * 2 + e) * K + yo],
+                                                         __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    ok = (int)(f - want) >= 0;
+                }
+                if (__builtin_amdgcn_ballot_w64(!ok) == 0) break;
+                __builtin_amdgcn_s_sleep(1);
+                if (++spins > (1 << 24)) {
+                    if (lane == 0) __hip_atomic_fetch_add(A.err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    break;
+                }
+            }
+#pragma unroll
+            for (int r = 0; r < RS; r++) {
+                if (!((halo >> r) & 1u)) continue;  // wave-uniform
+                const int Y = rs + wv * RS + r;
+                const bool top = j > 0 && Y < c0;
+                const int sj = top ? j - 1 : j + 1, e = top ? 1 : 0;
+                const int yo = top ? Y - (c0 - K) : Y - c1;
+                const float* theirs = xb + ((long long)(p * A.nb + sj) * 2 + par) * 2 * xplane;
+                const auto tr = rsrc(theirs, (uint32_t)(sizeof(float) * xplane * 2));
+                const int off = (int)(sizeof(float) * (e * xplane + (long long)yo * w + xl));
+#pragma unroll
+                for (int k = 0; k < NP; k += 2) {
+                    const u4v v = __builtin_amdgcn_raw_buffer_load_b128(tr, off + 8 * k, 0, kSC1);
+                    S.b[r][k] = f2{__uint_as_float(v[0]), __uint_as_float(v[1])};
+                    S.b[r][k + 1] = f2{__uint_as_float(v[2]), __uint_as_float(v[3])};
+                }
+            }
+            publish_edges(s);
+        }
+    }
+#else
     int s = 0, round = 0;
     while (true) {
         const int n = min(K, A.iters - s);
@@ -410,6 +562,8 @@ __global__ void __launch_bounds__(64 * NWV) k_jres(JresArgs A)
 #endif
     }
 
+#endif
+
     // ---- the core rows of the finished level
 #pragma unroll
     for (int r = 0; r < RS; r++) {
@@ -466,6 +620,8 @@ static void launch_cr(hipStream_t s, const JresArgs& A, int grid, int src_mode, 
 #endif
 static constexpr int kJW = PF_JRES_WAVES;
 int jres_words_per_value() { return PF_JRES_GRANULE ? 2 : 1; }
+// hand-off flag words per row block: one per published row (LDS-flag form) or one per block
+int jres_flags_per_block(int K) { return PF_JRES_LDSFLAG ? 2 * K : 1; }
 static constexpr int kRS512 = 64 / kJW, kRS256 = 128 / kJW;
 
 // region rows of the resident kernel's workgroup at this width (0: not supported)

@@ -27,7 +27,7 @@ EXPORTS = [
     "pf_depth_transform", "pf_register_joint", "pf_set_solver", "pf_fuse_normalize",
     "pf_fuse_border", "pf_fuse_band_plan", "pf_fuse_band_pass", "pf_fuse_multicover",
     "pf_fuse_multicover_patch", "pf_solve_smoothing", "pf_set_metrics_order",
-    "pf_jres_errors", "pf_set_jacobi_engine",
+    "pf_jres_errors", "pf_set_jacobi_engine", "pf_stream_wait_level",
 ]
 METRICS_ORDERS = {"tree": 0, "sequential": 1}  # PF_METRICS_*; "sequential" = the reference's
 SOLVERS = {"normal": 0, "lm": 1}  # PF_SOLVER_*; "lm" = the reference's Ceres LM (default)
@@ -102,6 +102,7 @@ def load():
     L.pf_profile_enable.argtypes = [vp, ip]
     L.pf_jres_errors.argtypes = [vp]
     L.pf_set_jacobi_engine.argtypes = [vp, ip, ip]
+    L.pf_stream_wait_level.argtypes = [vp, ip, vp]
     L.pf_profile_read.argtypes = [vp, C.POINTER(C.c_double), C.POINTER(C.c_double),
                                   C.POINTER(C.c_longlong)]
     for name in EXPORTS:
@@ -367,6 +368,10 @@ class Fuser:
 
     def synchronize(self):
         self._check(self.L.pf_synchronize(self.h))
+
+    def stream_wait_level(self, level, stream):
+        """Make torch `stream` wait for level `level` of this context's last enqueued fusion."""
+        self._check(self.L.pf_stream_wait_level(self.h, int(level), C.c_void_p(stream.cuda_stream)))
 
     def set_jacobi_engine(self, resident=True, row_blocks=0):
         """Jacobi engine of the fusion levels: the resident one-launch kernel where it applies
