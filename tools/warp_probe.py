@@ -43,6 +43,10 @@ def main():
     tiles = torch.empty((B, fz.tile_elems), dtype=torch.float32, device=dev)
     res = {}
     res["warp_ms"] = timed(lambda: fz.warp_depth(gt, tiles, resp))
+    import hashlib
+    fz.warp_depth(gt, tiles, resp)
+    torch.cuda.synchronize()
+    res["sha"] = hashlib.sha256(tiles.cpu().numpy().tobytes()).hexdigest()[:16]
     res["warp_noresp_ms"] = timed(lambda: fz.warp_depth(gt, tiles))
     res["fill_tiles_ms"] = timed(lambda: tiles.fill_(0.5))
     src = torch.empty_like(tiles)

@@ -29,30 +29,53 @@
 
 namespace pf {
 
-static constexpr int kWB = 256;                         // threads per block
-static constexpr int kPatch = 32;                       // patch edge in tile pixels
+#ifndef PF_WARP_WB
+#define PF_WARP_WB 256
+#endif
+#ifndef PF_WARP_PATCH
+#define PF_WARP_PATCH 32
+#endif
+static constexpr int kWB = PF_WARP_WB;                  // threads per block
+static constexpr int kPatch = PF_WARP_PATCH;            // patch edge in tile pixels
+static_assert(kWB % kPatch == 0 && kPatch * kPatch % kWB == 0, "whole patch rows per slot");
 static constexpr int kPx = kPatch * kPatch / kWB;       // pixels per thread
 #ifndef PF_WARP_CAP
 #define PF_WARP_CAP 4096
 #endif
 static constexpr int kCap = PF_WARP_CAP;                // LDS floats per staged footprint
 static constexpr int kSlots = kCap / kWB;               // staging loads per thread
+static_assert(kCap % (4 * kWB) == 0, "whole 16-B staging slots (the V4 path) fill the box");
 #ifndef PF_WARP_BATCH
 #define PF_WARP_BATCH 16
 #endif
 static constexpr int kNB = PF_WARP_BATCH;               // panoramas per block
-// Wider memory operations, measured on MI355X at C3 (tools/warp_probe.py, round 2) and not kept:
-// 16-B staging loads of quad-aligned boxes 0.596 ms, a thread's pixels in one row with 16-B
-// stores 0.600 ms, both 0.637 ms, against 0.586 ms for 4-B loads and stores -- the kernel is not
-// bound by its memory instruction count.
+// Memory operation widths and cache policy, measured on MI355X at C3 (tools/warp_probe.py,
+// tools/r3_warp2.sh).  Round 2: 16-B staging loads 0.596 ms, 16-B row stores 0.600, both 0.637,
+// against 0.586 for 4-B loads and stores.  Round 3, with the split LDS parities: nt tile stores
+// 0.545-0.551 ms against 0.560-0.569 (written tiles no longer evict the staged boxes' lines from
+// L2), and 16-B staging loads on top 0.527-0.531 (kept: the defaults below); 16-B stores through
+// a wave-local LDS transpose 0.573-0.578, 16-B row stores 0.576-0.586 (not kept); 64x64 patches
+// 0.75-1.4 ms (more footprints exceed the LDS box); 5 blocks per CU (3840-float box, 96 VGPRs)
+// 0.539-0.541 without the 16-B loads.
 #ifndef PF_WARP_V4
-#define PF_WARP_V4 0     // quad-aligned footprint boxes staged with 16-B loads (pw % 4 == 0)
+#define PF_WARP_V4 1     // quad-aligned footprint boxes staged with 16-B loads (pw % 4 == 0)
 #endif
 #ifndef PF_WARP_SPLIT
 // the two staging parities in separate LDS halves (consecutive lanes read/write consecutive
 // dwords: conflict-free) instead of interleaved (stride-2 dwords: 2-way bank conflicts, 64% of
 // the kernel's LDS-active cycles on MI355X, tools/warp_sq.sh)
 #define PF_WARP_SPLIT 1
+#endif
+#ifndef PF_WARP_STPOL
+#define PF_WARP_STPOL 2  // cache policy bits of the tile stores (gfx950: 2 = nt, 16 = sc1)
+#endif
+#ifndef PF_WARP_DIAG
+#define PF_WARP_DIAG 0   // probes only: 1 = no tile stores, 2 = no panorama loads (wrong output)
+#endif
+#ifndef PF_WARP_XPOSE
+// results pass through a wave-local LDS transpose so every lane stores its 4 pixels of one tile
+// row with one 16-B store (the compute keeps the 32-lanes-per-row mapping the box reads want)
+#define PF_WARP_XPOSE 0  // measured slower on MI355X (0.573-0.578 ms vs 0.527-0.528 at C3)
 #endif
 #ifndef PF_WARP_ROWPX
 #define PF_WARP_ROWPX 0  // a thread's pixels consecutive in one row: one 16-B store per panorama
@@ -132,10 +155,10 @@ __device__ __forceinline__ int patch_pixel(const WarpPatch& P, const TileGeom& g
                                            int& i)
 {  // thread t, slot k -> tile pixel index i; returns 0 outside the tile.  A thread owns kPx
    // consecutive pixels of one patch row (one 16-B store per panorama), a wave 8 whole rows.
-    static_assert(kPx == 4 && kPatch == 32, "4 pixels per thread, 8 threads per patch row");
 #if PF_WARP_ROWPX
+    static_assert(kPx == 4 && kPatch == 32, "4 pixels per thread, 8 threads per patch row");
     const int X = P.X0 + 4 * (t & 7) + k, Y = P.Y0 + (t >> 3);
-#else  // a wave covers 2 rows per slot, slots 8 rows apart
+#else  // a block covers kWB/kPatch whole rows per slot
     const int X = P.X0 + (t & (kPatch - 1)), Y = P.Y0 + t / kPatch + k * (kWB / kPatch);
 #endif
     i = Y * g.w + X;
@@ -292,6 +315,9 @@ struct WarpLanes {  // one thread's kPx pixels, all panorama-invariant
     f2 wx[kPx], wy[kPx];  // (1-fx, fx), (1-fy, fy)
     bool ok[kPx];
     bool full;  // the kPx pixels are inside the tile and contiguous (one channel): 16-B store
+    // XPOSE: oo[] are the byte offsets of the lane's 4 pixels AFTER the transpose (row
+    // 2*wave + (l>>3 & 1) + 8*(l>>4), columns 4*(l&7)..+3 of the patch); full = all inside,
+    // one channel, 16-B aligned
 };
 
 // LDS-staged interpolation of kNB panoramas for a box of at most NS*256 staging units (floats,
@@ -305,7 +331,8 @@ struct WarpLanes {  // one thread's kPx pixels, all panorama-invariant
 // are consecutive in one tile row: one 16-B store per panorama when they are all inside.
 typedef uint32_t u4v __attribute__((ext_vector_type(4)));
 template <int NS, bool RESP, bool V4>
-__device__ __forceinline__ void warp_staged(float* box, const RespK* rk, const WarpPatch& P,
+__device__ __forceinline__ void warp_staged(float* box, float* xbuf, const RespK* rk,
+                                            const WarpPatch& P,
                                             int t, const WarpLanes& W,
                                             const float* __restrict__ pano, int pw, int ph,
                                             long long pstride, float* __restrict__ tiles,
@@ -331,7 +358,9 @@ __device__ __forceinline__ void warp_staged(float* box, const RespK* rk, const W
         const auto pr = rsrc(pano + (long long)(bbeg + (q < nb ? q : nb - 1)) * pstride, pbytes);
 #pragma unroll
         for (int s = 0; s < NS; s++) {
-            if constexpr (V4) {
+            if constexpr (PF_WARP_DIAG == 2) {
+                for (int j = 0; j < U; j++) dst[s][j] = (float)(goff[s] & 1023u) * 1e-3f;
+            } else if constexpr (V4) {
                 const u4v v = __builtin_amdgcn_raw_buffer_load_b128(pr, (int)goff[s], 0, 0);
 #pragma unroll
                 for (int j = 0; j < 4; j++) dst[s][j] = __uint_as_float(v[j]);
@@ -389,15 +418,25 @@ __device__ __forceinline__ void warp_staged(float* box, const RespK* rk, const W
             out[k] = v[0];
             out[k + 1] = v[1];
         }
-        if (W.full) {
+        if constexpr (PF_WARP_XPOSE) {  // wave-local transpose through LDS (in order per wave)
+            float* xt = xbuf + (t >> 6) * (kPx * 64);
+#pragma unroll
+            for (int k = 0; k < kPx; k++) xt[k * 64 + (t & 63)] = out[k];
+            __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+            const float4 r = *reinterpret_cast<const float4*>(xt + 4 * (t & 63));
+            __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+            out[0] = r.x; out[1] = r.y; out[2] = r.z; out[3] = r.w;
+        }
+        if (PF_WARP_DIAG == 1 && out[0] != -12345.0f) {
+        } else if (kPx >= 4 && W.full) {
             const u4v o = {__float_as_uint(out[0]), __float_as_uint(out[1]),
-                           __float_as_uint(out[2]), __float_as_uint(out[3])};
-            __builtin_amdgcn_raw_buffer_store_b128(o, orr, (int)W.oo[0], 0, 0);
+                           __float_as_uint(out[2 % kPx]), __float_as_uint(out[3 % kPx])};
+            __builtin_amdgcn_raw_buffer_store_b128(o, orr, (int)W.oo[0], 0, PF_WARP_STPOL);
         } else {
 #pragma unroll
             for (int k = 0; k < kPx; k++)
                 __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(out[k]), orr, (int)W.oo[k],
-                                                      0, 0);
+                                                      0, PF_WARP_STPOL);
         }
         put(1 - PA, stg[1 - PA]);  // panorama q+1 (a duplicate past the chunk: unread)
         __syncthreads();
@@ -413,19 +452,24 @@ __device__ __forceinline__ void warp_staged(float* box, const RespK* rk, const W
 }
 
 template <int NS, bool V4>
-__device__ __forceinline__ void warp_staged_sel(bool resp, float* box, const RespK* rk,
+__device__ __forceinline__ void warp_staged_sel(bool resp, float* box, float* xbuf,
+                                                const RespK* rk,
                                                 const WarpPatch& P, int t, const WarpLanes& W,
                                                 const float* pano, int pw, int ph,
                                                 long long pstride, float* tiles,
                                                 long long tstride, int bbeg, int nb)
 {
-    if (resp) warp_staged<NS, true, V4>(box, rk, P, t, W, pano, pw, ph, pstride, tiles, tstride,
+    if (resp) warp_staged<NS, true, V4>(box, xbuf, rk, P, t, W, pano, pw, ph, pstride, tiles, tstride,
                                         bbeg, nb);
-    else warp_staged<NS, false, V4>(box, rk, P, t, W, pano, pw, ph, pstride, tiles, tstride,
+    else warp_staged<NS, false, V4>(box, xbuf, rk, P, t, W, pano, pw, ph, pstride, tiles, tstride,
                                     bbeg, nb);
 }
 
-__global__ void __launch_bounds__(kWB) k_warp_depth(const TileGeom* __restrict__ geom,
+#ifndef PF_WARP_WPE
+#define PF_WARP_WPE 1   // amdgpu_waves_per_eu minimum (occupancy target for the register budget)
+#endif
+__global__ void __launch_bounds__(kWB) __attribute__((amdgpu_waves_per_eu(PF_WARP_WPE)))
+k_warp_depth(const TileGeom* __restrict__ geom,
                                                     int ntiles,
                                                     const WarpPatch* __restrict__ patches,
                                                     int npatch, const uint32_t* __restrict__ wloc,
@@ -492,6 +536,24 @@ __global__ void __launch_bounds__(kWB) k_warp_depth(const TileGeom* __restrict__
     }
 
     W.full = PF_WARP_ROWPX && W.ok[0] && W.ok[kPx - 1] && g.c == 1;
+#if PF_WARP_XPOSE
+    static_assert(kPx == 4 && kPatch == 32 && !PF_WARP_ROWPX, "transpose: 8 rows x 32 per wave");
+    __shared__ float xbuf[kWB * kPx];
+    {
+        const int l = t & 63, rr = l >> 3;
+        const int Y = P.Y0 + 2 * (t >> 6) + (rr & 1) + 8 * (rr >> 1), X = P.X0 + 4 * (l & 7);
+        bool all = Y < g.h && g.c == 1;
+#pragma unroll
+        for (int j = 0; j < kPx; j++) {
+            const bool in = Y < g.h && X + j < g.w;
+            all = all && in;
+            W.oo[j] = in ? (uint32_t)(g.off + ((long long)Y * g.w + X + j) * g.c) * 4u : 0xFFFFFFF0u;
+        }
+        W.full = all && (W.oo[0] & 15u) == 0;
+    }
+#else
+    float* xbuf = nullptr;
+#endif
 #pragma unroll
     for (int k = 0; k < kPx; k++) W.la[k] *= PF_WARP_SPLIT ? 1 : 2;  // parity-interleaved box
     __shared__ RespK rk[kNB];  // published by the first barrier inside warp_staged
@@ -499,19 +561,21 @@ __global__ void __launch_bounds__(kWB) k_warp_depth(const TileGeom* __restrict__
     const bool rs = resp != nullptr;
     if (PF_WARP_V4 && (pw & 3) == 0) {  // quad-aligned boxes (k_patch_box): 16-B staging loads
         const int nq = (P.bw * P.bh / 4 + kWB - 1) / kWB;  // uniform: loads per thread
-        if (nq <= 1) warp_staged_sel<1, true>(rs, box, rk, P, t, W, pano, pw, ph, pstride, tiles,
+        if (nq <= 1) warp_staged_sel<1, true>(rs, box, xbuf, rk, P, t, W, pano, pw, ph, pstride, tiles,
                                               tstride, bbeg, nb);
-        else if (nq <= 2) warp_staged_sel<2, true>(rs, box, rk, P, t, W, pano, pw, ph, pstride,
+        else if (nq <= 2) warp_staged_sel<2, true>(rs, box, xbuf, rk, P, t, W, pano, pw, ph, pstride,
                                                    tiles, tstride, bbeg, nb);
-        else warp_staged_sel<kSlots / 4, true>(rs, box, rk, P, t, W, pano, pw, ph, pstride,
+        else warp_staged_sel<kSlots / 4, true>(rs, box, xbuf, rk, P, t, W, pano, pw, ph, pstride,
                                                tiles, tstride, bbeg, nb);
     } else {
         const int ns = (P.bw * P.bh + kWB - 1) / kWB;  // uniform: staging loads per thread
-        if (ns <= 4) warp_staged_sel<4, false>(rs, box, rk, P, t, W, pano, pw, ph, pstride,
-                                               tiles, tstride, bbeg, nb);
-        else if (ns <= 8) warp_staged_sel<8, false>(rs, box, rk, P, t, W, pano, pw, ph, pstride,
-                                                    tiles, tstride, bbeg, nb);
-        else warp_staged_sel<kSlots, false>(rs, box, rk, P, t, W, pano, pw, ph, pstride, tiles,
+        // staging slots never exceed kSlots: slot s writes LDS unit t + s*kWB < kCap
+        constexpr int N1 = kSlots < 4 ? kSlots : 4, N2 = kSlots < 8 ? kSlots : 8;
+        if (ns <= N1) warp_staged_sel<N1, false>(rs, box, xbuf, rk, P, t, W, pano, pw, ph, pstride,
+                                                 tiles, tstride, bbeg, nb);
+        else if (ns <= N2) warp_staged_sel<N2, false>(rs, box, xbuf, rk, P, t, W, pano, pw, ph, pstride,
+                                                      tiles, tstride, bbeg, nb);
+        else warp_staged_sel<kSlots, false>(rs, box, xbuf, rk, P, t, W, pano, pw, ph, pstride, tiles,
                                             tstride, bbeg, nb);
     }
 }
