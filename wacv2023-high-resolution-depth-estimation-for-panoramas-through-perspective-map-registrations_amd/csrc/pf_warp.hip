@@ -69,6 +69,9 @@ static constexpr int kNB = PF_WARP_BATCH;               // panoramas per block
 #ifndef PF_WARP_STPOL
 #define PF_WARP_STPOL 2  // cache policy bits of the tile stores (gfx950: 2 = nt, 16 = sc1)
 #endif
+#ifndef PF_WARP_PFD
+#define PF_WARP_PFD 2    // staging prefetch depth in panoramas (register sets in flight)
+#endif
 #ifndef PF_WARP_DIAG
 #define PF_WARP_DIAG 0   // probes only: 1 = no tile stores, 2 = no panorama loads (wrong output)
 #endif
@@ -352,7 +355,8 @@ __device__ __forceinline__ void warp_staged(float* box, float* xbuf, const RespK
         col = col < pw ? col : col - pw;
         goff[s] = (uint32_t)(row * pw + col) * 4u;
     }
-    float stg[2][NS][U];
+    constexpr int D = PF_WARP_PFD;  // prefetch depth: panorama j is staged in stg[j % D]
+    float stg[D][NS][U];
     const uint32_t pbytes = (uint32_t)(pstride * 4);
     auto fetch = [&](float (*dst)[U], int q) {
         const auto pr = rsrc(pano + (long long)(bbeg + (q < nb ? q : nb - 1)) * pstride, pbytes);
@@ -378,9 +382,9 @@ __device__ __forceinline__ void warp_staged(float* box, float* xbuf, const RespK
                 else box[2 * ((t + s * kWB) * U + j) + pa] = src[s][j];
             }
     };
-    auto iter = [&](auto parity, int q) {
-        constexpr int PA = decltype(parity)::value;
-        fetch(stg[PA], q + 2);  // panorama q was put into parity PA last iteration: reuse stg[PA]
+    auto iter = [&](auto parity, auto slot, int q) {
+        constexpr int PA = decltype(parity)::value, SL = decltype(slot)::value;  // q%2, q%D
+        fetch(stg[SL], q + D);  // panorama q was put into parity PA last iteration: reuse stg[SL]
         const float* L = PF_WARP_SPLIT ? box + PA * kCap : box + PA;
         const int b = bbeg + q;
         const auto orr = rsrc(tiles + b * tstride, (uint32_t)(tstride * 4));
@@ -438,16 +442,31 @@ __device__ __forceinline__ void warp_staged(float* box, float* xbuf, const RespK
                 __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(out[k]), orr, (int)W.oo[k],
                                                       0, PF_WARP_STPOL);
         }
-        put(1 - PA, stg[1 - PA]);  // panorama q+1 (a duplicate past the chunk: unread)
+        put(1 - PA, stg[(SL + 1) % D]);  // panorama q+1 (a duplicate past the chunk: unread)
         __syncthreads();
     };
-    fetch(stg[0], 0);
-    fetch(stg[1], 1);
+#pragma unroll
+    for (int j = 0; j < D; j++) fetch(stg[j], j);
     put(0, stg[0]);
     __syncthreads();
-    for (int q = 0; q < nb; q += 2) {
-        iter(std::integral_constant<int, 0>{}, q);
-        if (q + 1 < nb) iter(std::integral_constant<int, 1>{}, q + 1);
+    using I0 = std::integral_constant<int, 0>;
+    using I1 = std::integral_constant<int, 1>;
+    using I2 = std::integral_constant<int, 2 % D>;
+    if constexpr (D == 2) {
+        for (int q = 0; q < nb; q += 2) {
+            iter(I0{}, I0{}, q);
+            if (q + 1 < nb) iter(I1{}, I1{}, q + 1);
+        }
+    } else {  // D == 3: parity x slot repeats every 6 panoramas
+        static_assert(D == 3, "prefetch depth 2 or 3");
+        for (int q = 0; q < nb; q += 6) {
+            iter(I0{}, I0{}, q);
+            if (q + 1 < nb) iter(I1{}, I1{}, q + 1);
+            if (q + 2 < nb) iter(I0{}, I2{}, q + 2);
+            if (q + 3 < nb) iter(I1{}, I0{}, q + 3);
+            if (q + 4 < nb) iter(I0{}, I1{}, q + 4);
+            if (q + 5 < nb) iter(I1{}, I2{}, q + 5);
+        }
     }
 }
 
