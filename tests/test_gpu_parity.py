@@ -194,14 +194,15 @@ def test_warp_depth_tolerance(fuser, cfg):
 
 def test_warp_depth_ragged_batch_and_resize(fuser):
     """Batch 19 (one full 16-panorama chunk + a ragged one), distinct responses per panorama,
-    then a different panorama size on the same context (the cached warp map must follow)."""
+    then other panorama sizes on the same context (the cached warp map must follow): 300 wide
+    stages 16-B quads, 302 wide (not a multiple of 4) the 4-B staging path."""
     lay = PL.config_layout("C1")
     fuser.set_tiles(lay)
     tiles, total = O.make_tiles(lay)
     B = 19
     seeds = pf_synth.seeds_for(B, 777)
     resp = pf_synth.responses(seeds, lay.ntiles)
-    for (pw, ph) in ((512, 256), (300, 150)):
+    for (pw, ph) in ((512, 256), (300, 150), (302, 151)):
         gt = pf_synth.scene_depth(seeds, pw, ph).numpy()
         out = torch.zeros((B, total), dtype=torch.float32, device=DEV)
         fuser.warp_depth(_dev(gt), out, panofuse.make_responses(resp, DEV))

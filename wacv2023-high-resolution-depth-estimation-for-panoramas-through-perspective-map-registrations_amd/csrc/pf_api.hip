@@ -78,6 +78,10 @@ struct pf_ctx {
     DevBuf buf[3], lnorm, coeffs, lsum_ws, metrics_ws, reg_sums, reg_active;
     // SolveDepthBySmoothing (pf_smooth.hip): boxes, grid tables, per-pixel source and mask
     DevBuf sm_box, sm_cols, sm_rows, sm_src, sm_mask;
+    // its compacted pixel list (k_smooth_iter_list), cached for one (boxes, size, band) key
+    DevBuf sm_list, sm_off;
+    std::vector<SmoothBox> sm_key_boxes;
+    int sm_key[4] = {0, 0, 0, 0}, sm_nk = 0, sm_smin = 0, sm_smax = -1;
     // level-0 seed index tables of the streaming Jacobi (run_jacobi), keyed by level and emap
     DevBuf seed_ecol, seed_erow;
     // resident level kernel (pf_jres.hip): hand-off rows, and the sync words ([0] ticket
@@ -1408,9 +1412,66 @@ int pf_solve_smoothing(pf_ctx* c, const float* tiles, const float* coeffs, int b
     launch_smooth_map(c->stream, (const TileGeom*)c->geom.p, (const SmoothBox*)c->sm_box.p,
                       c->ntiles, (const GridCol*)c->sm_cols.p, (const GridRow*)c->sm_rows.p,
                       out_w, out_h, (int2*)c->sm_src.p, (uint8_t*)c->sm_mask.p);
-    launch_smooth(c->stream, (const TileGeom*)c->geom.p, c->ntiles, (const int2*)c->sm_src.p,
-                  (const uint8_t*)c->sm_mask.p, tiles, c->tile_elems, coeffs, out_w, out_h, L.h0,
-                  L.h1, 500, (float*)c->buf[0].p, batch);  // 500 iterations (:1838)
+    const int iters = 500;  // :1838
+    static const bool scan = getenv("PF_SMOOTH_SCAN") && atoi(getenv("PF_SMOOTH_SCAN"));
+    if (scan) {  // every (X, Y) of the diagonal tested against the mask (the first form)
+        launch_smooth(c->stream, (const TileGeom*)c->geom.p, c->ntiles, (const int2*)c->sm_src.p,
+                      (const uint8_t*)c->sm_mask.p, tiles, c->tile_elems, coeffs, out_w, out_h,
+                      L.h0, L.h1, iters, (float*)c->buf[0].p, batch);
+    } else {
+        const bool same = c->sm_key_boxes.size() == boxes.size() && c->sm_key[0] == out_w &&
+                          c->sm_key[1] == out_h && c->sm_key[2] == L.h0 && c->sm_key[3] == L.h1 &&
+                          std::equal(boxes.begin(), boxes.end(), c->sm_key_boxes.begin(),
+                                     [](const SmoothBox& a, const SmoothBox& b) {
+                                         return a.x0 == b.x0 && a.x1 == b.x1 && a.y0 == b.y0 &&
+                                                a.y1 == b.y1 && a.xs == b.xs;
+                                     });
+        if (!same) {  // the band's masked pixels by parity of d = X + Y, sorted by d
+            std::vector<uint8_t> mask(n);
+            HIPCHK(c, hipMemcpyAsync(mask.data(), c->sm_mask.p, n, hipMemcpyDeviceToHost,
+                                     c->stream));
+            HIPCHK(c, hipStreamSynchronize(c->stream));
+            const int nk = (out_w + out_h) / 2 + 1;  // d = 2k + p < w + h
+            std::vector<int> cnt(2 * (nk + 1), 0);
+            int dmin = INT32_MAX, dmax = -1;
+            for (int Y = L.h0; Y <= L.h1; Y++)
+                for (int X = 1; X <= out_w - 2; X++)
+                    if (mask[(long long)Y * out_w + X]) {
+                        const int d = X + Y;
+                        cnt[(d & 1) * (nk + 1) + (d >> 1) + 1]++;
+                        dmin = std::min(dmin, d);
+                        dmax = std::max(dmax, d);
+                    }
+            std::vector<int> off(cnt.size());
+            int acc = 0;
+            for (int p = 0; p < 2; p++)
+                for (int k = 0; k <= nk; k++) {
+                    acc += cnt[p * (nk + 1) + k];
+                    off[p * (nk + 1) + k] = acc;  // k = 0 holds the zero count: start of d = p
+                }
+            std::vector<int> fill(off), list(std::max(acc, 1));
+            for (int Y = L.h0; Y <= L.h1; Y++)
+                for (int X = 1; X <= out_w - 2; X++)
+                    if (mask[(long long)Y * out_w + X]) {
+                        const int d = X + Y;
+                        list[fill[(d & 1) * (nk + 1) + (d >> 1)]++] = Y * out_w + X;
+                    }
+            if ((rc = upload(c, c->sm_list, list))) return rc;
+            if ((rc = upload(c, c->sm_off, off))) return rc;
+            c->sm_nk = nk;
+            c->sm_smin = dmin;
+            c->sm_smax = dmax < 0 ? -1 : dmax + 2 * (iters - 1);
+            c->sm_key_boxes = boxes;
+            c->sm_key[0] = out_w; c->sm_key[1] = out_h; c->sm_key[2] = L.h0; c->sm_key[3] = L.h1;
+        }
+        launch_smooth_seed(c->stream, (const TileGeom*)c->geom.p, c->ntiles,
+                           (const int2*)c->sm_src.p, tiles, c->tile_elems, coeffs, out_w, out_h,
+                           (float*)c->buf[0].p, batch);
+        if (c->sm_smax >= c->sm_smin)
+            launch_smooth_list(c->stream, (const int*)c->sm_list.p, (const int*)c->sm_off.p,
+                               c->sm_nk, out_w, out_h, c->sm_smin, c->sm_smax, iters,
+                               (float*)c->buf[0].p, batch);
+    }
     launch_quantize(c->stream, (const float*)c->buf[0].p, n, (int)n, out, n, batch);
     HIPCHK(c, hipGetLastError());
     return PF_OK;

@@ -264,6 +264,11 @@ void launch_warp_rgb(hipStream_t s, const RgbCam* cams, const TileGeom* geom, in
 void launch_smooth_map(hipStream_t s, const TileGeom* geom, const SmoothBox* box, int ntiles,
                        const GridCol* cols, const GridRow* rows, int w, int h, int2* src,
                        uint8_t* mask);
+void launch_smooth_seed(hipStream_t s, const TileGeom* geom, int ntiles, const int2* src,
+                        const float* tiles, long long tstride, const float* coeffs, int w, int h,
+                        float* buf, int batch);
+void launch_smooth_list(hipStream_t s, const int* list, const int* off, int nk, int w, int h,
+                        int smin, int smax, int iters, float* buf, int batch);
 void launch_smooth(hipStream_t s, const TileGeom* geom, int ntiles, const int2* src,
                    const uint8_t* mask, const float* tiles, long long tstride,
                    const float* coeffs, int w, int h, int h0, int h1, int iters, float* buf,

@@ -11,7 +11,7 @@
 //    tables), and the to-smooth flag.
 //  * k_smooth_seed: per panorama the buffer (0 where no tile covers), with the optional
 //    Depth2DepthTransform applied on the fly as the fusion does.
-//  * k_smooth_iter: the Gauss-Seidel sweeps.  Pixel (X, Y) of iteration i reads (X-1, Y) and
+//  * k_smooth_iter_list (default) / k_smooth_iter: the Gauss-Seidel sweeps.  Pixel (X, Y) of iteration i reads (X-1, Y) and
 //    (X, Y-1) of iteration i and (X+1, Y), (X, Y+1) of iteration i-1, so the lexicographic order
 //    is reproduced exactly by the wavefront schedule s = X + Y + 2i: every read comes from step
 //    s-1 and is overwritten only at step s+1, and the pixels of one step (X + Y = s - 2i, one
@@ -115,6 +115,45 @@ __global__ void __launch_bounds__(1024) k_smooth_iter(float* __restrict__ buf,
     }
 }
 
+// The same schedule over a compacted pixel list (the default): the masked pixels of the band,
+// split by the parity of d = X + Y and sorted by d, with off[p*nk + k] the first index of
+// d = 2k + p (nk + 1 entries per parity).  Step s updates exactly the pixels with
+// d in [s - 2(iters-1), s] and d = s (mod 2) -- one contiguous index range -- instead of testing
+// every (X, Y) of the diagonal band against the mask (most of which are not smoothed).
+__global__ void __launch_bounds__(1024) k_smooth_iter_list(float* __restrict__ buf,
+                                                           const int* __restrict__ list,
+                                                           const int* __restrict__ off, int nk,
+                                                           int w, long long npx, int smin,
+                                                           int smax, int iters)
+{
+    float* B = buf + (long long)blockIdx.x * npx;
+    const int t = threadIdx.x;
+    for (int s = smin; s <= smax; s++) {
+        const int p = s & 1;
+        const int dlo = s - 2 * (iters - 1);
+        const int kl = dlo > p ? (dlo - p) >> 1 : 0, kh = min(nk - 1, (s - p) >> 1);
+        if (kl <= kh) {
+            const int* o2 = off + p * (nk + 1);
+            const int lo = o2[kl], hi = o2[kh + 1];
+            for (int j = lo + t; j < hi; j += 1024) {
+                const int o = list[j];
+                const float val = B[o];
+                const float v0 = B[o - 1], v1 = B[o + 1], v2 = B[o - w], v3 = B[o + w];
+                const float avg = (((v0 + v1) + v2) + v3) / 4.0f;
+                B[o] = (float)((double)val + 0.5 * (double)(avg - val));
+            }
+        }
+        __syncthreads();  // step s's writes are visible to step s+1 (one workgroup, one CU)
+    }
+}
+
+void launch_smooth_list(hipStream_t s, const int* list, const int* off, int nk, int w, int h,
+                        int smin, int smax, int iters, float* buf, int batch)
+{
+    hipLaunchKernelGGL(k_smooth_iter_list, dim3(batch), dim3(1024), 0, s, buf, list, off, nk, w,
+                       (long long)w * h, smin, smax, iters);
+}
+
 void launch_smooth_map(hipStream_t s, const TileGeom* geom, const SmoothBox* box, int ntiles,
                        const GridCol* cols, const GridRow* rows, int w, int h, int2* src,
                        uint8_t* mask)
@@ -124,14 +163,21 @@ void launch_smooth_map(hipStream_t s, const TileGeom* geom, const SmoothBox* box
                        box, ntiles, cols, rows, w, h, src, mask);
 }
 
+void launch_smooth_seed(hipStream_t s, const TileGeom* geom, int ntiles, const int2* src,
+                        const float* tiles, long long tstride, const float* coeffs, int w, int h,
+                        float* buf, int batch)
+{
+    const int n = w * h;
+    hipLaunchKernelGGL(k_smooth_seed, dim3((unsigned)((n + 255) / 256), batch), dim3(256), 0, s,
+                       geom, ntiles, src, n, tiles, tstride, coeffs, buf);
+}
+
 void launch_smooth(hipStream_t s, const TileGeom* geom, int ntiles, const int2* src,
                    const uint8_t* mask, const float* tiles, long long tstride,
                    const float* coeffs, int w, int h, int h0, int h1, int iters, float* buf,
                    int batch)
 {
-    const int n = w * h;
-    hipLaunchKernelGGL(k_smooth_seed, dim3((unsigned)((n + 255) / 256), batch), dim3(256), 0, s,
-                       geom, ntiles, src, n, tiles, tstride, coeffs, buf);
+    launch_smooth_seed(s, geom, ntiles, src, tiles, tstride, coeffs, w, h, buf, batch);
     hipLaunchKernelGGL(k_smooth_iter, dim3(batch), dim3(1024), 0, s, buf, mask, w, h, h0, h1,
                        iters);
 }
