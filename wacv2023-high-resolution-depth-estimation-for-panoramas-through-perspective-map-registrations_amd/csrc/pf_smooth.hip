@@ -120,6 +120,10 @@ __global__ void __launch_bounds__(1024) k_smooth_iter(float* __restrict__ buf,
 // d = 2k + p (nk + 1 entries per parity).  Step s updates exactly the pixels with
 // d in [s - 2(iters-1), s] and d = s (mod 2) -- one contiguous index range -- instead of testing
 // every (X, Y) of the diagonal band against the mask (most of which are not smoothed).
+// Measured on MI355X (C3 layout, 2048x1024): 426 -> 180 ms at batch 1, 642 -> 256 ms at batch
+// 64; 4 or 8 pixels per thread in flight measured the same or slower (tools/smooth_probe.py): the
+// one workgroup per panorama is bound by its CU's vector-memory issue, ~2.1k wave-updates of 7
+// scattered accesses per step.
 __global__ void __launch_bounds__(1024) k_smooth_iter_list(float* __restrict__ buf,
                                                            const int* __restrict__ list,
                                                            const int* __restrict__ off, int nk,
