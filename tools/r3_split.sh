@@ -1,5 +1,6 @@
 #!/bin/bash
-# Round 3: co-scheduled half-batch fusions (bench.py PF_SPLIT) vs the default step, alternating.
+# Round 3: co-scheduled half-batch fusions vs the default step, alternating.  The PF_SPLIT knob
+# lived in bench.py for this A/B only (measured slower, removed).
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
 mkdir -p gpurun_out/split
 for r in 1 2; do
