@@ -524,9 +524,9 @@ int pf_set_tiles(pf_ctx* c, const pf_window* fovs, const pf_window* ranges, int 
     c->reg_valid = false;
     c->wmap_pw = c->wmap_ph = 0;
     std::vector<WarpPatch> patches;
-    const int pe = warp_patch_edge();
+    const int pe = warp_patch_edge(), peh = warp_patch_height();
     for (int i = 0; i < ntiles; i++)
-        for (int y = 0; y < tile_h[i]; y += pe)
+        for (int y = 0; y < tile_h[i]; y += peh)
             for (int x = 0; x < tile_w[i]; x += pe) patches.push_back(WarpPatch{i, x, y, 0, 0, 0, 0, 0});
     c->npatch = (int)patches.size();
     int rc;

@@ -248,6 +248,7 @@ void launch_register_joint(hipStream_t s, const double* sums, const int* active,
 void launch_apply_cubic(hipStream_t s, const TileGeom* geom, int ntiles, long long tile_elems,
                         float* tiles, long long tstride, const float* coeffs, int batch);
 int warp_patch_edge();
+int warp_patch_height();
 void launch_warp_prepare(hipStream_t s, const TileGeom* geom, int ntiles, long long npix_max,
                          WarpPatch* patches, int npatch, int pw, int ph, uint32_t* wloc,
                          float* wfxy);

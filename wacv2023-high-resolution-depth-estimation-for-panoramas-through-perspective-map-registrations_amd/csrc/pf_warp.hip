@@ -35,16 +35,25 @@ namespace pf {
 #ifndef PF_WARP_PATCH
 #define PF_WARP_PATCH 32
 #endif
+#ifndef PF_WARP_WAVEBOX
+// one 32x8 patch per WAVE with its own LDS box and no workgroup barrier (waves drift and overlap
+// each other's latencies) instead of one 32x32 patch per 256-thread block with a barrier per
+// panorama (SQ counters: ~20% of the block form's wave-cycles wait at barriers)
+#define PF_WARP_WAVEBOX 0
+#endif
 static constexpr int kWB = PF_WARP_WB;                  // threads per block
-static constexpr int kPatch = PF_WARP_PATCH;            // patch edge in tile pixels
-static_assert(kWB % kPatch == 0 && kPatch * kPatch % kWB == 0, "whole patch rows per slot");
-static constexpr int kPx = kPatch * kPatch / kWB;       // pixels per thread
+static constexpr int kPatch = PF_WARP_PATCH;            // patch width in tile pixels
+static constexpr int kPatchH = PF_WARP_WAVEBOX ? 8 : kPatch;  // patch height
+static_assert(kWB % kPatch == 0 && kPatch * kPatchH % kWB == 0, "whole patch rows per slot");
+static_assert(!PF_WARP_WAVEBOX || (kPatch == 32 && kWB == 256), "wave boxes: 32x8 patches");
+static constexpr int kPx = kPatch * kPatchH / kWB;      // pixels per thread (prep passes)
 #ifndef PF_WARP_CAP
 #define PF_WARP_CAP 4096
 #endif
-static constexpr int kCap = PF_WARP_CAP;                // LDS floats per staged footprint
+static constexpr int kCapB = PF_WARP_CAP;               // LDS floats per parity per block
+static constexpr int kCap = PF_WARP_WAVEBOX ? kCapB / 4 : kCapB;  // per staged footprint
 static constexpr int kSlots = kCap / kWB;               // staging loads per thread
-static_assert(kCap % (4 * kWB) == 0, "whole 16-B staging slots (the V4 path) fill the box");
+static_assert(PF_WARP_WAVEBOX || kCap % (4 * kWB) == 0, "whole 16-B staging slots fill the box");
 #ifndef PF_WARP_BATCH
 #define PF_WARP_BATCH 16
 #endif
@@ -310,13 +319,14 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc(const void* base, uint32_
     return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), 0, (int)bytes, 0x00020000);
 }
 
-struct WarpLanes {  // one thread's kPx pixels, all panorama-invariant
-    uint32_t la[kPx];   // LDS float index of corner (x0, y0) in the parity-interleaved box (x2)
-    uint32_t oo[kPx];   // byte offset of the pixel inside one panorama's tile block; past the
+static constexpr int kLPx = PF_WARP_WAVEBOX ? 4 : kPx;  // pixels per lane in the main kernel
+struct WarpLanes {  // one thread's kLPx pixels, all panorama-invariant
+    uint32_t la[kLPx];  // LDS float index of corner (x0, y0) in the parity-interleaved box (x2)
+    uint32_t oo[kLPx];  // byte offset of the pixel inside one panorama's tile block; past the
                         // block (a dropped buffer store) for lanes outside the tile
-    uint32_t hp[kPx];   // mix32(pixel index): the per-pixel half of the noise hash
-    f2 wx[kPx], wy[kPx];  // (1-fx, fx), (1-fy, fy)
-    bool ok[kPx];
+    uint32_t hp[kLPx];  // mix32(pixel index): the per-pixel half of the noise hash
+    f2 wx[kLPx], wy[kLPx];  // (1-fx, fx), (1-fy, fy)
+    bool ok[kLPx];
     bool full;  // the kPx pixels are inside the tile and contiguous (one channel): 16-B store
     // XPOSE: oo[] are the byte offsets of the lane's 4 pixels AFTER the transpose (row
     // 2*wave + (l>>3 & 1) + 8*(l>>4), columns 4*(l&7)..+3 of the patch); full = all inside,
@@ -333,6 +343,7 @@ struct WarpLanes {  // one thread's kPx pixels, all panorama-invariant
 // for panorama q+1's loads -- an in-order vmcnt -- never covers them.  A thread's four pixels
 // are consecutive in one tile row: one 16-B store per panorama when they are all inside.
 typedef uint32_t u4v __attribute__((ext_vector_type(4)));
+#if !PF_WARP_WAVEBOX  // the block form (default)
 template <int NS, bool RESP, bool V4>
 __device__ __forceinline__ void warp_staged(float* box, float* xbuf, const RespK* rk,
                                             const WarpPatch& P,
@@ -599,6 +610,213 @@ k_warp_depth(const TileGeom* __restrict__ geom,
     }
 }
 
+#endif  // !PF_WARP_WAVEBOX
+
+#if PF_WARP_WAVEBOX
+__device__ __forceinline__ void wave_sync()
+{  // a wave's LDS operations complete in order; this only keeps the compiler from moving them
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// One wave, one 32x8 patch: the warp_staged loop with the box in the wave's own LDS region
+// (kCap floats per parity) and wave_sync() where the block form has __syncthreads().
+template <int NS, bool RESP, bool V4>
+__device__ __forceinline__ void warp_wave(float* box, const RespK* rk, const WarpPatch& P, int l,
+                                          const WarpLanes& W, const float* __restrict__ pano,
+                                          int pw, int ph, long long pstride,
+                                          float* __restrict__ tiles, long long tstride, int bbeg,
+                                          int nb)
+{
+    constexpr int U = V4 ? 4 : 1;
+    static_assert(NS * 64 * U <= kCap, "staging slots stay inside the wave's box");
+    const int bwu = P.bw / U, units = bwu * P.bh;
+    uint32_t goff[NS];
+#pragma unroll
+    for (int s = 0; s < NS; s++) {
+        int e = l + s * 64;
+        e = e < units ? e : units - 1;
+        const int r = e / bwu, c = (e - r * bwu) * U;
+        int row = P.gy0 + r;
+        row = row < ph ? row : ph - 1;
+        int col = P.gx0 + c;
+        col = col < pw ? col : col - pw;
+        goff[s] = (uint32_t)(row * pw + col) * 4u;
+    }
+    float stg[2][NS][U];
+    const uint32_t pbytes = (uint32_t)(pstride * 4);
+    auto fetch = [&](float (*dst)[U], int q) {
+        const auto pr = rsrc(pano + (long long)(bbeg + (q < nb ? q : nb - 1)) * pstride, pbytes);
+#pragma unroll
+        for (int s = 0; s < NS; s++) {
+            if constexpr (V4) {
+                const u4v v = __builtin_amdgcn_raw_buffer_load_b128(pr, (int)goff[s], 0, 0);
+#pragma unroll
+                for (int j = 0; j < 4; j++) dst[s][j] = __uint_as_float(v[j]);
+            } else {
+                dst[s][0] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(pr, (int)goff[s], 0, 0));
+            }
+        }
+    };
+    auto put = [&](int pa, const float (*src)[U]) {
+#pragma unroll
+        for (int s = 0; s < NS; s++)
+#pragma unroll
+            for (int j = 0; j < U; j++) box[pa * kCap + (l + s * 64) * U + j] = src[s][j];
+    };
+    auto iter = [&](auto parity, int q) {
+        constexpr int PA = decltype(parity)::value;
+        fetch(stg[PA], q + 2);
+        const float* L = box + PA * kCap;
+        const int b = bbeg + q;
+        const auto orr = rsrc(tiles + b * tstride, (uint32_t)(tstride * 4));
+        f2 al{}, ka{}, be{}, si{};
+        uint32_t key = 0;
+        if (RESP) {
+            const RespK r = rk[q];
+            al = f2{r.alpha, r.alpha}; ka = f2{r.kappa, r.kappa};
+            be = f2{r.beta, r.beta}; si = f2{r.sigma, r.sigma};
+            key = r.key;
+        }
+        float out[kLPx];
+#pragma unroll
+        for (int k = 0; k < kLPx; k += 2) {
+            f2 v;
+#pragma unroll
+            for (int j = 0; j < 2; j++) {
+                const float* c = L + W.la[k + j];
+                v[j] = bilinear(f2{c[0], c[1]}, f2{c[P.bw], c[P.bw + 1]}, W.wx[k + j], W.wy[k + j]);
+            }
+            if (RESP) {
+                const f2 u = f2{noise_top24(W.hp[k], key), noise_top24(W.hp[k + 1], key)};
+                const f2 nz = __builtin_elementwise_fma(u, f2{0x1p-23f, 0x1p-23f},
+                                                        f2{-1.0f, -1.0f});
+                f2 tt = al * v;
+                tt = tt + (ka * v) * v;
+                tt = tt + be;
+                v = pk_add_clamp01(tt, si * nz);
+            }
+            out[k] = v[0];
+            out[k + 1] = v[1];
+        }
+#pragma unroll
+        for (int k = 0; k < kLPx; k++)
+            __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(out[k]), orr, (int)W.oo[k], 0,
+                                                  PF_WARP_STPOL);
+        put(1 - PA, stg[1 - PA]);  // panorama q+1 (a duplicate past the chunk: unread)
+        wave_sync();
+    };
+    fetch(stg[0], 0);
+    fetch(stg[1], 1);
+    put(0, stg[0]);
+    wave_sync();
+    for (int q = 0; q < nb; q += 2) {
+        iter(std::integral_constant<int, 0>{}, q);
+        if (q + 1 < nb) iter(std::integral_constant<int, 1>{}, q + 1);
+    }
+}
+
+template <int NS, bool V4>
+__device__ __forceinline__ void warp_wave_sel(bool resp, float* box, const RespK* rk,
+                                              const WarpPatch& P, int l, const WarpLanes& W,
+                                              const float* pano, int pw, int ph, long long pstride,
+                                              float* tiles, long long tstride, int bbeg, int nb)
+{
+    if (resp) warp_wave<NS, true, V4>(box, rk, P, l, W, pano, pw, ph, pstride, tiles, tstride,
+                                      bbeg, nb);
+    else warp_wave<NS, false, V4>(box, rk, P, l, W, pano, pw, ph, pstride, tiles, tstride, bbeg,
+                                  nb);
+}
+
+__global__ void __launch_bounds__(kWB) k_warp_wave(const TileGeom* __restrict__ geom, int ntiles,
+                                                   const WarpPatch* __restrict__ patches,
+                                                   int npatch, const uint32_t* __restrict__ wloc,
+                                                   const float2* __restrict__ wfxy,
+                                                   const float* __restrict__ pano, int pw, int ph,
+                                                   long long pstride, const Resp* __restrict__ resp,
+                                                   float* __restrict__ tiles, long long tstride,
+                                                   int batch)
+{
+    __shared__ float boxes[4][2 * kCap];
+    __shared__ RespK rks[4][kNB];
+    const int npb = (npatch + 3) / 4;
+    const unsigned lb = xcd_remap(blockIdx.x, gridDim.x);
+    const int pb = (int)(lb % (unsigned)npb), chunk = (int)(lb / (unsigned)npb);
+    const int w = (int)(threadIdx.x >> 6), l = (int)(threadIdx.x & 63);
+    const int pid = pb * 4 + w;
+    if (pid >= npatch) return;  // whole wave; nothing below synchronises across waves
+    const WarpPatch P = patches[pid];
+    const TileGeom& g = geom[P.tile];
+    const int bbeg = chunk * kNB;
+    const int nb = min(kNB, batch - bbeg);
+    WarpLanes W;
+#pragma unroll
+    for (int k = 0; k < kLPx; k++) {  // lane l: column l & 31, rows (l >> 5) + 2k of the patch
+        const int X = P.X0 + (l & 31), Y = P.Y0 + (l >> 5) + 2 * k;
+        const int i = Y * g.w + X;
+        W.ok[k] = X < g.w && Y < g.h;
+        W.la[k] = 0; W.wx[k] = f2{1.0f, 0.0f}; W.wy[k] = f2{1.0f, 0.0f};
+        W.hp[k] = mix32((uint32_t)i);
+        W.oo[k] = W.ok[k] ? (uint32_t)(g.off + (long long)i * g.c) * 4u : 0xFFFFFFF0u;
+        if (W.ok[k]) {
+            W.la[k] = wloc[g.pix_off + i];
+            const float2 f = wfxy[g.pix_off + i];
+            W.wx[k] = f2{1.0f - f.x, f.x};
+            W.wy[k] = f2{1.0f - f.y, f.y};
+        }
+    }
+    if (P.wide) {  // footprint too large for the wave's box: direct corner gathers
+        for (int q = 0; q < nb; q++) {
+            const int b = bbeg + q;
+            const float* pp = pano + b * pstride;
+            const RespK r = resp_key(resp, b, ntiles, P.tile);
+            float* out = tiles + b * tstride;
+#pragma unroll
+            for (int k = 0; k < kLPx; k++) {
+                if (!W.ok[k]) continue;
+                const uint32_t o00 = W.la[k] & 0x3FFFFFFFu, dx = W.la[k] >> 31;
+                const uint32_t o10 = o00 + (((W.la[k] >> 30) & 1u) ? (uint32_t)pw : 0u);
+                float v = bilinear(f2{pp[o00], pp[o00 + dx]}, f2{pp[o10], pp[o10 + dx]},
+                                   W.wx[k], W.wy[k]);
+                if (resp) {
+                    const float nz = __builtin_fmaf(noise_top24(W.hp[k], r.key), 0x1p-23f, -1.0f);
+                    float tt = r.alpha * v;
+                    tt = tt + (r.kappa * v) * v;
+                    tt = tt + r.beta;
+                    tt = tt + r.sigma * nz;
+                    v = tt < 0.0f ? 0.0f : (tt > 1.0f ? 1.0f : tt);
+                }
+                out[W.oo[k] >> 2] = v;
+            }
+        }
+        return;
+    }
+    RespK* rk = rks[w];
+    if (l < nb) rk[l] = resp_key(resp, bbeg + l, ntiles, P.tile);
+    wave_sync();
+    const bool rs = resp != nullptr;
+    float* box = boxes[w];
+    if (PF_WARP_V4 && (pw & 3) == 0) {
+        const int nq = (P.bw * P.bh / 4 + 63) / 64;  // wave-uniform: 16-B loads per lane
+        if (nq <= 1) warp_wave_sel<1, true>(rs, box, rk, P, l, W, pano, pw, ph, pstride, tiles,
+                                            tstride, bbeg, nb);
+        else if (nq <= 2) warp_wave_sel<2, true>(rs, box, rk, P, l, W, pano, pw, ph, pstride,
+                                                 tiles, tstride, bbeg, nb);
+        else warp_wave_sel<kCap / 256, true>(rs, box, rk, P, l, W, pano, pw, ph, pstride, tiles,
+                                             tstride, bbeg, nb);
+    } else {
+        const int ns = (P.bw * P.bh + 63) / 64;
+        if (ns <= 4) warp_wave_sel<4, false>(rs, box, rk, P, l, W, pano, pw, ph, pstride, tiles,
+                                             tstride, bbeg, nb);
+        else if (ns <= 8) warp_wave_sel<8, false>(rs, box, rk, P, l, W, pano, pw, ph, pstride,
+                                                  tiles, tstride, bbeg, nb);
+        else warp_wave_sel<kCap / 64, false>(rs, box, rk, P, l, W, pano, pw, ph, pstride, tiles,
+                                             tstride, bbeg, nb);
+    }
+}
+#endif
+
 // ---------------------------------------------------------------------------------------------
 void launch_warp_prepare(hipStream_t s, const TileGeom* geom, int ntiles, long long npix_max,
                          WarpPatch* patches, int npatch, int pw, int ph, uint32_t* wloc,
@@ -613,16 +831,24 @@ void launch_warp_prepare(hipStream_t s, const TileGeom* geom, int ntiles, long l
 }
 
 int warp_patch_edge() { return kPatch; }
+int warp_patch_height() { return kPatchH; }
 
 void launch_warp_depth(hipStream_t s, const TileGeom* geom, int ntiles, const WarpPatch* patches,
                        int npatch, const uint32_t* wloc, const float* wfxy, const float* pano,
                        int pw, int ph, long long pstride, const Resp* resp, float* tiles,
                        long long tstride, int batch)
 {
+#if PF_WARP_WAVEBOX
+    const long long n = (long long)((npatch + 3) / 4) * ((batch + kNB - 1) / kNB);
+    hipLaunchKernelGGL(k_warp_wave, dim3((unsigned)n), dim3(kWB), 0, s, geom, ntiles, patches,
+                       npatch, wloc, (const float2*)wfxy, pano, pw, ph, pstride, resp, tiles,
+                       tstride, batch);
+#else
     const long long n = (long long)npatch * ((batch + kNB - 1) / kNB);
     hipLaunchKernelGGL(k_warp_depth, dim3((unsigned)n), dim3(kWB), 0, s, geom, ntiles, patches,
                        npatch, wloc, (const float2*)wfxy, pano, pw, ph, pstride, resp, tiles,
                        tstride, batch);
+#endif
 }
 
 }  // namespace pf
