@@ -38,7 +38,10 @@ namespace pf {
 #ifndef PF_WARP_WAVEBOX
 // one 32x8 patch per WAVE with its own LDS box and no workgroup barrier (waves drift and overlap
 // each other's latencies) instead of one 32x32 patch per 256-thread block with a barrier per
-// panorama (SQ counters: ~20% of the block form's wave-cycles wait at barriers)
+// panorama (SQ counters: ~20% of the block form's wave-cycles wait at barriers).  Measured
+// slower on MI355X at C3 (tools/r3_wb.sh): 0.69 ms with 1024-float wave boxes, 0.83 with 512,
+// against 0.53 for the block form (bit-identical tiles) -- the small boxes re-read more and send
+// more patches to the direct-gather path.  Off.
 #define PF_WARP_WAVEBOX 0
 #endif
 static constexpr int kWB = PF_WARP_WB;                  // threads per block
