@@ -146,6 +146,9 @@ static constexpr int kTGW = kTPW + 2, kTGH = kTPH + 2, kTG = kTGW * kTGH;  // gr
 #define PF_TGT_NB 8
 #endif
 static constexpr int kTNB = PF_TGT_NB;                           // panoramas per block
+#ifndef PF_TGT_NT
+#define PF_TGT_NT 1  // nt stores of the target planes (keep the tiles' lines in L2): 0.629-0.633 -> 0.618-0.623 ms per C3 step (tools/r3_tgt.sh); 4 / 16 panoramas per block 0.639-0.651 / 0.730
+#endif
 
 __device__ __forceinline__ bool box_meets(const TileBox& bx, int X0, int X1, int Y0, int Y1)
 {  // does the box (X from x0 stepping xs, stopping before x1; rows y0..y1) meet [X0,X1]x[Y0,Y1]
@@ -256,7 +259,8 @@ __global__ void __launch_bounds__(256) k_targets_patch(const TileGeom* __restric
             if (n[j] == 0) out = __uint_as_float(PF_NAN_MARKER);
             else if (n[j] == 1) out = acc[j][q];
             else out = acc[j][q] * scale;
-            lnorm[b * lstride + o] = out;
+            if constexpr (PF_TGT_NT) __builtin_nontemporal_store(out, &lnorm[b * lstride + o]);
+            else lnorm[b * lstride + o] = out;
         }
     }
 }
