@@ -147,7 +147,10 @@ static constexpr int kTGW = kTPW + 2, kTGH = kTPH + 2, kTG = kTGW * kTGH;  // gr
 #endif
 static constexpr int kTNB = PF_TGT_NB;                           // panoramas per block
 #ifndef PF_TGT_NT
-#define PF_TGT_NT 1  // nt stores of the target planes (keep the tiles' lines in L2): 0.629-0.633 -> 0.618-0.623 ms per C3 step (tools/r3_tgt.sh); 4 / 16 panoramas per block 0.639-0.651 / 0.730
+// nt stores of the target planes keep the tiles' lines in L2 for the neighbouring patches: the
+// stage went 0.629-0.633 -> 0.618-0.623 ms per C3 step (tools/r3_tgt.sh, profiles/r03/tgt/);
+// 4 / 16 panoramas per block measured 0.639-0.651 / 0.730
+#define PF_TGT_NT 1
 #endif
 
 __device__ __forceinline__ bool box_meets(const TileBox& bx, int X0, int X1, int Y0, int Y1)
