@@ -27,6 +27,10 @@
 // differ from W*-1/4 only in the sign of a zero, which cannot reach b' because b is never -0.)
 #include "pf_internal.hpp"
 
+#ifndef PF_JNT
+#define PF_JNT 0  // nt stores of the streamed passes' finished rows (A/B knob)
+#endif
+
 #include <cstdlib>
 #include <cstring>
 
@@ -549,7 +553,11 @@ struct JLag {
                         make_uint2(qv[0] | (qv[1] << 16), qv[2] | (qv[3] << 16));
                 }
             } else {
-                if constexpr (C == 2)
+                if constexpr (C == 2 && PF_JNT) {
+                    typedef float f2v __attribute__((ext_vector_type(2)));
+                    __builtin_nontemporal_store(f2v{nw[T - 1].v[0], nw[T - 1].v[1]},
+                                                reinterpret_cast<f2v*>(dst + rowb + lo));
+                } else if constexpr (C == 2)
                     *reinterpret_cast<float2*>(dst + rowb + lo) = make_float2(nw[T - 1].v[0], nw[T - 1].v[1]);
                 else
                     *reinterpret_cast<float4*>(dst + rowb + lo) =
