@@ -11,6 +11,9 @@ launched on 8 GPUs it is C4 (512 panoramas, 64 per GPU, no collective on the dat
     python bench.py [--gpus N --steps K --warmup W --batch B]
     python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N
 
+Run directly with --gpus N > 1 it launches the N ranks itself (torch.distributed.run as a child,
+started before any GPU call; launch_ranks), so both forms print the same N-rank line.
+
 Rank 0 prints one JSON line.  `roofline` is for the dominant kernel (the Jacobi sweep) against
 its real roof, VALU issue: algorithmic FLOP (14 per pixel-update) per launch over its average
 hipEvent-measured launch time; `roofline_hbm` puts the same kernel's measured PMC traffic on the
@@ -51,6 +54,8 @@ def parse():
     ap.add_argument("--prof-steps", type=int, default=2,
                     help="extra untimed steps with the per-stage hipEvent timers on (roofline)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-extra-configs", action="store_true",
+                    help="skip the C2 batch-1 latency and the one-GPU C5 sub-records")
     ap.add_argument("--pipeline", type=int, default=1,
                     help="1: software-pipelined steps -- the warp of batch k+1 (second stream) "
                          "runs while batch k is registered and fused; every step still warps, "
@@ -164,7 +169,7 @@ def _metrics_traffic():
     return 3 * h + e if h is not None and e is not None else None
 
 
-def run_c5(args, rank, world, local, dev):
+def c5_measure(args, rank, world, local, dev, steps, warmup):
     """BASELINE config C5: one 8192x4096 panorama, 80 tiles of 1024^2 sharded over the ranks.
     Each rank warps and registers its own tiles (a sub-layout context writing into its slice of
     the full tile block), scatters their targets per level (pf_fuse_partial); the (sum L, n) grids
@@ -216,19 +221,20 @@ def run_c5(args, rank, world, local, dev):
             be = pf_dist.HipTileShardBackend(fz, emap, tiles, coeffs, out_w, zr, out)
             pf_dist.fuse_tile_sharded(be, nlevels, lay.ntiles, rank, world, comm)
 
-    for _ in range(args.warmup):
+    for _ in range(warmup):
         step()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     ts = time.perf_counter()
-    for _ in range(args.steps):
+    for _ in range(steps):
         step()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - ts
+    fz.synchronize()  # PF_ETIMEOUT if any fusion's resident kernel timed out
     mine_s = elapsed
     if world > 1:
         t = torch.tensor([elapsed], dtype=torch.float64,
@@ -245,8 +251,17 @@ def run_c5(args, rank, world, local, dev):
         fz.merge(emap, full, ref[None], zr, coeffs=torch.zeros_like(coeffs)[None])
         torch.cuda.synchronize()
         bit_exact = bool(torch.equal(ref, out))
+    nz = int((out != 0).sum().item())
+    return {"value": steps / elapsed, "elapsed": elapsed, "mine_s": mine_s,
+            "bit_exact": bit_exact, "nonzero_px": nz}
+
+
+def run_c5(args, rank, world, local, dev):
+    """bench.py --mode c5: the C5 line (c5_measure) on `world` ranks."""
+    import torch.distributed as dist
+    r = c5_measure(args, rank, world, local, dev, args.steps, args.warmup)
+    elapsed, mine_s, bit_exact, nz = r["elapsed"], r["mine_s"], r["bit_exact"], r["nonzero_px"]
     if rank == 0:
-        nz = int((out != 0).sum().item())
         print(json.dumps({
             "metric": "panoramas/sec (whole node), 8192x4096 x 80 tiles (BASELINE config C5)",
             "value": args.steps / elapsed, "unit": "panoramas/s", "n_gpus": world,
@@ -268,6 +283,41 @@ def run_c5(args, rank, world, local, dev):
         dist.destroy_process_group()
     if rank == 0 and not bit_exact:
         sys.exit("C5: the sharded result differs from the one-GPU fusion")
+
+
+def c2_latency(local, dev, lay, zr, reps=7):
+    """BASELINE config C2 -- one 2048x1024 panorama, 20 tiles of 512^2, one GPU -- as a latency:
+    warp + registration + fusion of ONE panorama (what MergeDepthMaps times per panorama,
+    Depth.cpp:792-808, 907-916), hipEvents on the context's stream around each run, after the
+    layout caches exist (the facade keeps them across panoramas); median and min of `reps`."""
+    import torch
+
+    import panofuse
+    import pf_synth
+    seeds = pf_synth.seeds_for(1, 424242)
+    gt = pf_synth.scene_depth(seeds, 2048, 1024, dev).contiguous()
+    emap = pf_synth.baseline_emap(seeds, 512, 256, dev).contiguous()
+    resp = panofuse.make_responses(pf_synth.responses(seeds, lay.ntiles), dev)
+    f = panofuse.Fuser(local)
+    f.set_tiles(lay)
+    tiles = torch.empty((1, f.tile_elems), dtype=torch.float32, device=dev)
+    out = torch.empty((1, 1024, 2048), dtype=torch.int16, device=dev)
+    coeffs = torch.empty((1, lay.ntiles, 4), dtype=torch.float32, device=dev)
+    times = []
+    for i in range(reps + 2):
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        f.warp_depth(gt, tiles, resp)
+        f.merge(emap, tiles, out, zr, coeffs=coeffs)
+        e1.record()
+        torch.cuda.synchronize()
+        if i >= 2:  # two warm runs first
+            times.append(e0.elapsed_time(e1))
+    f.synchronize()
+    times.sort()
+    return {"median_ms": times[len(times) // 2], "min_ms": times[0], "reps": reps,
+            "workload": "C2: one 2048x1024 panorama, 20 tiles of 512^2: warp + registration + "
+                        "3-level fusion + u16, hipEvents around each run (median)"}
 
 
 def rank_seeds(batch, rank):
@@ -349,6 +399,53 @@ def timed_steps(step, sync, args, world, dist, device=None):
     return mine, elapsed
 
 
+def _free_port():
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def launch_ranks(args):
+    """`bench.py --gpus N` run directly (no WORLD_SIZE in the environment): start the N ranks
+    ourselves -- one process per GPU under torch.distributed.run, rendezvous on 127.0.0.1 -- and
+    return their exit status.  Runs BEFORE anything touches the GPU: only the device count is read
+    (torch.cuda.device_count() does not initialise HIP), and the parent makes no other GPU call,
+    so no process that has initialised the GPU is ever replaced or forked.  Returns None when this
+    process is itself the (only) rank.  Refuses, with a message and a non-zero exit:
+      * --gpus that disagrees with a launcher's WORLD_SIZE;
+      * N ranks on fewer than N visible devices (unless --same-device: the one-GPU rehearsal);
+      * --same-device with the nccl backend (RCCL refuses two ranks on one device)."""
+    env_world = os.environ.get("WORLD_SIZE")
+    if env_world is not None:
+        if int(env_world) != args.gpus:
+            sys.exit(f"bench.py: --gpus {args.gpus} but the launcher started WORLD_SIZE="
+                     f"{env_world} ranks; pass --gpus {env_world}")
+        return None
+    if args.gpus < 1:
+        sys.exit(f"bench.py: --gpus {args.gpus}: need at least one")
+    if args.gpus == 1:
+        return None
+    if args.same_device and args.backend == "nccl" and not args.stand_in:
+        sys.exit("bench.py: --same-device needs --backend gloo (RCCL refuses two ranks on one "
+                 "device)")
+    if not args.stand_in and not args.same_device:
+        import torch
+        n = torch.cuda.device_count()
+        if n < args.gpus:
+            sys.exit(f"bench.py: --gpus {args.gpus} needs {args.gpus} GPUs, {n} visible (for a "
+                     f"one-GPU rehearsal add --same-device --backend gloo)")
+    import subprocess
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+           f"--nproc-per-node={args.gpus}", "--master-addr", "127.0.0.1",
+           f"--master-port={_free_port()}", os.path.abspath(__file__)] + sys.argv[1:]
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")  # dmabuf IPC (RCCL across processes)
+    return subprocess.run(cmd, env=env).returncode
+
+
 def run_stand_in(args, rank, world):
     """The batch-sharded launcher with a CPU stand-in step (gloo): each rank 'processes' its own
     seed block, sleeping a rank-dependent time per step; rank 0 prints the bench line plus the
@@ -377,6 +474,9 @@ def run_stand_in(args, rank, world):
 
 def main():
     args = parse()
+    rc = launch_ranks(args)
+    if rc is not None:
+        sys.exit(rc)
     import numpy as np
     import torch
     import torch.distributed as dist
@@ -394,6 +494,9 @@ def main():
         return run_stand_in(args, rank, world)
     if args.same_device:
         local = 0
+    elif torch.cuda.device_count() <= local:
+        sys.exit(f"bench.py: rank {rank} wants cuda:{local}, "
+                 f"{torch.cuda.device_count()} device(s) visible")
     if world > 1:
         if args.backend == "nccl":
             dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local}"))
@@ -428,6 +531,9 @@ def main():
         mine_s, elapsed = timed_steps(pstep, torch.cuda.synchronize, args, world, dist, dev)
     else:
         mine_s, elapsed = timed_steps(step, torch.cuda.synchronize, args, world, dist, dev)
+    # every fusion of the run was valid: raises PF_ETIMEOUT (non-zero exit) if a resident-kernel
+    # hand-off wait timed out in any of them
+    fz.synchronize()
     # Per-kernel roofline: the same steps again with the library's hipEvent stage timers on
     # (recorded on the stream the kernels run on).  With the timers on, the library runs each
     # batch unsplit (no half-batch stream overlap), so every stage's time is its own.
@@ -464,6 +570,16 @@ def main():
         torch.cuda.synchronize()
         smooth[f"batch{nb}_ms"] = e0.elapsed_time(e1)
         del o_s
+
+    # the other single-GPU BASELINE configs, for the record (outside the timed steps)
+    c2 = c2_latency(local, dev, lay, zr) if not args.no_extra_configs else None
+    c5 = None
+    if world == 1 and not args.no_extra_configs:
+        r5 = c5_measure(args, 0, 1, local, dev, steps=3, warmup=1)
+        c5 = {"value": r5["value"], "unit": "panoramas/s", "ms_per_panorama": 1e3 / r5["value"],
+              "steps": 3, "bit_exact_vs_one_gpu": r5["bit_exact"],
+              "workload": "C5 on one GPU: one 8192x4096 panorama, 80 tiles of 1024^2 (10x8), "
+                          "2048x1024 baseline, 4 levels (bench.py --mode c5 at world 1)"}
 
     total_panos = B * world * args.steps
     value = total_panos / elapsed
@@ -582,6 +698,9 @@ def main():
             "smoothing_ablation": dict(smooth, note="pf_solve_smoothing (SolveDepthBySmoothing, "
                                        "500 Gauss-Seidel sweeps near tile edges), outside the step"),
             "bit_exact_vs_one_process": bit_exact,
+            "c2_batch1_ms": c2["median_ms"] if c2 else None,
+            "c2_batch1": c2,
+            "c5_one_gpu": c5,
             "backend": args.backend if world > 1 else None,
             "per_rank": per_rank,
         }

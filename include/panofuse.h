@@ -30,6 +30,9 @@ extern "C" {
 #define PF_EHIP (-3)       /* HIP runtime error */
 #define PF_ESTATE (-4)     /* call order (e.g. no tiles set) */
 #define PF_EDEGENERATE (-5) /* a tile box with x0 == x1 (the reference loops forever there) */
+#define PF_ETIMEOUT (-6)   /* a resident-kernel hand-off wait timed out: the fusion's output is
+                            * invalid (see pf_jres_errors); reported by pf_synchronize, and by
+                            * the next pf_fuse / pf_merge once the timed-out fusion has finished */
 
 typedef struct pf_ctx pf_ctx;
 
@@ -54,6 +57,9 @@ void pf_destroy(pf_ctx* ctx);
 const char* pf_last_error(const pf_ctx* ctx);
 /* hipStream_t to order all work on (NULL = the null stream). */
 int pf_set_stream(pf_ctx* ctx, void* hip_stream);
+/* Waits for the context stream.  Returns PF_ETIMEOUT (message in pf_last_error) when a fusion
+ * enqueued since the last report had a resident-kernel wait time out, i.e. its u16 output is
+ * invalid -- the reference's "return false" on a failed merge (Depth.cpp:767-778). */
 int pf_synchronize(pf_ctx* ctx);
 const char* pf_version(void);
 
@@ -212,6 +218,11 @@ int pf_set_jacobi_engine(pf_ctx* ctx, int mode, int row_blocks);
  * here instead of hanging the device (the level's result is then invalid).  Synchronises the
  * context stream; returns the count since the context was created (>= 0) or an error code. */
 int pf_jres_errors(pf_ctx* ctx);
+/* Test hook (no reference counterpart): in the context's NEXT resident launch, row block 0 of
+ * every panorama withholds its hand-off flag and every wait gives up after 2^spin_log2 polls
+ * (spin_log2 in [4, 24]), so the neighbouring blocks time out: the fusion must then report
+ * PF_ETIMEOUT.  The launch after that runs normally. */
+int pf_debug_jres_fault(pf_ctx* ctx, int spin_log2);
 
 /* ---- parity probes (bit-exact index maps) ----
  * For level `level` of out_w: per covered pixel and tap k (5 taps in std::map order), the
@@ -219,6 +230,18 @@ int pf_jres_errors(pf_ctx* ctx);
  * tap_index: [out_h_level][w][5] int32 device buffer.  lsum/cnt as pf_fuse_partial. */
 int pf_probe_taps(pf_ctx* ctx, int out_w, int out_h, float zr0, float zr1, int level,
                   int32_t* tap_index);
+/* The E->P warps' coordinate maps, exactly as pf_warp_depth / pf_warp_rgb build and cache them
+ * (host code, glibc transcendentals as the reference calls them; no context or GPU needed).
+ * HOST buffers, one tile of tile_w x tile_h with viewing window *fov, panorama pw x ph:
+ *   pf_probe_warp_coords: wxy[h*w] = x0 | y0 << 16, wfxy[h*w][2] = (fx, fy) -- the bilinear
+ *     corner and weights of ToSphericalCoord (Depth.cpp:157-166) at ValueAtCoord's convention;
+ *   pf_probe_rgb_taps: taps[h*w][4] = {ix0 | iy0 << 16, ix1 | iy1 << 16, ax bits, ay bits} --
+ *     the GL_REPEAT corners and GL_LINEAR weights of SaveCubeMap's camera ray (Main.cpp:246-269,
+ *     fs_perspective.txt:67-73). */
+int pf_probe_warp_coords(const pf_window* fov, int tile_w, int tile_h, int pw, int ph,
+                         uint32_t* wxy, float* wfxy);
+int pf_probe_rgb_taps(const pf_window* fov, int tile_w, int tile_h, int pw, int ph,
+                      uint32_t* taps);
 
 /* ---- accuracy metrics ----
  * ErrorData (Depth.cpp:1980-2213) when given16 != NULL: the u16 result [batch][h][w];

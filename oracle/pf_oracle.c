@@ -653,27 +653,53 @@ static inline float response(const pfo_response* r, uint32_t idx, float d)
     return v;
 }
 
+/* a5's coordinate map of tile pixel (X,Y): (X/(W-1), Y/(H-1)) -> ToSphericalCoord
+ * (Depth.cpp:157-166, WorldToSpherical :2960-2971 with glibc atan2f) -> ValueAtCoord's pixel
+ * convention (az/2pi*(pw-1), zen/pi*(ph-1)) -> bilinear corner (x0, y0) and weights (fx, fy). */
+static inline void warp_coord(const pfo_tile* t, int X, int Y, int pw, int ph, int* x0o, int* y0o,
+                              float* fxo, float* fyo)
+{
+    float xy_x = (float)X / (float)(t->width - 1);
+    float xy_y = (float)Y / (float)(t->height - 1);
+    float sc[2];
+    pfo_to_spherical_coord(t, xy_x, xy_y, sc);
+    float px = (float)((double)sc[0] / (2 * MYPI) * (double)(pw - 1));
+    float py = (float)((double)sc[1] / MYPI * (double)(ph - 1));
+    int x0 = (int)floorf(px), y0 = (int)floorf(py);
+    float fx = px - (float)x0, fy = py - (float)y0;
+    if (x0 < 0) { x0 = 0; fx = 0; }
+    if (y0 < 0) { y0 = 0; fy = 0; }
+    if (x0 > pw - 1) { x0 = pw - 1; fx = 0; }
+    if (y0 > ph - 1) { y0 = ph - 1; fy = 0; }
+    *x0o = x0; *y0o = y0; *fxo = fx; *fyo = fy;
+}
+
+void pfo_warp_coords(const pfo_tile* t, int pw, int ph, uint32_t* wxy, float* wfxy)
+{ /* the map of one tile: wxy = x0 | y0 << 16, wfxy = (fx, fy) per pixel, row-major */
+#pragma omp parallel for schedule(static)
+    for (int Y = 0; Y < t->height; Y++)
+        for (int X = 0; X < t->width; X++) {
+            int x0, y0;
+            float fx, fy;
+            warp_coord(t, X, Y, pw, ph, &x0, &y0, &fx, &fy);
+            long long i = (long long)Y * t->width + X;
+            wxy[i] = (uint32_t)x0 | ((uint32_t)y0 << 16);
+            wfxy[2 * i] = fx;
+            wfxy[2 * i + 1] = fy;
+        }
+}
+
 void pfo_warp_depth(const float* pano, int pw, int ph, const pfo_tile* tiles, int ntiles,
                     const pfo_response* resp, float* tile_data)
-{ /* a5: tile pixel (X,Y) -> (X/(W-1), Y/(H-1)) -> ToSphericalCoord -> bilinear sample of the
-   * equirectangular map at (az/2pi*(pw-1), zen/pi*(ph-1)) (ValueAtCoord's pixel convention) */
+{ /* a5: bilinear sample of the equirectangular map at warp_coord's corner and weights */
     for (int p = 0; p < ntiles; p++) {
         const pfo_tile* t = &tiles[p];
 #pragma omp parallel for schedule(static)
         for (int Y = 0; Y < t->height; Y++)
             for (int X = 0; X < t->width; X++) {
-                float xy_x = (float)X / (float)(t->width - 1);
-                float xy_y = (float)Y / (float)(t->height - 1);
-                float sc[2];
-                pfo_to_spherical_coord(t, xy_x, xy_y, sc);
-                float px = (float)((double)sc[0] / (2 * MYPI) * (double)(pw - 1));
-                float py = (float)((double)sc[1] / MYPI * (double)(ph - 1));
-                int x0 = (int)floorf(px), y0 = (int)floorf(py);
-                float fx = px - (float)x0, fy = py - (float)y0;
-                if (x0 < 0) { x0 = 0; fx = 0; }
-                if (y0 < 0) { y0 = 0; fy = 0; }
-                if (x0 > pw - 1) { x0 = pw - 1; fx = 0; }
-                if (y0 > ph - 1) { y0 = ph - 1; fy = 0; }
+                int x0, y0;
+                float fx, fy;
+                warp_coord(t, X, Y, pw, ph, &x0, &y0, &fx, &fy);
                 int x1 = x0 + 1 < pw ? x0 + 1 : pw - 1;
                 int y1 = y0 + 1 < ph ? y0 + 1 : ph - 1;
                 float g00 = pano[(long long)y0 * pw + x0], g01 = pano[(long long)y0 * pw + x1];
@@ -688,14 +714,14 @@ void pfo_warp_depth(const float* pano, int pw, int ph, const pfo_tile* tiles, in
     }
 }
 
-void pfo_warp_rgb(const uint8_t* pano, int pw, int ph, const pfo_tile* tiles, int ntiles,
-                  uint8_t* out)
+static void warp_rgb_impl(const uint8_t* pano, int pw, int ph, const pfo_tile* tiles, int ntiles,
+                          uint8_t* out, uint32_t* taps)
 { /* a18: the GL camera of SaveCubeMap (Main.cpp:242-326; gluLookAt up = z, gluPerspective
    * fovy/aspect), pixel centres, the exact texcoord map of fs_perspective.txt:67-73 that the
    * sphere mesh (SphereMesh.cpp:154-210) approximates, GL_LINEAR + GL_REPEAT (SphereMesh.cpp:74-
    * 77) on the u8 RGB texture, rows flipped to top-first as stbi_flip_vertically_on_write does.
    * Direction and angles are evaluated in double; parity against real OpenGL is unpinned. */
-    long long obase = 0;
+    long long obase = 0, tbase = 0;
     for (int p = 0; p < ntiles; p++) {
         const pfo_tile* t = &tiles[p];
         float s0 = t->az_left, s1 = t->az_right, s2 = t->zen_top, s3 = t->zen_down;
@@ -728,6 +754,14 @@ void pfo_warp_rgb(const uint8_t* pano, int pw, int ph, const pfo_tile* tiles, in
                 float ax = sx - (float)ix, ay = sy - (float)iy;
                 int ix0 = ((ix % pw) + pw) % pw, ix1 = (((ix + 1) % pw) + pw) % pw;
                 int iy0 = ((iy % ph) + ph) % ph, iy1 = (((iy + 1) % ph) + ph) % ph;
+                if (taps) { /* pfo_rgb_taps: the map only */
+                    uint32_t* tp = taps + 4 * (tbase + (long long)r * W + i);
+                    tp[0] = (uint32_t)ix0 | ((uint32_t)iy0 << 16);
+                    tp[1] = (uint32_t)ix1 | ((uint32_t)iy1 << 16);
+                    memcpy(&tp[2], &ax, 4);
+                    memcpy(&tp[3], &ay, 4);
+                    continue;
+                }
                 for (int c = 0; c < 3; c++) {
                     float t00 = pano[((long long)iy0 * pw + ix0) * 3 + c];
                     float t01 = pano[((long long)iy0 * pw + ix1) * 3 + c];
@@ -743,7 +777,20 @@ void pfo_warp_rgb(const uint8_t* pano, int pw, int ph, const pfo_tile* tiles, in
                 }
             }
         obase += (long long)W * H * 3;
+        tbase += (long long)W * H;
     }
+}
+
+void pfo_warp_rgb(const uint8_t* pano, int pw, int ph, const pfo_tile* tiles, int ntiles,
+                  uint8_t* out)
+{
+    warp_rgb_impl(pano, pw, ph, tiles, ntiles, out, NULL);
+}
+
+void pfo_rgb_taps(int pw, int ph, const pfo_tile* tiles, int ntiles, uint32_t* taps)
+{ /* the map of pfo_warp_rgb: per tile pixel (tiles in order, rows top-first) {ix0 | iy0 << 16,
+   * ix1 | iy1 << 16, bits of ax, bits of ay} */
+    warp_rgb_impl(NULL, pw, ph, tiles, ntiles, NULL, taps);
 }
 
 /* Parity probe: per pixel of a level, the linear tile index of each of the 5 taps of the first

@@ -157,10 +157,14 @@ int  pfo_merge(const float* emap, int ew, int eh, int ec, const pfo_tile* tiles,
 void pfo_warp_depth(const float* pano, int pw, int ph, const pfo_tile* tiles, int ntiles,
                     const pfo_response* resp, float* tile_data);
 uint32_t pfo_hash32(uint32_t seed, uint32_t idx);
+/* its coordinate map for one tile: wxy = x0 | y0 << 16, wfxy = (fx, fy) per pixel */
+void pfo_warp_coords(const pfo_tile* t, int pw, int ph, uint32_t* wxy, float* wfxy);
 
 /* ---------------- E->P RGB warp (a18: Main.cpp:242-326, fs_perspective.txt:67-73) --------- */
 void pfo_warp_rgb(const uint8_t* pano, int pw, int ph, const pfo_tile* tiles, int ntiles,
                   uint8_t* out);
+/* its tap map: 4 words per tile pixel {ix0 | iy0 << 16, ix1 | iy1 << 16, ax bits, ay bits} */
+void pfo_rgb_taps(int pw, int ph, const pfo_tile* tiles, int ntiles, uint32_t* taps);
 
 int  pfo_probe_taps(const pfo_tile* tiles, int ntiles, const pfo_level* L, int32_t* out);
 void pfo_set_threads(int n);

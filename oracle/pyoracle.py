@@ -99,6 +99,8 @@ def lib():
                                           C.c_float, C.POINTER(C.c_uint16)]
         L.pfo_warp_rgb.argtypes = [C.POINTER(C.c_uint8), C.c_int, C.c_int, TP, C.c_int,
                                    C.POINTER(C.c_uint8)]
+        L.pfo_warp_coords.argtypes = [TP, C.c_int, C.c_int, C.POINTER(C.c_uint32), fp]
+        L.pfo_rgb_taps.argtypes = [C.c_int, C.c_int, TP, C.c_int, C.POINTER(C.c_uint32)]
         L.pfo_hash32.argtypes = [C.c_uint32, C.c_uint32]
         L.pfo_hash32.restype = C.c_uint32
         L.pfo_set_threads.argtypes = [C.c_int]
@@ -342,6 +344,24 @@ def warp_depth(pano, tiles, total, resp=None):
     lib().pfo_warp_depth(_p(np.ascontiguousarray(pano, np.float32)), pw, ph, tiles, len(tiles),
                          resp, _p(out))
     return out
+
+
+def warp_coords(tile, pw, ph):
+    """The depth warp's map of one tile: (wxy uint32 [h*w] = x0 | y0 << 16, wfxy float32
+    [h*w, 2] = (fx, fy))."""
+    n = tile.width * tile.height
+    wxy = np.zeros(n, np.uint32)
+    wf = np.zeros((n, 2), np.float32)
+    lib().pfo_warp_coords(C.byref(tile), pw, ph, _p(wxy, C.c_uint32), _p(wf))
+    return wxy, wf
+
+
+def rgb_taps(tiles, pw, ph):
+    """The RGB warp's tap map of the layout: uint32 [sum h*w, 4]."""
+    total = sum(t.width * t.height for t in tiles)
+    taps = np.zeros((total, 4), np.uint32)
+    lib().pfo_rgb_taps(pw, ph, tiles, len(tiles), _p(taps, C.c_uint32))
+    return taps
 
 
 def warp_rgb(pano_u8, tiles):

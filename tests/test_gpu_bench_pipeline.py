@@ -65,3 +65,6 @@ def test_pipelined_bench_line():
     assert d["steps"] == 3 and d["n_gpus"] == 1 and d["value"] > 0
     assert "warp of batch k+1" in d["config"]["pipeline"]
     assert 0 < d["roofline"]["frac"] <= 1
+    # the other single-GPU configs ride along in the line
+    assert d["c2_batch1_ms"] > 0 and d["c2_batch1"]["reps"] >= 5
+    assert d["c5_one_gpu"]["value"] > 0 and d["c5_one_gpu"]["bit_exact_vs_one_gpu"] is True

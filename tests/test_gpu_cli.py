@@ -160,8 +160,9 @@ def test_export_rgb_tiles(tmp_path):
     """`panofuse_main export`: the tile render of mode 0 (SaveCubeMap, Main.cpp:242-326) for
     the LeReS layout at 1024 x 988 px, written as JPEG at quality 100 / 4:4:4 (Main.cpp:320)
     and decoded here by libjpeg (PIL), against the oracle's restatement of the GL camera: the
-    warp's 1 LSB bar (test_gpu_parity.py) plus the JPEG round trip's (tests/test_io.py), i.e.
-    within 4 levels, mean under 0.5.  OpenGL rasterisation parity is unpinned."""
+    warp itself is bit-exact (test_gpu_parity.py::test_warp_rgb_bit_exact), so what remains is
+    the JPEG round trip's bar (tests/test_io.py), i.e. within 4 levels, mean under 0.5.  OpenGL
+    rasterisation parity is unpinned."""
     Image = pytest.importorskip("PIL.Image")
     (tmp_path / "rgb").mkdir()
     h, w = 512, 1024

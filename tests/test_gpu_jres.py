@@ -102,3 +102,38 @@ def test_resident_concurrent_launches(fusers):
     assert torch.equal(o1, ref1)
     assert torch.equal(o2, ref2)
     other.close()
+
+
+def test_resident_timeout_is_reported(fusers):
+    """VERDICT r3 item 3 / ADVICE r3: a resident hand-off wait that times out must surface as
+    PF_ETIMEOUT (pf_synchronize, or the next pf_fuse / pf_merge), not as a silently wrong
+    panorama.  The fault hook makes row block 0 withhold its flag in one launch with waits
+    bounded at 2^10 polls; the launches after it run normally and stay bit-exact."""
+    stream, _ = fusers
+    f = panofuse.Fuser(0)
+    f.set_jacobi_engine(resident=True, row_blocks=4)  # 4 blocks per panorama: hand-offs happen
+    lay, emap, tiles = _inputs("C2", 2, 321)
+    ref = _fuse(stream, lay, emap, tiles, 2048)
+    torch.cuda.synchronize()
+    # 1. reported by pf_synchronize
+    f.debug_jres_fault(10)
+    _fuse(f, lay, emap, tiles, 2048)
+    with pytest.raises(panofuse.PanofuseError) as e:
+        f.synchronize()
+    assert e.value.code == panofuse.PF_ETIMEOUT and "timed out" in str(e.value)
+    assert f.jres_errors() > 0
+    # 2. the next launch runs normally: no error, bit-exact
+    got = _fuse(f, lay, emap, tiles, 2048)
+    f.synchronize()
+    assert torch.equal(got, ref)
+    # 3. reported by the next pf_fuse once the faulty fusion has finished
+    f.debug_jres_fault(10)
+    _fuse(f, lay, emap, tiles, 2048)
+    torch.cuda.synchronize()
+    with pytest.raises(panofuse.PanofuseError) as e:
+        _fuse(f, lay, emap, tiles, 2048)
+    assert e.value.code == panofuse.PF_ETIMEOUT
+    got = _fuse(f, lay, emap, tiles, 2048)
+    f.synchronize()
+    assert torch.equal(got, ref)
+    f.close()

@@ -34,7 +34,7 @@ def _port():
 def _launch(args, timeout=600):
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
            "--master-addr", "127.0.0.1", "--master-port", str(_port()), "bench.py",
-           "--backend", "gloo", "--same-device", "--no-cpu-baseline"] + args
+           "--backend", "gloo", "--same-device", "--no-cpu-baseline", "--no-extra-configs"] + args
     r = subprocess.run(cmd, cwd=ROOT, capture_output=True, text=True, timeout=timeout)
     assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
     lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
@@ -62,3 +62,38 @@ def test_batch_mode_two_processes():
     # whole-job value over the slowest rank's time
     tmax = max(p["elapsed_s"] for p in pr)
     assert d["value"] == pytest.approx(2 * B * steps / tmax, rel=1e-6)
+
+
+def _direct(args, timeout=600):
+    """bench.py run directly, as the driver runs `python3 bench.py --gpus N` (no torchrun)."""
+    env = dict(os.environ)
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT"):
+        env.pop(k, None)
+    return subprocess.run([sys.executable, "bench.py"] + args, cwd=ROOT, capture_output=True,
+                          text=True, timeout=timeout, env=env)
+
+
+def test_bench_gpus2_self_launch_same_device():
+    """`bench.py --gpus 2` without torchrun launches two ranks itself."""
+    B = 4
+    r = _direct(["--gpus", "2", "--same-device", "--backend", "gloo", "--batch", str(B),
+                 "--steps", "2", "--warmup", "1", "--prof-steps", "1", "--no-cpu-baseline",
+                 "--no-extra-configs"])
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout[-2000:]
+    d = json.loads(lines[0])
+    assert d["n_gpus"] == 2 and d["config"]["global_batch"] == 2 * B
+    assert d["bit_exact_vs_one_process"] is True
+    pr = sorted(d["per_rank"], key=lambda x: x["rank"])
+    blocks = [set(range(p["seed0"], p["seedN"] + 1)) for p in pr]
+    assert all(len(b) == B for b in blocks) and not (blocks[0] & blocks[1])
+
+
+def test_bench_gpus_more_than_visible_refused():
+    import torch
+    n = torch.cuda.device_count()  # counting devices does not initialise HIP
+    r = _direct(["--gpus", str(n + 1), "--steps", "1", "--warmup", "0", "--batch", "2",
+                 "--no-cpu-baseline"], timeout=300)
+    assert r.returncode != 0
+    assert f"needs {n + 1} GPUs" in r.stderr and not r.stdout.strip()

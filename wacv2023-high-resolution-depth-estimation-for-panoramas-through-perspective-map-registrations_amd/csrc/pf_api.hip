@@ -65,7 +65,11 @@ struct pf_ctx {
     std::vector<TileGeom> geom_h;
     std::vector<RegGrid> reg_h;
     long long tile_elems = 0, npix_max = 0, rgb_elems = 0;
-    DevBuf geom, reg, rcols, rrows, cams, rgb_off;
+    DevBuf geom, reg, rcols, rrows, rgb_off;
+    std::vector<RgbCam> cams_h;  // GL cameras of the RGB warp (SaveCubeMap), host only
+    // RGB warp taps for one panorama size (rgb_taps_host), built on first use
+    int rgb_pw = 0, rgb_ph = 0;
+    DevBuf rgbtap;
     LevelCache lc;
     bool reg_valid = false;
     uint32_t reg_zr0 = 0, reg_zr1 = 0;
@@ -90,6 +94,11 @@ struct pf_ctx {
     DevBuf jres_x, jres_sync;
     uint32_t jres_tk = 0, jres_fb = 1;
     int jres_mode = -1, jres_nb = 0;  // pf_set_jacobi_engine (-1: not set, PF_JRES decides)
+    // timeout reporting: after every resident launch the error word is copied (stream-ordered)
+    // into pinned host memory; a count above jres_err_seen is reported once as PF_ETIMEOUT
+    uint32_t* jres_err_h = nullptr;
+    uint32_t jres_err_seen = 0;
+    int jres_fault = 0;  // pf_debug_jres_fault: spin_log2 for the next resident launch (0: off)
     int seed_key[5] = {0, 0, 0, 0, 0};
     // stage profiling
     struct Span {
@@ -221,6 +230,30 @@ TileGeom set_window(const pf_window& f, int w, int h, int ch)
     return g;
 }
 
+// RGB camera of SaveCubeMap (Main.cpp:246-269: gluLookAt toward the window centre, up = z;
+// gluPerspective fovy / aspect), in double.
+RgbCam rgb_cam(const pf_window& f)
+{
+    float azc = (f.az_right + f.az_left) / 2, zenc = (f.zen_down + f.zen_top) / 2;
+    float fovx = (float)((f.az_right - f.az_left) / PF_MYPI * 180.0);
+    float fovy = (float)((f.zen_down - f.zen_top) / PF_MYPI * 180.0);
+    float aspect = (float)(tan(fovx / 180.0 * PF_MYPI / 2) / tan(fovy / 180.0 * PF_MYPI / 2));
+    RgbCam cam{};
+    double fv[3] = {cos((double)azc) * sin((double)zenc), sin((double)azc) * sin((double)zenc),
+                    cos((double)zenc)};
+    double fl = sqrt(fv[0] * fv[0] + fv[1] * fv[1] + fv[2] * fv[2]);
+    for (int k = 0; k < 3; k++) cam.f[k] = fv[k] / fl;
+    double sv[3] = {cam.f[1], -cam.f[0], 0.0};
+    double sl = sqrt(sv[0] * sv[0] + sv[1] * sv[1]);
+    cam.s[0] = sv[0] / sl; cam.s[1] = sv[1] / sl; cam.s[2] = 0.0;
+    cam.u[0] = cam.s[1] * cam.f[2] - cam.s[2] * cam.f[1];
+    cam.u[1] = cam.s[2] * cam.f[0] - cam.s[0] * cam.f[2];
+    cam.u[2] = cam.s[0] * cam.f[1] - cam.s[1] * cam.f[0];
+    cam.ty = tan((double)fovy / 180.0 * PF_MYPI / 2);
+    cam.tx = cam.ty * (double)aspect;
+    return cam;
+}
+
 LevelDims level_dims(int out_w, int out_h, float zr0, float zr1, int level)
 {  // Depth.cpp:1420-1437, 1650-1675
     LevelDims L{};
@@ -304,7 +337,7 @@ void pf_destroy(pf_ctx* c)
     if (!c) return;
     (void)hipSetDevice(c->device);
     (void)hipStreamSynchronize(c->stream);
-    DevBuf* all[] = {&c->geom, &c->reg, &c->rcols, &c->rrows, &c->cams, &c->rgb_off,
+    DevBuf* all[] = {&c->geom, &c->reg, &c->rcols, &c->rrows, &c->rgbtap, &c->rgb_off,
                      &c->buf[0], &c->buf[1], &c->buf[2], &c->lnorm, &c->coeffs, &c->lsum_ws,
                      &c->wmap, &c->wfxy, &c->wpatch, &c->metrics_ws, &c->reg_sums,
                      &c->reg_active, &c->sm_box, &c->sm_cols, &c->sm_rows, &c->sm_src,
@@ -333,6 +366,7 @@ void pf_destroy(pf_ctx* c)
     }
     for (hipEvent_t e : c->ev_level)
         if (e) (void)hipEventDestroy(e);
+    if (c->jres_err_h) (void)hipHostFree(c->jres_err_h);
     delete c;
 }
 
@@ -350,6 +384,26 @@ int pf_set_jacobi_engine(pf_ctx* c, int mode, int row_blocks)
     if (!c || mode < 0 || mode > 1 || row_blocks < 0) return PF_EINVAL;
     c->jres_mode = mode;
     c->jres_nb = row_blocks;
+    return PF_OK;
+}
+
+// PF_ETIMEOUT once for every new batch of timed-out resident-kernel waits whose count has
+// reached the host (the copy queued behind each resident launch); never blocks.
+static int jres_check(pf_ctx* c)
+{
+    if (!c->jres_err_h) return PF_OK;
+    const uint32_t n = __atomic_load_n(c->jres_err_h, __ATOMIC_ACQUIRE) & 0x7FFFFFFFu;
+    if (n == c->jres_err_seen) return PF_OK;
+    const uint32_t d = n - c->jres_err_seen;
+    c->jres_err_seen = n;
+    return fail(c, PF_ETIMEOUT, "resident Jacobi kernel: %u hand-off wait(s) timed out; the "
+                "fused output of that call is invalid", d);
+}
+
+int pf_debug_jres_fault(pf_ctx* c, int spin_log2)
+{
+    if (!c || spin_log2 < 4 || spin_log2 > 24) return PF_EINVAL;
+    c->jres_fault = spin_log2;
     return PF_OK;
 }
 
@@ -418,7 +472,7 @@ int pf_synchronize(pf_ctx* c)
     if (!c) return PF_EINVAL;
     HIPCHK(c, hipSetDevice(c->device));
     HIPCHK(c, hipStreamSynchronize(c->stream));
-    return PF_OK;
+    return jres_check(c);
 }
 
 int pf_level_info(int out_w, int out_h, float zr0, float zr1, int level, int* w, int* h,
@@ -434,6 +488,28 @@ int pf_level_info(int out_w, int out_h, float zr0, float zr1, int level, int* w,
     if (h1) *h1 = L.h1;
     if (iters) *iters = L.iters;
     if (nlevels) *nlevels = L.nlevels;
+    return PF_OK;
+}
+
+int pf_probe_warp_coords(const pf_window* fov, int tile_w, int tile_h, int pw, int ph,
+                         uint32_t* wxy, float* wfxy)
+{
+    if (!fov || !wxy || !wfxy || tile_w < 2 || tile_h < 2 || pw < 2 || ph < 2 || pw >= 65536 ||
+        ph >= 65536)
+        return PF_EINVAL;
+    const TileGeom g = set_window(*fov, tile_w, tile_h, 1);
+    warp_coords_host(g, pw, ph, wxy, wfxy);
+    return PF_OK;
+}
+
+int pf_probe_rgb_taps(const pf_window* fov, int tile_w, int tile_h, int pw, int ph,
+                      uint32_t* taps)
+{
+    static_assert(sizeof(RgbTap) == 16, "RgbTap is 4 words");
+    if (!fov || !taps || tile_w < 1 || tile_h < 1 || pw < 2 || ph < 2 || pw >= 65536 ||
+        ph >= 65536)
+        return PF_EINVAL;
+    rgb_taps_host(rgb_cam(*fov), tile_w, tile_h, pw, ph, reinterpret_cast<RgbTap*>(taps));
     return PF_OK;
 }
 
@@ -496,26 +572,7 @@ int pf_set_tiles(pf_ctx* c, const pf_window* fovs, const pf_window* ranges, int 
         long long np = (long long)tile_w[i] * tile_h[i];
         if (np > npmax) npmax = np;
         c->geom_h[i] = g;
-        // RGB camera (SaveCubeMap, Main.cpp:246-269), in double.
-        const pf_window& f = fovs[i];
-        float azc = (f.az_right + f.az_left) / 2, zenc = (f.zen_down + f.zen_top) / 2;
-        float fovx = (float)((f.az_right - f.az_left) / PF_MYPI * 180.0);
-        float fovy = (float)((f.zen_down - f.zen_top) / PF_MYPI * 180.0);
-        float aspect = (float)(tan(fovx / 180.0 * PF_MYPI / 2) / tan(fovy / 180.0 * PF_MYPI / 2));
-        RgbCam cam{};
-        double fv[3] = {cos((double)azc) * sin((double)zenc), sin((double)azc) * sin((double)zenc),
-                        cos((double)zenc)};
-        double fl = sqrt(fv[0] * fv[0] + fv[1] * fv[1] + fv[2] * fv[2]);
-        for (int k = 0; k < 3; k++) cam.f[k] = fv[k] / fl;
-        double sv[3] = {cam.f[1], -cam.f[0], 0.0};
-        double sl = sqrt(sv[0] * sv[0] + sv[1] * sv[1]);
-        cam.s[0] = sv[0] / sl; cam.s[1] = sv[1] / sl; cam.s[2] = 0.0;
-        cam.u[0] = cam.s[1] * cam.f[2] - cam.s[2] * cam.f[1];
-        cam.u[1] = cam.s[2] * cam.f[0] - cam.s[0] * cam.f[2];
-        cam.u[2] = cam.s[0] * cam.f[1] - cam.s[1] * cam.f[0];
-        cam.ty = tan((double)fovy / 180.0 * PF_MYPI / 2);
-        cam.tx = cam.ty * (double)aspect;
-        cams[i] = cam;
+        cams[i] = rgb_cam(fovs[i]);
     }
     c->tile_elems = off;
     c->rgb_elems = roff;
@@ -523,6 +580,8 @@ int pf_set_tiles(pf_ctx* c, const pf_window* fovs, const pf_window* ranges, int 
     c->lc.out_w = 0;  // boxes and registration grids depend on the ranges: rebuild lazily
     c->reg_valid = false;
     c->wmap_pw = c->wmap_ph = 0;
+    c->rgb_pw = c->rgb_ph = 0;
+    c->cams_h = cams;
     std::vector<WarpPatch> patches;
     const int pe = warp_patch_edge(), peh = warp_patch_height();
     for (int i = 0; i < ntiles; i++)
@@ -532,7 +591,6 @@ int pf_set_tiles(pf_ctx* c, const pf_window* fovs, const pf_window* ranges, int 
     int rc;
     if ((rc = upload(c, c->wpatch, patches))) return rc;
     if ((rc = upload(c, c->geom, c->geom_h))) return rc;
-    if ((rc = upload(c, c->cams, cams))) return rc;
     if ((rc = upload(c, c->rgb_off, rgb_off))) return rc;
     c->layout_ok = true;
     return PF_OK;
@@ -965,9 +1023,20 @@ static int jres_prepare(pf_ctx* c, const LevelDims& L, int batch, const JresPlan
                       (size_t)jp.K * L.w;
     if ((rc = ensure(c, c->jres_x, xb))) return rc;
     const size_t sb = sizeof(uint32_t) * (2 + (size_t)batch * jp.nb * jres_flags_per_block(jp.K));
+    if (!c->jres_err_h) {
+        HIPCHK(c, hipHostMalloc((void**)&c->jres_err_h, sizeof(uint32_t), hipHostMallocDefault));
+        *c->jres_err_h = 0;
+        c->jres_err_seen = 0;
+    }
     if (c->jres_sync.bytes < sb) {
+        if (c->jres_sync.p) {  // a new sync block restarts the error count at 0
+            HIPCHK(c, hipStreamSynchronize(c->stream));
+            if ((rc = jres_check(c))) return rc;  // report the old block's last timeouts first
+        }
         if ((rc = ensure(c, c->jres_sync, sb))) return rc;
         HIPCHK(c, hipMemsetAsync(c->jres_sync.p, 0, sb, c->stream));
+        *c->jres_err_h = 0;
+        c->jres_err_seen = 0;
         c->jres_tk = 0;
         c->jres_fb = 1;
     }
@@ -1009,6 +1078,12 @@ static float* run_jacobi(pf_ctx* c, const LevelDims& L, int first, const float* 
         A.flags = sync + 2;
         static const int dbg = getenv("PF_JRES_DBG") ? atoi(getenv("PF_JRES_DBG")) : 0;
         A.dbg = dbg;
+        A.spin_log2 = 24;
+        if (c->jres_fault) {  // pf_debug_jres_fault: this launch only
+            A.dbg |= 16;
+            A.spin_log2 = c->jres_fault;
+            c->jres_fault = 0;
+        }
         A.tbase = c->jres_tk;
         A.fbase = c->jres_fb;
         c->jres_tk += (uint32_t)(batch * jp->nb);
@@ -1018,6 +1093,10 @@ static float* run_jacobi(pf_ctx* c, const LevelDims& L, int first, const float* 
             fprintf(stderr, "jacobi plan %dx%d band %d iters %d batch %d resident: nb %d core %d K %d rounds %d\n",
                     L.w, L.h, L.h1 - L.h0 + 1, L.iters, batch, jp->nb, jp->core, jp->K, jp->rounds);
         launch_jres(c->stream, A);
+        // the error word, stream-ordered into pinned memory: jres_check reports it
+        if (c->jres_err_h)
+            (void)hipMemcpyAsync(c->jres_err_h, A.err, sizeof(uint32_t), hipMemcpyDeviceToHost,
+                                 c->stream);
         if (npasses) *npasses = 1;
         return dst;
     }
@@ -1345,6 +1424,7 @@ int pf_fuse(pf_ctx* c, const float* emap, int ew, int eh, int ec, const float* t
     if ((rc = check_common(c, batch))) return rc;
     if ((rc = check_emap(c, emap, ew, eh, ec))) return rc;
     if (!tiles || !out) return fail(c, PF_EINVAL, "tiles/out is NULL");
+    if ((rc = jres_check(c))) return rc;  // an earlier fusion's timeout, once it has landed
     return fuse_impl(c, emap, ew, eh, ec, tiles, coeffs, batch, out_w, out_h, zr0, zr1, out);
 }
 
@@ -1355,6 +1435,7 @@ int pf_merge(pf_ctx* c, const float* emap, int ew, int eh, int ec, const float* 
     if ((rc = check_common(c, batch))) return rc;
     if ((rc = check_emap(c, emap, ew, eh, ec))) return rc;
     if (!tiles || !out) return fail(c, PF_EINVAL, "tiles/out is NULL");
+    if ((rc = jres_check(c))) return rc;  // an earlier fusion's timeout, once it has landed
     float* cf = coeffs;
     if (!cf) {
         if ((rc = ensure(c, c->coeffs, sizeof(float) * 4 * c->ntiles * batch))) return rc;
@@ -1494,9 +1575,21 @@ int pf_warp_depth(pf_ctx* c, const float* pano, int pw, int ph, int batch,
     if (c->wmap_pw != pw || c->wmap_ph != ph) {
         if ((rc = ensure(c, c->wmap, sizeof(uint32_t) * npix))) return rc;
         if ((rc = ensure(c, c->wfxy, sizeof(float) * 2 * npix))) return rc;
-        launch_warp_prepare(c->stream, (const TileGeom*)c->geom.p, c->ntiles, c->npix_max,
-                            (WarpPatch*)c->wpatch.p, c->npatch, pw, ph, (uint32_t*)c->wmap.p,
-                            (float*)c->wfxy.p);
+        // corners and weights on the host (glibc atan2f: the reference's bits), tile by tile
+        std::vector<uint32_t> wxy((size_t)c->npix_max);
+        std::vector<float> wf(2 * (size_t)c->npix_max);
+        for (int p = 0; p < c->ntiles; p++) {
+            const TileGeom& g = c->geom_h[p];
+            const size_t n = (size_t)g.w * g.h;
+            warp_coords_host(g, pw, ph, wxy.data(), wf.data());
+            HIPCHK(c, hipMemcpyAsync((uint32_t*)c->wmap.p + g.pix_off, wxy.data(), 4 * n,
+                                     hipMemcpyHostToDevice, c->stream));
+            HIPCHK(c, hipMemcpyAsync((float*)c->wfxy.p + 2 * (size_t)g.pix_off, wf.data(), 8 * n,
+                                     hipMemcpyHostToDevice, c->stream));
+            HIPCHK(c, hipStreamSynchronize(c->stream));  // the host rows are reused
+        }
+        launch_warp_boxes(c->stream, (const TileGeom*)c->geom.p, (WarpPatch*)c->wpatch.p,
+                          c->npatch, pw, ph, (uint32_t*)c->wmap.p);
         HIPCHK(c, hipGetLastError());
         if ((rc = sort_warp_patches(c, pw))) return rc;
         c->wmap_pw = pw;
@@ -1517,9 +1610,26 @@ int pf_warp_rgb(pf_ctx* c, const uint8_t* pano, int pw, int ph, int batch, uint8
     if ((rc = check_common(c, batch))) return rc;
     if (!pano || !tiles || pw < 2 || ph < 2)
         return fail(c, PF_EINVAL, "bad pano %p %dx%d", (const void*)pano, pw, ph);
+    if (pw >= 65536 || ph >= 65536)
+        return fail(c, PF_EINVAL, "pano %dx%d: sides must be < 65536", pw, ph);
+    if (c->rgb_pw != pw || c->rgb_ph != ph) {  // the taps of this size, on the host (glibc)
+        const long long npix = c->tile_elems / c->tile_c;
+        if ((rc = ensure(c, c->rgbtap, sizeof(RgbTap) * npix))) return rc;
+        std::vector<RgbTap> taps((size_t)c->npix_max);
+        for (int p = 0; p < c->ntiles; p++) {
+            const TileGeom& g = c->geom_h[p];
+            rgb_taps_host(c->cams_h[p], g.w, g.h, pw, ph, taps.data());
+            HIPCHK(c, hipMemcpyAsync((RgbTap*)c->rgbtap.p + g.pix_off, taps.data(),
+                                     sizeof(RgbTap) * (size_t)g.w * g.h, hipMemcpyHostToDevice,
+                                     c->stream));
+            HIPCHK(c, hipStreamSynchronize(c->stream));
+        }
+        c->rgb_pw = pw;
+        c->rgb_ph = ph;
+    }
     StageTimer t(c, PF_STAGE_WARP, batch * (3.0 * pw * ph + (double)c->rgb_elems), 1);
-    launch_warp_rgb(c->stream, (const RgbCam*)c->cams.p, (const TileGeom*)c->geom.p, c->ntiles,
-                    c->npix_max, nullptr, (const long long*)c->rgb_off.p, pano, pw, ph,
+    launch_warp_rgb(c->stream, (const RgbTap*)c->rgbtap.p, (const TileGeom*)c->geom.p, c->ntiles,
+                    c->npix_max, (const long long*)c->rgb_off.p, pano, pw, ph,
                     (long long)pw * ph * 3, tiles, c->rgb_elems, batch);
     HIPCHK(c, hipGetLastError());
     return PF_OK;

@@ -514,7 +514,8 @@ bool SolveDepthAll(EquirectangularMap& emap, std::vector<PerspectiveMap>& pmaps,
     if (!pf_ok(c, pf_fuse(c, de.as<float>(), emap.width, emap.height, emap.channels,
                           dt.as<float>(), nullptr, 1, out_width, out_height, zr[0], zr[1],
                           dout.as<uint16_t>()),
-               "pf_fuse"))
+               "pf_fuse") ||
+        !pf_ok(c, pf_synchronize(c), "pf_synchronize"))  // PF_ETIMEOUT: invalid output
         return false;
     return hip_ok(hipMemcpy(data, dout.p, no * 2, hipMemcpyDeviceToHost), "download");
 }

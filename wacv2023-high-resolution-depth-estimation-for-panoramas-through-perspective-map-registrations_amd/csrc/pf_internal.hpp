@@ -62,6 +62,13 @@ struct RgbCam {
     double tx, ty;
 };
 
+// One RGB warp tap (k_warp_rgb): GL_REPEAT corners (x | y << 16) and GL_LINEAR weights of a tile
+// pixel, built on the host per layout and panorama size (rgb_taps_host).
+struct RgbTap {
+    uint32_t x0y0, x1y1;
+    float ax, ay;
+};
+
 // Synthetic depth-net response (same layout as pf_response in panofuse.h).
 struct Resp {
     float alpha, kappa, beta, sigma;
@@ -181,7 +188,9 @@ struct JresArgs {
     uint32_t* ticket;      // workgroup ticket counter (monotone across launches)
     uint32_t* err;         // spin timeouts (pf_jres_errors)
     uint32_t tbase, fbase; // this launch's first ticket / flag base
-    int dbg;               // profiling only (wrong results): 1 no hand-offs, 4 no rows, 8 no barriers
+    int dbg;               // profiling only (wrong results): 1 no hand-offs, 4 no rows, 8 no
+                           // barriers; 16 (pf_debug_jres_fault): row block 0 withholds its flag
+    int spin_log2;         // a hand-off wait gives up (and counts into err) after 2^spin_log2 polls
 };
 int jres_region_rows(int w);
 int jres_threads();
@@ -249,17 +258,19 @@ void launch_apply_cubic(hipStream_t s, const TileGeom* geom, int ntiles, long lo
                         float* tiles, long long tstride, const float* coeffs, int batch);
 int warp_patch_edge();
 int warp_patch_height();
-void launch_warp_prepare(hipStream_t s, const TileGeom* geom, int ntiles, long long npix_max,
-                         WarpPatch* patches, int npatch, int pw, int ph, uint32_t* wloc,
-                         float* wfxy);
+// host tables (pf_warp.hip): wxy/wfxy of one tile's pixels; the RGB taps of one tile
+void warp_coords_host(const TileGeom& g, int pw, int ph, uint32_t* wxy, float* wfxy);
+void rgb_taps_host(const RgbCam& cam, int W, int H, int pw, int ph, RgbTap* taps);
+// patch footprint boxes and in-box corner indices from the uploaded wxy (in place over wloc)
+void launch_warp_boxes(hipStream_t s, const TileGeom* geom, WarpPatch* patches, int npatch,
+                       int pw, int ph, uint32_t* wloc);
 void launch_warp_depth(hipStream_t s, const TileGeom* geom, int ntiles, const WarpPatch* patches,
                        int npatch, const uint32_t* wloc, const float* wfxy, const float* pano,
                        int pw, int ph, long long pstride, const Resp* resp, float* tiles,
                        long long tstride, int batch);
-void launch_warp_rgb(hipStream_t s, const RgbCam* cams, const TileGeom* geom, int ntiles,
-                     long long npix_total, const long long* pix_prefix,
-                     const long long* rgb_off, const uint8_t* pano, int pw, int ph,
-                     long long pstride, uint8_t* tiles, long long tstride, int batch);
+void launch_warp_rgb(hipStream_t s, const RgbTap* taps, const TileGeom* geom, int ntiles,
+                     long long npix_max, const long long* rgb_off, const uint8_t* pano, int pw,
+                     int ph, long long pstride, uint8_t* tiles, long long tstride, int batch);
 
 // SolveDepthBySmoothing (pf_smooth.hip).
 void launch_smooth_map(hipStream_t s, const TileGeom* geom, const SmoothBox* box, int ntiles,

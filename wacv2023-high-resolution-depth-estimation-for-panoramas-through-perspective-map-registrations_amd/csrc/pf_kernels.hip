@@ -696,8 +696,10 @@ __global__ void __launch_bounds__(kBlock) k_d2d_map(float* __restrict__ data, lo
         data[i * c] = cubic_map(data[i * c], a, b, cc, d);
 }
 
-// E->P RGB warp with the GL camera (a18).
-__global__ void __launch_bounds__(kBlock) k_warp_rgb(const RgbCam* __restrict__ cams,
+// E->P RGB warp with the GL camera (a18): the taps (corners, weights) come from the host table
+// (rgb_taps_host, glibc double atan2 as the oracle); per channel the GL_LINEAR blend in fp32 and
+// the round-to-nearest u8 store.
+__global__ void __launch_bounds__(kBlock) k_warp_rgb(const RgbTap* __restrict__ taps,
                                                      const TileGeom* __restrict__ geom,
                                                      const long long* __restrict__ rgb_off,
                                                      const uint8_t* __restrict__ pano, int pw,
@@ -709,22 +711,12 @@ __global__ void __launch_bounds__(kBlock) k_warp_rgb(const RgbCam* __restrict__ 
     const int W = geom[p].w, H = geom[p].h;
     long long i = (long long)blockIdx.x * kBlock + threadIdx.x;
     if (i >= (long long)W * H) return;
-    const RgbCam cam = cams[p];
-    int r = (int)(i / W), c = (int)(i - (long long)r * W);
-    double xn = 2.0 * (c + 0.5) / W - 1.0, yn = 1.0 - 2.0 * (r + 0.5) / H;
-    double d[3];
-    for (int k = 0; k < 3; k++) d[k] = cam.f[k] + cam.s[k] * (xn * cam.tx) + cam.u[k] * (yn * cam.ty);
-    double az = fmod(atan2(d[1], d[0]), 2 * PF_MYPI);
-    if (az < 0) az += 2 * PF_MYPI;
-    double zen = atan2(sqrt(d[0] * d[0] + d[1] * d[1]), d[2]);
-    float uu = (float)(az / (2 * PF_MYPI)), vv = (float)(zen / PF_MYPI);
-    float sx = uu * (float)pw - 0.5f, sy = vv * (float)ph - 0.5f;
-    int ix = (int)floorf(sx), iy = (int)floorf(sy);
-    float ax = sx - (float)ix, ay = sy - (float)iy;
-    int ix0 = ((ix % pw) + pw) % pw, ix1 = (((ix + 1) % pw) + pw) % pw;
-    int iy0 = ((iy % ph) + ph) % ph, iy1 = (((iy + 1) % ph) + ph) % ph;
-    long long a00 = ((long long)iy0 * pw + ix0) * 3, a01 = ((long long)iy0 * pw + ix1) * 3;
-    long long a10 = ((long long)iy1 * pw + ix0) * 3, a11 = ((long long)iy1 * pw + ix1) * 3;
+    const RgbTap t = taps[geom[p].pix_off + i];
+    const float ax = t.ax, ay = t.ay;
+    const long long ix0 = t.x0y0 & 0xFFFFu, iy0 = t.x0y0 >> 16;
+    const long long ix1 = t.x1y1 & 0xFFFFu, iy1 = t.x1y1 >> 16;
+    long long a00 = (iy0 * pw + ix0) * 3, a01 = (iy0 * pw + ix1) * 3;
+    long long a10 = (iy1 * pw + ix0) * 3, a11 = (iy1 * pw + ix1) * 3;
     for (int b = 0; b < batch; b++) {
         const uint8_t* pp = pano + b * pstride;
         uint8_t* out = tiles + b * tstride + rgb_off[p] + i * 3;
@@ -875,14 +867,12 @@ void launch_d2d_map(hipStream_t s, float* data, long long npx, int c, const floa
                        abcd[2], abcd[3]);
 }
 
-void launch_warp_rgb(hipStream_t s, const RgbCam* cams, const TileGeom* geom, int ntiles,
-                     long long npix_max, const long long* pix_prefix, const long long* rgb_off,
-                     const uint8_t* pano, int pw, int ph, long long pstride, uint8_t* tiles,
-                     long long tstride, int batch)
+void launch_warp_rgb(hipStream_t s, const RgbTap* taps, const TileGeom* geom, int ntiles,
+                     long long npix_max, const long long* rgb_off, const uint8_t* pano, int pw,
+                     int ph, long long pstride, uint8_t* tiles, long long tstride, int batch)
 {
-    (void)pix_prefix;
     dim3 grid(nblocks(npix_max), ntiles);
-    hipLaunchKernelGGL(k_warp_rgb, grid, dim3(kBlock), 0, s, cams, geom, rgb_off, pano, pw, ph,
+    hipLaunchKernelGGL(k_warp_rgb, grid, dim3(kBlock), 0, s, taps, geom, rgb_off, pano, pw, ph,
                        pstride, tiles, tstride, batch);
 }
 

@@ -3,10 +3,11 @@
 // For every tile pixel (X, Y) the reference mapping is ToSphericalCoord (Depth.cpp:157-166):
 // corner0 + hedge*x + vedge*y -> WorldToSpherical (Depth.cpp:2960-2971) -> a bilinear sample of
 // the panorama at ValueAtCoord's pixel convention (az/2pi*(pw-1), zen/pi*(ph-1)).  That mapping
-// depends only on the layout and the panorama size, so it is evaluated once (three small
-// passes, cached by the context) and the per-call kernel does no trigonometry:
+// depends only on the layout and the panorama size, so it is evaluated once (cached by the
+// context) and the per-call kernel does no trigonometry:
 //
-//  1. k_warp_coords: per tile pixel the bilinear corner (x0, y0) and weights (fx, fy).
+//  1. warp_coords_host: per tile pixel the bilinear corner (x0, y0) and weights (fx, fy), on the
+//                    host with glibc atan2f as the reference calls it (bit-exact maps).
 //  2. k_patch_box:   tiles are cut into 32x32-pixel patches; per patch the panorama footprint
 //                    (an azimuth-unwrapped box, <= kCap floats, or "wide").
 //  3. k_warp_local:  per tile pixel the corner's index inside its patch's footprint box (or the
@@ -22,10 +23,14 @@
 // when px == pw-1 exactly (az < 2*MYPI), i.e. fx == 0, and likewise y0 == ph-1 means fy == 0; the
 // neighbour's weight is then exactly zero, so the box may hold any finite value there (the box
 // wraps in azimuth and clamps rows).  Inputs are depth maps, finite by contract.
+#include "pf_geom.hpp"
 #include "pf_internal.hpp"
 
+#include <algorithm>
 #include <cfloat>
+#include <thread>
 #include <type_traits>
+#include <vector>
 
 namespace pf {
 
@@ -96,37 +101,6 @@ static constexpr int kNB = PF_WARP_BATCH;               // panoramas per block
 #define PF_WARP_ROWPX 0  // a thread's pixels consecutive in one row: one 16-B store per panorama
 #endif
 
-__device__ __forceinline__ void world_to_sph(float p0, float p1, float p2, float& az,
-                                             float& zen)
-{  // Depth.cpp:2960-2971, Imath normalize/length; atan2 evaluated in fp64 and rounded
-    float l2 = p0 * p0 + p1 * p1 + p2 * p2;
-    float l;
-    if (l2 < 2.0f * FLT_MIN) {
-        float ax = fabsf(p0), ay = fabsf(p1), az_ = fabsf(p2);
-        float mx = ax;
-        if (mx < ay) mx = ay;
-        if (mx < az_) mx = az_;
-        if (mx == 0.0f) l = 0.0f;
-        else { ax /= mx; ay /= mx; az_ /= mx; l = mx * sqrtf(ax * ax + ay * ay + az_ * az_); }
-    } else
-        l = sqrtf(l2);
-    if (l != 0.0f) { p0 /= l; p1 /= l; p2 /= l; }
-    float a = (float)atan2((double)p1, (double)p0);
-    float azf = (float)fmod((double)a, 2 * PF_MYPI);
-    if (azf < 0) azf = (float)((double)azf + 2 * PF_MYPI);
-    float q2 = p0 * p0 + p1 * p1;
-    float ql;
-    if (q2 < 2.0f * FLT_MIN) {
-        float ax = fabsf(p0), ay = fabsf(p1);
-        float mx = ax < ay ? ay : ax;
-        if (mx == 0.0f) ql = 0.0f;
-        else { ax /= mx; ay /= mx; ql = mx * sqrtf(ax * ax + ay * ay); }
-    } else
-        ql = sqrtf(q2);
-    az = azf;
-    zen = (float)atan2((double)ql, (double)p2);
-}
-
 __device__ __forceinline__ uint32_t mix32(uint32_t x)
 {  // lowbias32 finaliser (the oracle's pfo_hash32)
     x ^= x >> 16;
@@ -137,33 +111,84 @@ __device__ __forceinline__ uint32_t mix32(uint32_t x)
     return x;
 }
 
-// Pass 1: bilinear corner and weights of every tile pixel; wxy = x0 | y0 << 16.
-__global__ void __launch_bounds__(kWB) k_warp_coords(const TileGeom* __restrict__ geom, int pw,
-                                                     int ph, uint32_t* __restrict__ wxy,
-                                                     float2* __restrict__ wfxy)
+// Pass 1 (host, once per layout and panorama size): bilinear corner and weights of every tile
+// pixel, wxy = x0 | y0 << 16.  Evaluated on the host with glibc's atan2f -- the function the
+// reference's WorldToSpherical calls (Depth.cpp:2960-2971) -- through pf_geom.hpp's Imath-order
+// ToSphericalCoord (Depth.cpp:157-166), so the corner indices and weights are the reference's
+// bits (glibc atan2f is not correctly rounded: 16% of its results differ from a rounded fp64
+// evaluation, which is what device code would give).  Rows are split over host threads.
+template <class F>
+static void host_rows(int h, F&& f)
 {
-    const int p = blockIdx.y;
-    const TileGeom g = geom[p];
-    long long npx = (long long)g.w * g.h;
-    long long i = (long long)blockIdx.x * kWB + threadIdx.x;
-    if (i >= npx) return;
-    int Y = (int)(i / g.w), X = (int)(i - (long long)Y * g.w);
-    float xf = (float)X / (float)(g.w - 1), yf = (float)Y / (float)(g.h - 1);
-    float q0 = g.corner0[0] + g.hedge[0] * xf, q1 = g.corner0[1] + g.hedge[1] * xf,
-          q2 = g.corner0[2] + g.hedge[2] * xf;
-    q0 = q0 + g.vedge[0] * yf; q1 = q1 + g.vedge[1] * yf; q2 = q2 + g.vedge[2] * yf;
-    float az, zen;
-    world_to_sph(q0, q1, q2, az, zen);
-    float px = (float)((double)az / (2 * PF_MYPI) * (double)(pw - 1));
-    float py = (float)((double)zen / PF_MYPI * (double)(ph - 1));
-    int x0 = (int)floorf(px), y0 = (int)floorf(py);
-    float fx = px - (float)x0, fy = py - (float)y0;
-    if (x0 < 0) { x0 = 0; fx = 0; }
-    if (y0 < 0) { y0 = 0; fy = 0; }
-    if (x0 > pw - 1) { x0 = pw - 1; fx = 0; }
-    if (y0 > ph - 1) { y0 = ph - 1; fy = 0; }
-    wxy[g.pix_off + i] = (uint32_t)x0 | ((uint32_t)y0 << 16);
-    wfxy[g.pix_off + i] = make_float2(fx, fy);
+    unsigned nt = std::thread::hardware_concurrency();
+    nt = nt < 1 ? 1 : (nt > 16 ? 16 : nt);  // the GPU box grants 16 host CPUs per GPU
+    if ((long long)h * 64 < 4096 || nt == 1) {
+        f(0, h);
+        return;
+    }
+    std::vector<std::thread> th;
+    const int per = (h + (int)nt - 1) / (int)nt;
+    for (int y0 = 0; y0 < h; y0 += per) th.emplace_back(f, y0, std::min(h, y0 + per));
+    for (auto& t : th) t.join();
+}
+
+void warp_coords_host(const TileGeom& g, int pw, int ph, uint32_t* wxy, float* wfxy)
+{
+    pfgeom::Window win{};
+    win.corner0 = {g.corner0[0], g.corner0[1], g.corner0[2]};
+    win.hedge = {g.hedge[0], g.hedge[1], g.hedge[2]};
+    win.vedge = {g.vedge[0], g.vedge[1], g.vedge[2]};
+    host_rows(g.h, [&](int ya, int yb) {
+        for (int Y = ya; Y < yb; Y++)
+            for (int X = 0; X < g.w; X++) {
+                const float xf = (float)X / (float)(g.w - 1), yf = (float)Y / (float)(g.h - 1);
+                float az, zen;
+                pfgeom::to_spherical_coord(win, xf, yf, az, zen);
+                const float px = (float)((double)az / (2 * PF_MYPI) * (double)(pw - 1));
+                const float py = (float)((double)zen / PF_MYPI * (double)(ph - 1));
+                int x0 = (int)floorf(px), y0 = (int)floorf(py);
+                float fx = px - (float)x0, fy = py - (float)y0;
+                if (x0 < 0) { x0 = 0; fx = 0; }
+                if (y0 < 0) { y0 = 0; fy = 0; }
+                if (x0 > pw - 1) { x0 = pw - 1; fx = 0; }
+                if (y0 > ph - 1) { y0 = ph - 1; fy = 0; }
+                const long long i = (long long)Y * g.w + X;
+                wxy[i] = (uint32_t)x0 | ((uint32_t)y0 << 16);
+                wfxy[2 * i] = fx;
+                wfxy[2 * i + 1] = fy;
+            }
+    });
+}
+
+// The RGB warp's texel taps (row f4 / a18): the GL camera ray of pixel centre (i, r)
+// (SaveCubeMap, Main.cpp:246-269) -> the exact sphere texcoord (fs_perspective.txt:67-73) ->
+// GL_LINEAR + GL_REPEAT corners and weights, in double with glibc atan2/sqrt/fmod as the oracle
+// (pfo_warp_rgb) evaluates them; once per layout and panorama size.
+void rgb_taps_host(const RgbCam& cam, int W, int H, int pw, int ph, RgbTap* taps)
+{
+    host_rows(H, [&](int ra, int rb) {
+        for (int r = ra; r < rb; r++)
+            for (int i = 0; i < W; i++) {
+                const double xn = 2.0 * (i + 0.5) / W - 1.0, yn = 1.0 - 2.0 * (r + 0.5) / H;
+                double d[3];
+                for (int k = 0; k < 3; k++)
+                    d[k] = cam.f[k] + cam.s[k] * (xn * cam.tx) + cam.u[k] * (yn * cam.ty);
+                double az = fmod(atan2(d[1], d[0]), 2 * PF_MYPI);
+                if (az < 0) az += 2 * PF_MYPI;
+                const double zen = atan2(sqrt(d[0] * d[0] + d[1] * d[1]), d[2]);
+                const float uu = (float)(az / (2 * PF_MYPI)), vv = (float)(zen / PF_MYPI);
+                const float sx = uu * (float)pw - 0.5f, sy = vv * (float)ph - 0.5f;
+                const int ix = (int)floorf(sx), iy = (int)floorf(sy);
+                RgbTap t;
+                t.ax = sx - (float)ix;
+                t.ay = sy - (float)iy;
+                const int ix0 = ((ix % pw) + pw) % pw, ix1 = (((ix + 1) % pw) + pw) % pw;
+                const int iy0 = ((iy % ph) + ph) % ph, iy1 = (((iy + 1) % ph) + ph) % ph;
+                t.x0y0 = (uint32_t)ix0 | ((uint32_t)iy0 << 16);
+                t.x1y1 = (uint32_t)ix1 | ((uint32_t)iy1 << 16);
+                taps[(long long)r * W + i] = t;
+            }
+    });
 }
 
 __device__ __forceinline__ int patch_pixel(const WarpPatch& P, const TileGeom& g, int t, int k,
@@ -821,12 +846,9 @@ __global__ void __launch_bounds__(kWB) k_warp_wave(const TileGeom* __restrict__ 
 #endif
 
 // ---------------------------------------------------------------------------------------------
-void launch_warp_prepare(hipStream_t s, const TileGeom* geom, int ntiles, long long npix_max,
-                         WarpPatch* patches, int npatch, int pw, int ph, uint32_t* wloc,
-                         float* wfxy)
+void launch_warp_boxes(hipStream_t s, const TileGeom* geom, WarpPatch* patches, int npatch,
+                       int pw, int ph, uint32_t* wloc)
 {
-    dim3 g1((unsigned)((npix_max + kWB - 1) / kWB), ntiles);
-    hipLaunchKernelGGL(k_warp_coords, g1, dim3(kWB), 0, s, geom, pw, ph, wloc, (float2*)wfxy);
     hipLaunchKernelGGL(k_patch_box, dim3(npatch), dim3(kWB), 0, s, geom, patches, pw,
                        (const uint32_t*)wloc);
     hipLaunchKernelGGL(k_warp_local, dim3(npatch), dim3(kWB), 0, s, geom,

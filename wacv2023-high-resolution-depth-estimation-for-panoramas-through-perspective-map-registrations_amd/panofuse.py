@@ -17,6 +17,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("PANOFUSE_LIB") or os.path.join(HERE, "lib", "libpanofuse.so")
 
 PF_OK, PF_EINVAL, PF_ENOMEM, PF_EHIP, PF_ESTATE, PF_EDEGENERATE = 0, -1, -2, -3, -4, -5
+PF_ETIMEOUT = -6  # a resident-kernel hand-off wait timed out: that fusion's output is invalid
 
 # Every symbol declared in include/panofuse.h.
 EXPORTS = [
@@ -27,7 +28,8 @@ EXPORTS = [
     "pf_depth_transform", "pf_register_joint", "pf_set_solver", "pf_fuse_normalize",
     "pf_fuse_border", "pf_fuse_band_plan", "pf_fuse_band_pass", "pf_fuse_multicover",
     "pf_fuse_multicover_patch", "pf_solve_smoothing", "pf_set_metrics_order",
-    "pf_jres_errors", "pf_set_jacobi_engine", "pf_stream_wait_level",
+    "pf_jres_errors", "pf_set_jacobi_engine", "pf_stream_wait_level", "pf_debug_jres_fault",
+    "pf_probe_warp_coords", "pf_probe_rgb_taps",
 ]
 METRICS_ORDERS = {"tree": 0, "sequential": 1}  # PF_METRICS_*; "sequential" = the reference's
 SOLVERS = {"normal": 0, "lm": 1}  # PF_SOLVER_*; "lm" = the reference's Ceres LM (default)
@@ -101,6 +103,9 @@ def load():
                                     ip, ip, ip, ip]
     L.pf_profile_enable.argtypes = [vp, ip]
     L.pf_jres_errors.argtypes = [vp]
+    L.pf_debug_jres_fault.argtypes = [vp, ip]
+    L.pf_probe_warp_coords.argtypes = [C.POINTER(Window), ip, ip, ip, ip, vp, vp]
+    L.pf_probe_rgb_taps.argtypes = [C.POINTER(Window), ip, ip, ip, ip, vp]
     L.pf_set_jacobi_engine.argtypes = [vp, ip, ip]
     L.pf_stream_wait_level.argtypes = [vp, ip, vp]
     L.pf_profile_read.argtypes = [vp, C.POINTER(C.c_double), C.POINTER(C.c_double),
@@ -367,6 +372,8 @@ class Fuser:
         return {STAGES[i]: (ms[i], by[i], ln[i]) for i in range(n)}
 
     def synchronize(self):
+        """Wait for the context stream; raises PanofuseError(PF_ETIMEOUT) if a fusion enqueued
+        since the last report had a resident-kernel wait time out (its output is invalid)."""
         self._check(self.L.pf_synchronize(self.h))
 
     def stream_wait_level(self, level, stream):
@@ -385,6 +392,34 @@ class Fuser:
         if n < 0:
             self._check(n)
         return n
+
+    def debug_jres_fault(self, spin_log2=10):
+        """Test hook: the next resident launch withholds row block 0's hand-off flag with waits
+        bounded at 2^spin_log2 polls, so that fusion must report PF_ETIMEOUT."""
+        self._check(self.L.pf_debug_jres_fault(self.h, int(spin_log2)))
+
+
+def warp_coords(fov, tile_w, tile_h, pw, ph):
+    """The depth warp's cached map of one tile (host code, no GPU): (wxy uint32 [h*w] =
+    x0 | y0 << 16, wfxy float32 [h*w, 2] = (fx, fy))."""
+    n = int(tile_w) * int(tile_h)
+    wxy = np.zeros(n, np.uint32)
+    wf = np.zeros((n, 2), np.float32)
+    rc = load().pf_probe_warp_coords(C.byref(Window(*map(float, fov))), int(tile_w), int(tile_h),
+                                     int(pw), int(ph), wxy.ctypes.data, wf.ctypes.data)
+    if rc != PF_OK:
+        raise PanofuseError(rc, "pf_probe_warp_coords")
+    return wxy, wf
+
+
+def rgb_taps(fov, tile_w, tile_h, pw, ph):
+    """The RGB warp's cached tap map of one tile (host code, no GPU): uint32 [h*w, 4]."""
+    taps = np.zeros((int(tile_w) * int(tile_h), 4), np.uint32)
+    rc = load().pf_probe_rgb_taps(C.byref(Window(*map(float, fov))), int(tile_w), int(tile_h),
+                                  int(pw), int(ph), taps.ctypes.data)
+    if rc != PF_OK:
+        raise PanofuseError(rc, "pf_probe_rgb_taps")
+    return taps
 
 
 def make_responses(params, device):
