@@ -33,7 +33,7 @@ def _port():
 
 def _launch(args, timeout=600):
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
-           "--master-addr", "127.0.0.1", "--master-port", str(_port()), "bench.py",
+           "--master-addr", "127.0.0.1", "--master-port", str(_port()), "bench.py", "--gpus", "2",
            "--backend", "gloo", "--same-device", "--no-cpu-baseline", "--no-extra-configs"] + args
     r = subprocess.run(cmd, cwd=ROOT, capture_output=True, text=True, timeout=timeout)
     assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]

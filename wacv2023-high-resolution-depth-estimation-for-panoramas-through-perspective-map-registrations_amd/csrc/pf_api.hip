@@ -46,6 +46,9 @@ struct LevelCache {
     // tap-grid points of each level (one tile texel gathered per point): the targets stage's
     // algorithmic read count
     long long taps[4] = {0, 0, 0, 0};
+    // the one-launch targets of every level (k_targets_multi): (level, patch) gather order
+    DevBuf tgt_order;
+    int tgt_nentries = 0;
 };
 
 }  // namespace
@@ -94,10 +97,10 @@ struct pf_ctx {
     DevBuf jres_x, jres_sync;
     uint32_t jres_tk = 0, jres_fb = 1;
     int jres_mode = -1, jres_nb = 0;  // pf_set_jacobi_engine (-1: not set, PF_JRES decides)
-    // timeout reporting: after every resident launch the error word is copied (stream-ordered)
-    // into pinned host memory; a count above jres_err_seen is reported once as PF_ETIMEOUT
+    // timeout reporting: a resident launch whose wait times out also raises this flag in
+    // coherent pinned host memory (a system-scope store from the kernel, no extra stream work);
+    // jres_check reports a raised flag once as PF_ETIMEOUT and lowers it
     uint32_t* jres_err_h = nullptr;
-    uint32_t jres_err_seen = 0;
     int jres_fault = 0;  // pf_debug_jres_fault: spin_log2 for the next resident launch (0: off)
     int seed_key[5] = {0, 0, 0, 0, 0};
     // stage profiling
@@ -352,6 +355,7 @@ void pf_destroy(pf_ctx* c)
         release(c->lc.hcol[l]);
         release(c->lc.mcpairs[l]);
     }
+    release(c->lc.tgt_order);
 
     for (auto& s : c->spans) {
         (void)hipEventDestroy(s.a);
@@ -391,13 +395,11 @@ int pf_set_jacobi_engine(pf_ctx* c, int mode, int row_blocks)
 // reached the host (the copy queued behind each resident launch); never blocks.
 static int jres_check(pf_ctx* c)
 {
-    if (!c->jres_err_h) return PF_OK;
-    const uint32_t n = __atomic_load_n(c->jres_err_h, __ATOMIC_ACQUIRE) & 0x7FFFFFFFu;
-    if (n == c->jres_err_seen) return PF_OK;
-    const uint32_t d = n - c->jres_err_seen;
-    c->jres_err_seen = n;
-    return fail(c, PF_ETIMEOUT, "resident Jacobi kernel: %u hand-off wait(s) timed out; the "
-                "fused output of that call is invalid", d);
+    if (!c->jres_err_h || !__atomic_load_n(c->jres_err_h, __ATOMIC_ACQUIRE)) return PF_OK;
+    __atomic_store_n(c->jres_err_h, 0u, __ATOMIC_RELEASE);
+    return fail(c, PF_ETIMEOUT, "resident Jacobi kernel: hand-off wait(s) timed out (%d so far "
+                "on this context, pf_jres_errors); the fused output of that call is invalid",
+                pf_jres_errors(c));
 }
 
 int pf_debug_jres_fault(pf_ctx* c, int spin_log2)
@@ -763,6 +765,27 @@ static int prepare_levels(pf_ctx* c, int out_w, int out_h, float zr0, float zr1)
                       (const GridRow*)lc.rows[l].p, (int32_t*)lc.tapmap[l].p);
         HIPCHK(c, hipGetLastError());
     }
+    {
+        // gather order of k_targets_multi: zenith bands = the coarsest level's patch rows; per
+        // band the finest level's patches first, then each coarser level's patches of that band
+        const int pw_ = targets_patch_w(), ph_ = targets_patch_h();
+        int npy[4], npx[4];
+        for (int l = 0; l < nl; l++) {
+            npx[l] = (lc.dims[l].w + pw_ - 1) / pw_;
+            npy[l] = (lc.dims[l].h1 - lc.dims[l].h0 + 1 + ph_ - 1) / ph_;
+        }
+        std::vector<int2> order;
+        for (int j = 0; j < npy[0]; j++)
+            for (int l = nl - 1; l >= 0; l--)
+                for (int r = 0; r < npy[l]; r++) {
+                    const int band = std::min(npy[0] - 1, (int)((long long)r * npy[0] / npy[l]));
+                    if (band != j) continue;
+                    for (int x = 0; x < npx[l]; x++) order.push_back(make_int2(l, r * npx[l] + x));
+                }
+        int rc;
+        if ((rc = upload(c, lc.tgt_order, order))) return rc;
+        lc.tgt_nentries = (int)order.size();
+    }
     lc.nlevels = nl;
     lc.out_w = out_w;
     lc.out_h = out_h;
@@ -1023,20 +1046,15 @@ static int jres_prepare(pf_ctx* c, const LevelDims& L, int batch, const JresPlan
                       (size_t)jp.K * L.w;
     if ((rc = ensure(c, c->jres_x, xb))) return rc;
     const size_t sb = sizeof(uint32_t) * (2 + (size_t)batch * jp.nb * jres_flags_per_block(jp.K));
-    if (!c->jres_err_h) {
-        HIPCHK(c, hipHostMalloc((void**)&c->jres_err_h, sizeof(uint32_t), hipHostMallocDefault));
-        *c->jres_err_h = 0;
-        c->jres_err_seen = 0;
+    static const bool errhost = !(getenv("PF_JRES_ERRHOST") && atoi(getenv("PF_JRES_ERRHOST")) == 0);
+    if (!c->jres_err_h && errhost) {
+        HIPCHK(c, hipHostMalloc((void**)&c->jres_err_h, sizeof(uint32_t),
+                                hipHostMallocMapped | hipHostMallocCoherent));
+        __atomic_store_n(c->jres_err_h, 0u, __ATOMIC_RELEASE);
     }
     if (c->jres_sync.bytes < sb) {
-        if (c->jres_sync.p) {  // a new sync block restarts the error count at 0
-            HIPCHK(c, hipStreamSynchronize(c->stream));
-            if ((rc = jres_check(c))) return rc;  // report the old block's last timeouts first
-        }
         if ((rc = ensure(c, c->jres_sync, sb))) return rc;
         HIPCHK(c, hipMemsetAsync(c->jres_sync.p, 0, sb, c->stream));
-        *c->jres_err_h = 0;
-        c->jres_err_seen = 0;
         c->jres_tk = 0;
         c->jres_fb = 1;
     }
@@ -1076,6 +1094,7 @@ static float* run_jacobi(pf_ctx* c, const LevelDims& L, int first, const float* 
         A.ticket = sync;
         A.err = sync + 1;
         A.flags = sync + 2;
+        A.err_host = c->jres_err_h;  // mapped + coherent: the device pointer is the host one
         static const int dbg = getenv("PF_JRES_DBG") ? atoi(getenv("PF_JRES_DBG")) : 0;
         A.dbg = dbg;
         A.spin_log2 = 24;
@@ -1094,9 +1113,6 @@ static float* run_jacobi(pf_ctx* c, const LevelDims& L, int first, const float* 
                     L.w, L.h, L.h1 - L.h0 + 1, L.iters, batch, jp->nb, jp->core, jp->K, jp->rounds);
         launch_jres(c->stream, A);
         // the error word, stream-ordered into pinned memory: jres_check reports it
-        if (c->jres_err_h)
-            (void)hipMemcpyAsync(c->jres_err_h, A.err, sizeof(uint32_t), hipMemcpyDeviceToHost,
-                                 c->stream);
         if (npasses) *npasses = 1;
         return dst;
     }
@@ -1243,7 +1259,33 @@ static int fuse_range(pf_ctx* c, const float* emap, int ew, int eh, int ec, cons
                                (const int32_t*)lc.tapmap[l].p, tiles, c->tile_elems, coeffs, L,
                                lnl[l], st, batch);
     };
-    const bool side = !c->prof_on && !noside && lc.nlevels > 1;
+    // PF_TGT_MULTI=0: the per-level target launches (levels 1+ on the side stream) -- A/B runs
+    static const bool multi = !(getenv("PF_TGT_MULTI") && atoi(getenv("PF_TGT_MULTI")) == 0) &&
+                              !naive && !(getenv("PF_TARGETS"));
+    if (multi) {
+        TgtMulti M{};
+        M.nlev = lc.nlevels;
+        M.nentries = lc.tgt_nentries;
+        const int pw_ = targets_patch_w(), ph_ = targets_patch_h();
+        double bytes = 0;
+        for (int l = 0; l < lc.nlevels; l++) {
+            const LevelDims& L = lc.dims[l];
+            TgtLevel& T = M.lv[l];
+            T.L = L;
+            T.box = (const TileBox*)lc.box[l].p;
+            T.tb = (const TapBox*)lc.tapbox[l].p;
+            T.map = (const int32_t*)lc.tapmap[l].p;
+            T.lnorm = lnl[l];
+            T.lstride = (long long)L.w * L.h;
+            T.npx = (L.w + pw_ - 1) / pw_;
+            T.npy = (L.h1 - L.h0 + 1 + ph_ - 1) / ph_;
+            bytes += (double)batch * (4.0 * L.w * (L.h1 - L.h0 + 1) + 4.0 * (double)lc.taps[l]);
+        }
+        StageTimer t(c, PF_STAGE_TARGETS, bytes, 1);
+        launch_targets_multi(c->stream, (const TileGeom*)c->geom.p, c->ntiles, tiles,
+                             c->tile_elems, coeffs, M, (const int2*)lc.tgt_order.p, batch);
+    }
+    const bool side = !multi && !c->prof_on && !noside && lc.nlevels > 1;
     if (side) {
         int rc;
         if ((rc = ensure_aux(c))) return rc;
@@ -1273,7 +1315,9 @@ static int fuse_range(pf_ctx* c, const float* emap, int ew, int eh, int ec, cons
         const GridCol* cols = (const GridCol*)lc.cols[l].p;
         const GridRow* rows = (const GridRow*)lc.rows[l].p;
         float* const lnorm_l = lnl[l];
-        if (side && l > 0) {
+        if (multi) {
+            // gathered above, for every level
+        } else if (side && l > 0) {
             HIPCHK(c, hipStreamWaitEvent(c->stream, c->ev_tgt[l], 0));
         } else {
             // algorithmic bytes: one 4-B tile texel per tap-grid point (k_targets_patch gathers

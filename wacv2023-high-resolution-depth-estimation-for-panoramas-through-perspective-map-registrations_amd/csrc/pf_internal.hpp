@@ -187,6 +187,7 @@ struct JresArgs {
     uint32_t* flags;       // [batch][nb] last round published (monotone across launches)
     uint32_t* ticket;      // workgroup ticket counter (monotone across launches)
     uint32_t* err;         // spin timeouts (pf_jres_errors)
+    uint32_t* err_host;    // raised (system-scope store) on any timeout: coherent pinned memory
     uint32_t tbase, fbase; // this launch's first ticket / flag base
     int dbg;               // profiling only (wrong results): 1 no hand-offs, 4 no rows, 8 no
                            // barriers; 16 (pf_debug_jres_fault): row block 0 withholds its flag
@@ -211,6 +212,27 @@ void launch_targets_patch(hipStream_t s, const TileGeom* geom, const TileBox* bo
                           const TapBox* tb, int ntiles, const int32_t* map, const float* tiles,
                           long long tstride, const float* coeffs, LevelDims L, float* lnorm,
                           long long lstride, int batch);
+// All levels' targets in one launch (pf_targets.hip): per level its tables and plane, and a host
+// table of (level, patch) entries in gather order (fuse_range builds it once per level set).
+struct TgtLevel {
+    LevelDims L;
+    const TileBox* box;
+    const TapBox* tb;
+    const int32_t* map;
+    float* lnorm;
+    long long lstride;
+    int npx, npy;
+};
+struct TgtMulti {
+    TgtLevel lv[4];
+    int nlev, nentries;
+};
+int targets_patch_w();
+int targets_patch_h();
+int targets_batch();
+void launch_targets_multi(hipStream_t s, const TileGeom* geom, int ntiles, const float* tiles,
+                          long long tstride, const float* coeffs, const TgtMulti& M,
+                          const int2* order, int batch);
 bool jstream_supported_T(int T);
 int jstream_waves_per_cu(int C, int T, bool fast);
 bool jstream_supported_C(int C, bool fast);

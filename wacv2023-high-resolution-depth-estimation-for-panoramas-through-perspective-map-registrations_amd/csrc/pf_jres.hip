@@ -86,6 +86,14 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc(const void* base, uint32_
 
 }  // namespace
 
+// A bounded wait gave up: count it on the device (pf_jres_errors) and raise the host's flag
+// (coherent pinned memory; the host reports PF_ETIMEOUT).  Only on the failure path.
+__device__ __forceinline__ void jres_timeout(const JresArgs& A)
+{
+    __hip_atomic_fetch_add(A.err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (A.err_host) __hip_atomic_store(A.err_host, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
 template <int CPL, int RS, int NWV, int SRC, bool OUT16>
 struct JRes {
     static constexpr int NP = CPL / 2;  // column pairs per lane
@@ -278,7 +286,7 @@ __global__ void __launch_bounds__(64 * NWV) k_jres(JresArgs A)
         while (*reinterpret_cast<volatile int*>(&eflag[nbw]) < st) {
             __builtin_amdgcn_s_sleep(0);
             if (++spins > (1 << 26)) {
-                if (lane == 0) __hip_atomic_fetch_add(A.err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                if (lane == 0) jres_timeout(A);
                 break;
             }
         }
@@ -382,7 +390,7 @@ __global__ void __launch_bounds__(64 * NWV) k_jres(JresArgs A)
                 if (__builtin_amdgcn_ballot_w64(!ok) == 0) break;
                 __builtin_amdgcn_s_sleep(1);
                 if (++spins > (1 << A.spin_log2)) {
-                    if (lane == 0) __hip_atomic_fetch_add(A.err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    if (lane == 0) jres_timeout(A);
                     break;
                 }
             }
@@ -491,7 +499,7 @@ __global__ void __launch_bounds__(64 * NWV) k_jres(JresArgs A)
                     if (__builtin_amdgcn_ballot_w64(!ok) == 0) break;  // every lane's granules current
                     __builtin_amdgcn_s_sleep(1);
                     if (++spins > (1 << (A.spin_log2 - 2))) {  // bounded: counted, never hangs
-                        if (lane == 0) __hip_atomic_fetch_add(A.err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                        if (lane == 0) jres_timeout(A);
                         break;
                     }
                 }
@@ -536,7 +544,7 @@ __global__ void __launch_bounds__(64 * NWV) k_jres(JresArgs A)
                 while ((int)(__hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) - want) < 0) {
                     __builtin_amdgcn_s_sleep(2);
                     if (++spins > (1 << A.spin_log2)) {
-                        __hip_atomic_fetch_add(A.err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                        jres_timeout(A);
                         break;
                     }
                 }

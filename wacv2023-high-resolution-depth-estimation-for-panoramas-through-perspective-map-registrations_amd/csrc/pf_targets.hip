@@ -160,22 +160,18 @@ __device__ __forceinline__ bool box_meets(const TileBox& bx, int X0, int X1, int
     return lo <= hi && hi >= X0 && lo <= X1;
 }
 
+// One block's work: patch `pid` of level L for panoramas [bgrp*kTNB, +kTNB).
 template <bool XFORM>
-__global__ void __launch_bounds__(256) k_targets_patch(const TileGeom* __restrict__ geom,
-                                                       const TileBox* __restrict__ box,
-                                                       const TapBox* __restrict__ tb, int ntiles,
-                                                       const int32_t* __restrict__ map,
-                                                       const float* __restrict__ tiles,
-                                                       long long tstride,
-                                                       const float* __restrict__ coeffs,
-                                                       LevelDims L, int npx, int npatch,
-                                                       float* __restrict__ lnorm,
-                                                       long long lstride, int batch)
+__device__ __forceinline__ void targets_patch(const TileGeom* __restrict__ geom,
+                                              const TileBox* __restrict__ box,
+                                              const TapBox* __restrict__ tb, int ntiles,
+                                              const int32_t* __restrict__ map,
+                                              const float* __restrict__ tiles, long long tstride,
+                                              const float* __restrict__ coeffs, const LevelDims& L,
+                                              int npx, int pid, int bgrp,
+                                              float* __restrict__ lnorm, long long lstride,
+                                              int batch, float (*sv)[kTG])
 {
-    __shared__ float sv[kTNB][kTG];
-    // XCD-contiguous runs of patches (neighbouring patches read the same tile lines)
-    const unsigned lb = xcd_remap(blockIdx.x, gridDim.x);
-    const int pid = (int)(lb % (unsigned)npatch), bgrp = (int)(lb / (unsigned)npatch);
     const int X0 = (pid % npx) * kTPW, Y0 = L.h0 + (pid / npx) * kTPH;
     const int t = threadIdx.x;
     const int X = X0 + (t & (kTPW - 1));
@@ -266,6 +262,68 @@ __global__ void __launch_bounds__(256) k_targets_patch(const TileGeom* __restric
             else lnorm[b * lstride + o] = out;
         }
     }
+}
+
+template <bool XFORM>
+__global__ void __launch_bounds__(256) k_targets_patch(const TileGeom* __restrict__ geom,
+                                                       const TileBox* __restrict__ box,
+                                                       const TapBox* __restrict__ tb, int ntiles,
+                                                       const int32_t* __restrict__ map,
+                                                       const float* __restrict__ tiles,
+                                                       long long tstride,
+                                                       const float* __restrict__ coeffs,
+                                                       LevelDims L, int npx, int npatch,
+                                                       float* __restrict__ lnorm,
+                                                       long long lstride, int batch)
+{
+    __shared__ float sv[kTNB][kTG];
+    // XCD-contiguous runs of patches (neighbouring patches read the same tile lines)
+    const unsigned lb = xcd_remap(blockIdx.x, gridDim.x);
+    const int pid = (int)(lb % (unsigned)npatch), bgrp = (int)(lb / (unsigned)npatch);
+    targets_patch<XFORM>(geom, box, tb, ntiles, map, tiles, tstride, coeffs, L, npx, pid, bgrp,
+                         lnorm, lstride, batch, sv);
+}
+
+// Every level's targets in ONE launch (round 4).  The per-level launches each streamed the
+// tiles' lines from HBM: the coarse levels sample the same tile areas as the finest one, so the
+// stage moved ~2x the tile bytes the finest level needs.  Here the blocks of all levels are
+// ordered so that one region of the sphere is gathered at every level within a short window:
+// per panorama group, the coarsest level's patch rows define zenith bands, and band by band the
+// finest level's patches come first, then each coarser level's patches of the same band (a host
+// table of (level, patch) entries).  The XCD-contiguous mapping gives every XCD a contiguous run
+// of the table, so a band's lines are re-read from its L2 / the MALL instead of HBM.
+template <bool XFORM>
+__global__ void __launch_bounds__(256) k_targets_multi(const TileGeom* __restrict__ geom,
+                                                       int ntiles, const float* __restrict__ tiles,
+                                                       long long tstride,
+                                                       const float* __restrict__ coeffs,
+                                                       TgtMulti M, const int2* __restrict__ order,
+                                                       int batch)
+{
+    __shared__ float sv[kTNB][kTG];
+    const unsigned lb = xcd_remap(blockIdx.x, gridDim.x);
+    const int e = (int)(lb % (unsigned)M.nentries), bgrp = (int)(lb / (unsigned)M.nentries);
+    const int2 ent = order[e];  // (level, patch)
+    const TgtLevel& T = M.lv[ent.x];
+    targets_patch<XFORM>(geom, T.box, T.tb, ntiles, T.map, tiles, tstride, coeffs, T.L, T.npx,
+                         ent.y, bgrp, T.lnorm, T.lstride, batch, sv);
+}
+
+int targets_patch_w() { return kTPW; }
+int targets_patch_h() { return kTPH; }
+int targets_batch() { return kTNB; }
+
+void launch_targets_multi(hipStream_t s, const TileGeom* geom, int ntiles, const float* tiles,
+                          long long tstride, const float* coeffs, const TgtMulti& M,
+                          const int2* order, int batch)
+{
+    const long long nblk = (long long)M.nentries * ((batch + kTNB - 1) / kTNB);
+    if (coeffs)
+        hipLaunchKernelGGL(k_targets_multi<true>, dim3((unsigned)nblk), dim3(256), 0, s, geom,
+                           ntiles, tiles, tstride, coeffs, M, order, batch);
+    else
+        hipLaunchKernelGGL(k_targets_multi<false>, dim3((unsigned)nblk), dim3(256), 0, s, geom,
+                           ntiles, tiles, tstride, coeffs, M, order, batch);
 }
 
 void launch_targets_patch(hipStream_t s, const TileGeom* geom, const TileBox* box,

@@ -31,6 +31,7 @@ EXPORTS = [
     "pf_jres_errors", "pf_set_jacobi_engine", "pf_stream_wait_level", "pf_debug_jres_fault",
     "pf_probe_warp_coords", "pf_probe_rgb_taps",
 ]
+NEW_R4 = {"pf_debug_jres_fault", "pf_probe_warp_coords", "pf_probe_rgb_taps"}
 METRICS_ORDERS = {"tree": 0, "sequential": 1}  # PF_METRICS_*; "sequential" = the reference's
 SOLVERS = {"normal": 0, "lm": 1}  # PF_SOLVER_*; "lm" = the reference's Ceres LM (default)
 
@@ -103,15 +104,19 @@ def load():
                                     ip, ip, ip, ip]
     L.pf_profile_enable.argtypes = [vp, ip]
     L.pf_jres_errors.argtypes = [vp]
-    L.pf_debug_jres_fault.argtypes = [vp, ip]
-    L.pf_probe_warp_coords.argtypes = [C.POINTER(Window), ip, ip, ip, ip, vp, vp]
-    L.pf_probe_rgb_taps.argtypes = [C.POINTER(Window), ip, ip, ip, ip, vp]
+    # (entry points added after round 3: an A/B variant built from older sources may lack them)
+    for name, at in (("pf_debug_jres_fault", [vp, ip]),
+                     ("pf_probe_warp_coords", [C.POINTER(Window), ip, ip, ip, ip, vp, vp]),
+                     ("pf_probe_rgb_taps", [C.POINTER(Window), ip, ip, ip, ip, vp])):
+        if hasattr(L, name):
+            getattr(L, name).argtypes = at
     L.pf_set_jacobi_engine.argtypes = [vp, ip, ip]
     L.pf_stream_wait_level.argtypes = [vp, ip, vp]
     L.pf_profile_read.argtypes = [vp, C.POINTER(C.c_double), C.POINTER(C.c_double),
                                   C.POINTER(C.c_longlong)]
+    variant = os.environ.get("PANOFUSE_LIB") is not None
     for name in EXPORTS:
-        if not hasattr(L, name):
+        if not hasattr(L, name) and not (variant and name in NEW_R4):
             raise RuntimeError(f"libpanofuse.so lacks {name}")
     _lib = L
     return L
