@@ -51,7 +51,7 @@ def parse():
                     help="batch: configs C3/C4 (the headline metric); c5: one 8192x4096 "
                          "panorama, tiles sharded over the ranks")
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
-    ap.add_argument("--prof-steps", type=int, default=2,
+    ap.add_argument("--prof-steps", type=int, default=5,
                     help="extra untimed steps with the per-stage hipEvent timers on (roofline)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-extra-configs", action="store_true",
@@ -537,10 +537,18 @@ def main():
     # Per-kernel roofline: the same steps again with the library's hipEvent stage timers on
     # (recorded on the stream the kernels run on).  With the timers on, the library runs each
     # batch unsplit (no half-batch stream overlap), so every stage's time is its own.
+    # Each step is read on its own and a stage's time is its MEDIAN over the steps: single serial
+    # steps right after the pipelined loop vary by up to ~10 % (the chip's clock after the loop),
+    # the median keeps one slow step out of the roofline.
     fz.profile(True)
-    for _ in range(args.prof_steps):
+    per_step = []
+    for _ in range(max(1, args.prof_steps)):
         step()
-    prof = fz.profile_read()
+        per_step.append(fz.profile_read())
+    nps = len(per_step)
+    prof = {k: (nps * sorted(p[k][0] for p in per_step)[nps // 2],  # median ms x steps
+                sum(p[k][1] for p in per_step), sum(p[k][2] for p in per_step))
+            for k in per_step[0]}
     # Accuracy metrics (ErrorData of each result against its ground truth, median alignment,
     # Depth.cpp:1980-2213): not part of the step (the reference computes them only when a
     # ground-truth file is given), timed the same way on the same batch.

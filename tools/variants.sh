@@ -1,5 +1,6 @@
 #!/bin/bash
-# Build library variants with extra compile flags into lib/variants/ (run here, on the CPU).
+# Build library variants with extra compile flags into lib/variants/ (run here, on the CPU): each
+# variant is the package Makefile run in a scratch copy with HIPFLAGS_EXTRA set.
 # Usage: tools/variants.sh NAME "FLAGS" [NAME "FLAGS" ...]
 set -e
 cd "$(dirname "$0")/.."
@@ -7,13 +8,10 @@ PKG=$(ls -d wacv2023-*_amd)
 mkdir -p $PKG/lib/variants
 while [ $# -ge 2 ]; do
   name=$1; flags=$2; shift 2
-  rm -rf /tmp/pfvar_$name && mkdir -p /tmp/pfvar_$name
-  for f in $PKG/csrc/*.hip; do
-    /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -ffp-contract=off -fno-fast-math \
-      -fhip-fp32-correctly-rounded-divide-sqrt -fno-gpu-flush-denormals-to-zero $flags \
-      -c $f -o /tmp/pfvar_$name/$(basename $f .hip).o &
-  done
-  wait
-  /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o $PKG/lib/variants/libpanofuse_$name.so /tmp/pfvar_$name/*.o
+  W=/tmp/pfvar_$name
+  rm -rf $W && mkdir -p $W/pkg $W/include
+  cp -r $PKG/csrc $PKG/Makefile $W/pkg/ && cp include/*.h $W/include/
+  make -s -j8 -C $W/pkg lib/libpanofuse.so HIPFLAGS_EXTRA="$flags" > $W/build.log 2>&1 || { tail -20 $W/build.log; exit 1; }
+  cp $W/pkg/lib/libpanofuse.so $PKG/lib/variants/libpanofuse_$name.so
   echo "built $name: $flags"
 done
