@@ -84,3 +84,24 @@ def test_smoothing_rejects_stencil_outside(fuser):
     out = torch.zeros((1, out_w // 2, out_w), dtype=torch.int16, device=DEV)
     with pytest.raises(RuntimeError):
         fuser.solve_smoothing(torch.from_numpy(data).to(DEV), out, (0.0, ZR[1]))
+
+
+@pytest.mark.parametrize("nb", ["0", "2", "3", "7", "64"])
+def test_smoothing_row_blocks_equal(fuser, nb, monkeypatch):
+    """The row-band form (k_smooth_band: a panorama's Gauss-Seidel steps spread over nb
+    workgroups with a step hand-off between neighbouring row blocks) equals the one-workgroup
+    form (PF_SMOOTH_BAND=0) bit for bit, for several block counts; then the oracle at one."""
+    lay, tiles, data, out_w = _tiles("C2", 4, 2)
+    fuser.set_tiles(lay)
+    t = torch.from_numpy(data).to(DEV)
+    monkeypatch.setenv("PF_SMOOTH_BAND", "0")
+    ref = torch.zeros((2, out_w // 2, out_w), dtype=torch.int16, device=DEV)
+    fuser.solve_smoothing(t, ref, ZR)
+    monkeypatch.setenv("PF_SMOOTH_BAND", nb)
+    got = torch.zeros_like(ref)
+    fuser.solve_smoothing(t, got, ZR)
+    fuser.synchronize()  # PF_ETIMEOUT if a step hand-off timed out
+    assert torch.equal(got, ref)
+    if nb == "7":
+        r0 = O.solve_smoothing(tiles, np.ascontiguousarray(data[0]), out_w, out_w // 2, ZR)
+        assert np.array_equal(got.cpu().numpy().view(np.uint16)[0], r0)

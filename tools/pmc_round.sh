@@ -6,7 +6,7 @@ set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
 mkdir -p gpurun_out
-ARGS="${PMC_ARGS:---steps 1 --warmup 1 --no-cpu-baseline}"
+ARGS="${PMC_ARGS:---steps 1 --warmup 1 --no-cpu-baseline --no-extra-configs --prof-steps 1}"
 pass() {
   local name=$1; shift
   timeout -k 5 -s KILL 240 rocprofv3 --pmc "$@" -d gpurun_out/pmc_$name -o run --output-format csv -- \

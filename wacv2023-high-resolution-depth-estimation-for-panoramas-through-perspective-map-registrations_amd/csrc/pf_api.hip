@@ -88,7 +88,10 @@ struct pf_ctx {
     // its compacted pixel list (k_smooth_iter_list), cached for one (boxes, size, band) key
     DevBuf sm_list, sm_off;
     std::vector<SmoothBox> sm_key_boxes;
-    int sm_key[4] = {0, 0, 0, 0}, sm_nk = 0, sm_smin = 0, sm_smax = -1;
+    int sm_key[4] = {0, 0, 0, 0}, sm_nk = 0, sm_nb = 0, sm_smin = 0, sm_smax = -1;
+    // row-band smoothing (k_smooth_band): ticket, timeouts, per-block step flags
+    DevBuf sm_sync;
+    uint32_t sm_tk = 0, sm_fb = 1;
     // level-0 seed index tables of the streaming Jacobi (run_jacobi), keyed by level and emap
     DevBuf seed_ecol, seed_erow;
     // resident level kernel (pf_jres.hip): hand-off rows, and the sync words ([0] ticket
@@ -344,7 +347,8 @@ void pf_destroy(pf_ctx* c)
                      &c->buf[0], &c->buf[1], &c->buf[2], &c->lnorm, &c->coeffs, &c->lsum_ws,
                      &c->wmap, &c->wfxy, &c->wpatch, &c->metrics_ws, &c->reg_sums,
                      &c->reg_active, &c->sm_box, &c->sm_cols, &c->sm_rows, &c->sm_src,
-                     &c->sm_mask, &c->seed_ecol, &c->seed_erow, &c->jres_x, &c->jres_sync};
+                     &c->sm_mask, &c->seed_ecol, &c->seed_erow, &c->jres_x, &c->jres_sync,
+                     &c->sm_sync, &c->sm_list, &c->sm_off};
     for (DevBuf* b : all) release(*b);
     for (int l = 0; l < 4; l++) {
         release(c->lc.box[l]);
@@ -397,9 +401,9 @@ static int jres_check(pf_ctx* c)
 {
     if (!c->jres_err_h || !__atomic_load_n(c->jres_err_h, __ATOMIC_ACQUIRE)) return PF_OK;
     __atomic_store_n(c->jres_err_h, 0u, __ATOMIC_RELEASE);
-    return fail(c, PF_ETIMEOUT, "resident Jacobi kernel: hand-off wait(s) timed out (%d so far "
-                "on this context, pf_jres_errors); the fused output of that call is invalid",
-                pf_jres_errors(c));
+    return fail(c, PF_ETIMEOUT, "resident kernel (Jacobi level or row-band smoothing): "
+                "hand-off wait(s) timed out (%d resident-Jacobi timeouts so far on this context, "
+                "pf_jres_errors); the output of that call is invalid", pf_jres_errors(c));
 }
 
 int pf_debug_jres_fault(pf_ctx* c, int spin_log2)
@@ -1544,46 +1548,82 @@ int pf_solve_smoothing(pf_ctx* c, const float* tiles, const float* coeffs, int b
                       (const uint8_t*)c->sm_mask.p, tiles, c->tile_elems, coeffs, out_w, out_h,
                       L.h0, L.h1, iters, (float*)c->buf[0].p, batch);
     } else {
+        // row blocks per panorama (k_smooth_band): a panorama's steps spread over nb CUs;
+        // PF_SMOOTH_BAND=0 keeps one workgroup per panorama (k_smooth_iter_list, nb = 1)
+        const char* be = getenv("PF_SMOOTH_BAND");  // read per call (tests vary it)
+        const int band_mode = be ? atoi(be) : 1;
+        int nb = 1;
+        if (band_mode != 0) {
+            nb = band_mode > 1 ? band_mode : std::max(1, std::min(64, 1024 / batch));
+            nb = std::max(1, std::min(nb, (L.h1 - L.h0 + 1) / 4));
+        }
         const bool same = c->sm_key_boxes.size() == boxes.size() && c->sm_key[0] == out_w &&
                           c->sm_key[1] == out_h && c->sm_key[2] == L.h0 && c->sm_key[3] == L.h1 &&
+                          c->sm_nb == nb &&
                           std::equal(boxes.begin(), boxes.end(), c->sm_key_boxes.begin(),
                                      [](const SmoothBox& a, const SmoothBox& b) {
                                          return a.x0 == b.x0 && a.x1 == b.x1 && a.y0 == b.y0 &&
                                                 a.y1 == b.y1 && a.xs == b.xs;
                                      });
-        if (!same) {  // the band's masked pixels by parity of d = X + Y, sorted by d
+        if (!same) {  // per row block, the masked pixels by parity of d = X + Y, sorted by d
             std::vector<uint8_t> mask(n);
             HIPCHK(c, hipMemcpyAsync(mask.data(), c->sm_mask.p, n, hipMemcpyDeviceToHost,
                                      c->stream));
             HIPCHK(c, hipStreamSynchronize(c->stream));
             const int nk = (out_w + out_h) / 2 + 1;  // d = 2k + p < w + h
-            std::vector<int> cnt(2 * (nk + 1), 0);
+            // row blocks of about equal masked-pixel counts
+            std::vector<long long> rowcnt(out_h, 0);
+            long long total = 0;
+            for (int Y = L.h0; Y <= L.h1; Y++) {
+                for (int X = 1; X <= out_w - 2; X++) rowcnt[Y] += mask[(long long)Y * out_w + X];
+                total += rowcnt[Y];
+            }
+            std::vector<int> blk_of(out_h, 0);
+            {
+                long long acc = 0;
+                int b = 0, rows_in = 0;
+                for (int Y = L.h0; Y <= L.h1; Y++) {
+                    const int rows_left = L.h1 - Y + 1;
+                    if (b < nb - 1 && rows_in > 0 &&
+                        (acc >= total * (b + 1) / nb || rows_left <= nb - 1 - b)) {
+                        b++;
+                        rows_in = 0;
+                    }
+                    blk_of[Y] = b;
+                    acc += rowcnt[Y];
+                    rows_in++;
+                }
+            }
+            const size_t per = (size_t)(nk + 1);
+            std::vector<int> cnt((size_t)nb * 2 * per, 0);
             int dmin = INT32_MAX, dmax = -1;
             for (int Y = L.h0; Y <= L.h1; Y++)
                 for (int X = 1; X <= out_w - 2; X++)
                     if (mask[(long long)Y * out_w + X]) {
                         const int d = X + Y;
-                        cnt[(d & 1) * (nk + 1) + (d >> 1) + 1]++;
+                        cnt[((size_t)blk_of[Y] * 2 + (d & 1)) * per + (d >> 1) + 1]++;
                         dmin = std::min(dmin, d);
                         dmax = std::max(dmax, d);
                     }
             std::vector<int> off(cnt.size());
             int acc = 0;
-            for (int p = 0; p < 2; p++)
-                for (int k = 0; k <= nk; k++) {
-                    acc += cnt[p * (nk + 1) + k];
-                    off[p * (nk + 1) + k] = acc;  // k = 0 holds the zero count: start of d = p
+            for (size_t q = 0; q < (size_t)nb * 2; q++)
+                for (size_t k = 0; k < per; k++) {
+                    acc += cnt[q * per + k];
+                    off[q * per + k] = acc;  // k = 0 holds the zero count: start of d = p
                 }
             std::vector<int> fill(off), list(std::max(acc, 1));
             for (int Y = L.h0; Y <= L.h1; Y++)
                 for (int X = 1; X <= out_w - 2; X++)
                     if (mask[(long long)Y * out_w + X]) {
                         const int d = X + Y;
-                        list[fill[(d & 1) * (nk + 1) + (d >> 1)]++] = Y * out_w + X;
+                        list[fill[((size_t)blk_of[Y] * 2 + (d & 1)) * per + (d >> 1)]++] =
+                            Y * out_w + X;
                     }
             if ((rc = upload(c, c->sm_list, list))) return rc;
             if ((rc = upload(c, c->sm_off, off))) return rc;
             c->sm_nk = nk;
+            c->sm_nb = nb;
             c->sm_smin = dmin;
             c->sm_smax = dmax < 0 ? -1 : dmax + 2 * (iters - 1);
             c->sm_key_boxes = boxes;
@@ -1592,10 +1632,39 @@ int pf_solve_smoothing(pf_ctx* c, const float* tiles, const float* coeffs, int b
         launch_smooth_seed(c->stream, (const TileGeom*)c->geom.p, c->ntiles,
                            (const int2*)c->sm_src.p, tiles, c->tile_elems, coeffs, out_w, out_h,
                            (float*)c->buf[0].p, batch);
-        if (c->sm_smax >= c->sm_smin)
-            launch_smooth_list(c->stream, (const int*)c->sm_list.p, (const int*)c->sm_off.p,
-                               c->sm_nk, out_w, out_h, c->sm_smin, c->sm_smax, iters,
-                               (float*)c->buf[0].p, batch);
+        if (c->sm_smax >= c->sm_smin) {
+            if (nb == 1) {
+                launch_smooth_list(c->stream, (const int*)c->sm_list.p, (const int*)c->sm_off.p,
+                                   c->sm_nk, out_w, out_h, c->sm_smin, c->sm_smax, iters,
+                                   (float*)c->buf[0].p, batch);
+            } else {
+                // sync words: [0] ticket, [1] timeouts, [2..] one step flag per (panorama, block);
+                // tickets and flags are monotone across launches (sm_tk, sm_fb)
+                const size_t sb = sizeof(uint32_t) * (2 + (size_t)batch * nb);
+                if (c->sm_sync.bytes < sb) {
+                    if ((rc = ensure(c, c->sm_sync, sb))) return rc;
+                    HIPCHK(c, hipMemsetAsync(c->sm_sync.p, 0, sb, c->stream));
+                    c->sm_tk = 0;
+                    c->sm_fb = 1;
+                }
+                if (!c->jres_err_h)
+                    HIPCHK(c, hipHostMalloc((void**)&c->jres_err_h, sizeof(uint32_t),
+                                            hipHostMallocMapped | hipHostMallocCoherent));
+                SmoothSync S{};
+                uint32_t* w32 = (uint32_t*)c->sm_sync.p;
+                S.ticket = w32;
+                S.err = w32 + 1;
+                S.flags = w32 + 2;
+                S.err_host = c->jres_err_h;
+                S.tbase = c->sm_tk;
+                S.fbase = c->sm_fb;
+                c->sm_tk += (uint32_t)(batch * nb);
+                c->sm_fb += (uint32_t)(c->sm_smax - c->sm_smin + 2);
+                launch_smooth_band(c->stream, (const int*)c->sm_list.p, (const int*)c->sm_off.p,
+                                   c->sm_nk, nb, out_w, out_h, c->sm_smin, c->sm_smax, iters,
+                                   (float*)c->buf[0].p, batch, S);
+            }
+        }
     }
     launch_quantize(c->stream, (const float*)c->buf[0].p, n, (int)n, out, n, batch);
     HIPCHK(c, hipGetLastError());

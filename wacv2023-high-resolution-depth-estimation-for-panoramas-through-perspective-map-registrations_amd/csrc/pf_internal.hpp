@@ -303,6 +303,17 @@ void launch_smooth_seed(hipStream_t s, const TileGeom* geom, int ntiles, const i
                         float* buf, int batch);
 void launch_smooth_list(hipStream_t s, const int* list, const int* off, int nk, int w, int h,
                         int smin, int smax, int iters, float* buf, int batch);
+// the row-band form: tickets, per-block step flags (monotone across launches), timeouts
+struct SmoothSync {
+    uint32_t* ticket;
+    uint32_t* flags;     // [batch][nb]
+    uint32_t* err;
+    uint32_t* err_host;  // coherent pinned flag (PF_ETIMEOUT), may be null
+    uint32_t tbase, fbase;
+};
+void launch_smooth_band(hipStream_t s, const int* list, const int* off, int nk, int nb, int w,
+                        int h, int smin, int smax, int iters, float* buf, int batch,
+                        const SmoothSync& S);
 void launch_smooth(hipStream_t s, const TileGeom* geom, int ntiles, const int2* src,
                    const uint8_t* mask, const float* tiles, long long tstride,
                    const float* coeffs, int w, int h, int h0, int h1, int iters, float* buf,

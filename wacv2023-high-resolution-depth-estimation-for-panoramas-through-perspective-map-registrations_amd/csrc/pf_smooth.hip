@@ -151,6 +151,98 @@ __global__ void __launch_bounds__(1024) k_smooth_iter_list(float* __restrict__ b
     }
 }
 
+// Row-band form (round 4, the default): the band's rows are cut into `nb` row blocks of about
+// equal masked-pixel counts, and one 256-thread workgroup per (panorama, block) runs the same
+// wavefront schedule over its block's pixels, so a panorama's steps spread over nb CUs.  A
+// pixel's vertical neighbours may sit in the next block, so before step s a workgroup waits until
+// both neighbouring blocks have finished step s-1 -- which orders every cross-block read after
+// the write it needs (step s-1) and every write after the neighbour's last read of the old value
+// (its step s-1).  The hand-off is MI355X_MICROARCH.md's write-through form: every access to the
+// level is sc1 (L1-bypassing, write-through), every storing wave drains (vmcnt(0)), a barrier,
+// one agent-scope flag store; one lane polls the two neighbours' flags, a barrier.  Workgroups
+// take (panorama, block) from a ticket counter when they start, so a panorama's blocks are held
+// by running workgroups and groups fill in ticket order (no co-residency assumption beyond nb
+// workgroups).  Waits are bounded: a timeout is counted (and raised to the host's flag) instead
+// of hanging the device.  Lists: per block, the masked pixels split by the parity of d = X + Y and
+// sorted by d; off[(blk*2 + p)*(nk+1) + k] = first index of d = 2k + p in the block's list.
+constexpr int kSB = 256;
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t smooth_rsrc(const void* base, uint32_t bytes)
+{
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), 0, (int)bytes, 0x00020000);
+}
+__device__ __forceinline__ float ld_sc1(__amdgpu_buffer_rsrc_t r, int o)
+{
+    return __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(r, 4 * o, 0, 16));
+}
+
+__global__ void __launch_bounds__(kSB) k_smooth_band(float* __restrict__ buf,
+                                                     const int* __restrict__ list,
+                                                     const int* __restrict__ off, int nk, int nb,
+                                                     int w, long long npx, int smin, int smax,
+                                                     int iters, SmoothSync S)
+{
+    __shared__ uint32_t lds_ticket;
+    const int tid = threadIdx.x;
+    if (tid == 0) lds_ticket = __hip_atomic_fetch_add(S.ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __syncthreads();
+    const uint32_t tk = __builtin_amdgcn_readfirstlane(lds_ticket - S.tbase);
+    const int pano = (int)(tk / (uint32_t)nb), blk = (int)(tk % (uint32_t)nb);
+    const auto B = smooth_rsrc(buf + (long long)pano * npx, (uint32_t)(npx * 4));
+    uint32_t* const flags = S.flags + (long long)pano * nb;
+    const int* const offb = off + (long long)blk * 2 * (nk + 1);
+    for (int s = smin; s <= smax; s++) {
+        if (s > smin) {  // both neighbouring blocks finished step s-1
+            if (tid == 0) {
+                const uint32_t want = S.fbase + (uint32_t)(s - smin);  // step s-1 done
+                for (int nbj = blk - 1; nbj <= blk + 1; nbj += 2) {
+                    if (nbj < 0 || nbj >= nb) continue;
+                    int spins = 0;
+                    while ((int)(__hip_atomic_load(&flags[nbj], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) - want) < 0) {
+                        __builtin_amdgcn_s_sleep(1);
+                        if (++spins > (1 << 22)) {
+                            __hip_atomic_fetch_add(S.err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                            if (S.err_host) __hip_atomic_store(S.err_host, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                            break;
+                        }
+                    }
+                }
+            }
+            __syncthreads();
+        }
+        const int p = s & 1;
+        const int dlo = s - 2 * (iters - 1);
+        const int kl = dlo > p ? (dlo - p) >> 1 : 0, kh = min(nk - 1, (s - p) >> 1);
+        if (kl <= kh) {
+            const int* o2 = offb + p * (nk + 1);
+            const int lo = o2[kl], hi = o2[kh + 1];
+            for (int j = lo + tid; j < hi; j += kSB) {
+                const int o = list[j];
+                const float val = ld_sc1(B, o);
+                const float v0 = ld_sc1(B, o - 1), v1 = ld_sc1(B, o + 1), v2 = ld_sc1(B, o - w),
+                            v3 = ld_sc1(B, o + w);
+                const float avg = (((v0 + v1) + v2) + v3) / 4.0f;
+                const float nv = (float)((double)val + 0.5 * (double)(avg - val));
+                __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(nv), B, 4 * o, 0, 16);
+            }
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        if (tid == 0) {
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            __hip_atomic_store(&flags[blk], S.fbase + (uint32_t)(s - smin) + 1u, __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);
+        }
+    }
+}
+
+void launch_smooth_band(hipStream_t s, const int* list, const int* off, int nk, int nb, int w,
+                        int h, int smin, int smax, int iters, float* buf, int batch,
+                        const SmoothSync& S)
+{
+    hipLaunchKernelGGL(k_smooth_band, dim3((unsigned)(nb * batch)), dim3(kSB), 0, s, buf, list, off,
+                       nk, nb, w, (long long)w * h, smin, smax, iters, S);
+}
+
 void launch_smooth_list(hipStream_t s, const int* list, const int* off, int nk, int w, int h,
                         int smin, int smax, int iters, float* buf, int batch)
 {
