@@ -55,7 +55,12 @@
 #define PF_JLAG_PF 2  // steps of lead for the input and L row loads (1 or 2)
 #endif
 #ifndef PF_JLREG_T
-#define PF_JLREG_T 5  // passes of depth <= this keep their L ring in registers instead of LDS
+// passes of depth <= this keep their L ring in registers instead of LDS.  Round 4: at T = 10 the
+// register ring takes the packed pass from 132 VGPRs + 48 KB of LDS per 4-wave workgroup to
+// 166-167 VGPRs and no LDS -- the same 3 waves per SIMD -- and drops the T LDS reads per step:
+// C3 Jacobi stage 3.37-3.38 -> 3.19-3.24 ms, 14.10-14.35k -> 14.75-14.81k panoramas/s (three
+// alternating rounds on one MI355X, tools/r4_ab.sh)
+#define PF_JLREG_T 10
 #endif
 
 namespace pf {
@@ -149,9 +154,9 @@ struct JLag {
     // ring of R >= 2T+1 rows, R a multiple of 6: the loop body is unrolled over the R/6 groups
     // of 6 steps so every ring slot is a compile-time constant (LDS immediate offsets, no SALU)
     static constexpr int R = (2 * T + 1 + 5) / 6 * 6, NG = R / 6;
-    // Shallow passes (the coarse levels: few waves, latency-bound) keep the L ring in registers
-    // -- every slot index is a compile-time constant of the unrolled step -- so no LDS store /
-    // load latency sits on a step's dependency chain; deep passes keep it in LDS (VGPR budget).
+    // The L ring in registers -- every slot index is a compile-time constant of the unrolled
+    // step -- so no LDS store / load latency sits on a step's dependency chain (passes deeper
+    // than PF_JLREG_T keep it in LDS: VGPR budget).
     static constexpr bool LREG = T <= PF_JLREG_T;
     Row<C> Lr[LREG ? R : 1];  // LREG: ring slot s = Lr[s]
     Row<C> H[T][3];   // H[t][r % 3] = level t row r
