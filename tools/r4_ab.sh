@@ -9,7 +9,7 @@ export TMPDIR=/tmp
 for r in $(seq 1 ${ROUNDS:-2}); do
   for v in $VARIANTS; do
     name=${v%%:*}; envs=${v#*:}
-    ( IFS=','; for kv in $envs; do [ -n "$kv" ] && export "$kv"; done
+    ( for kv in ${envs//,/ }; do [ -n "$kv" ] && export "$kv"; done
       timeout -k 10 300 python bench.py --no-cpu-baseline --no-extra-configs ${BENCH_ARGS:-} \
         > $OUT/$name.$r.log 2>&1 ); rc=$?
     [ $rc -eq 0 ] || { echo "$name rc=$rc"; tail -5 $OUT/$name.$r.log; exit $rc; }
