@@ -1,6 +1,7 @@
 #!/bin/bash
 # SQ issue / LDS counters of k_warp_depth for the current library and, if present, the round-2
-# library (tools/ubench/bin/old_libpanofuse.so, built from git): output under gpurun_out/warp_sq/.
+# library ($OLD_LIB, default tools/ubench/bin/old_libpanofuse.so, built from git): output under
+# gpurun_out/warp_sq/.
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
 o=gpurun_out/warp_sq
@@ -8,8 +9,8 @@ mkdir -p $o
 for tag in new old; do
   lib=""
   if [ $tag = old ]; then
-    [ -f tools/ubench/bin/old_libpanofuse.so ] || continue
-    lib=$PWD/tools/ubench/bin/old_libpanofuse.so
+    lib=${OLD_LIB:-$PWD/tools/ubench/bin/old_libpanofuse.so}
+    [ -f "$lib" ] || continue
   fi
   PANOFUSE_LIB=$lib timeout -k 10 120 python3 tools/warp_probe.py > $o/probe_$tag.txt 2>&1 || exit 1
   PANOFUSE_LIB=$lib timeout -s KILL 90 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY \
