@@ -40,8 +40,8 @@ VALU_PEAK_TF = 157.3   # MI355X_MICROARCH.md: peak FP32 vector (packed FMA), spe
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=5)
-    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--batch", type=int, default=64, help="panoramas per GPU per step")
     ap.add_argument("--c5-shard", choices=("rows", "tiles"), default="rows",
                     help="c5 mode: rows = tiles AND sweep row bands sharded over the ranks "
@@ -56,10 +56,11 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-extra-configs", action="store_true",
                     help="skip the C2 batch-1 latency and the one-GPU C5 sub-records")
-    ap.add_argument("--pipeline", type=int, default=1,
-                    help="1: software-pipelined steps -- the warp of batch k+1 (second stream) "
+    ap.add_argument("--pipeline", type=int, default=2,
+                    help="0: serial steps; 1: the warp of batch k+1 (second stream) "
                          "runs while batch k is registered and fused; every step still warps, "
-                         "registers and fuses one whole batch")
+                         "registers and fuses one whole batch; N >= 2: N fusion lanes (own "
+                         "context, stream and buffers), batch k on lane k %% N")
     ap.add_argument("--backend", choices=("nccl", "gloo"), default="nccl",
                     help="torch.distributed backend for N > 1: nccl (= RCCL over xGMI, the "
                          "default) or gloo with host-staged tensors (several ranks sharing one "
@@ -348,7 +349,7 @@ def pipelined_step(fz, lay, local, dev, gt, emap, resp, tiles, out, coeffs, zr):
     fw = panofuse.Fuser(local, stream=sw)
     fw.set_tiles(lay)
     bufs = [tiles, torch.empty_like(tiles)]
-    main = torch.cuda.current_stream(dev)
+    main = fz.stream  # the fusion's stream (the caller's current stream unless fz has its own)
     st = {"k": 0, "warped": None, "fused": None, "fw": fw}
     fw.warp_depth(gt, bufs[0], resp)
     st["warped"] = torch.cuda.Event()
@@ -371,6 +372,45 @@ def pipelined_step(fz, lay, local, dev, gt, emap, resp, tiles, out, coeffs, zr):
         st.update(k=k + 1, warped=warped, fused=fused)
 
     return pstep
+
+
+def lane_steps(fz, lay, local, dev, gt, emap, resp, tiles, out, coeffs, zr, nlanes):
+    """`--pipeline N` (N >= 2): N fusion lanes, each its own context on its own stream with its own
+    tile / output / coefficient buffers; step k warps, registers and fuses one whole batch on lane
+    k % N, so N consecutive batches are in flight at once and their kernels fill each other's
+    gaps (the under-occupied level-1 passes, launch tails).  Each lane is pipelined like
+    `--pipeline 1` (the warp of its next batch on a second stream).  Same work per step as the
+    serial step.  Returns (step, lanes): lanes[i] = (context, tiles, out, coeffs); lane 0 uses the
+    caller's context and buffers."""
+    import torch
+
+    import panofuse
+
+    lanes = [(fz, tiles, out, coeffs)]
+    for _ in range(1, nlanes):
+        f = panofuse.Fuser(local, stream=torch.cuda.Stream(dev))
+        f.set_tiles(lay)
+        lanes.append((f, torch.empty_like(tiles), torch.empty_like(out), torch.empty_like(coeffs)))
+    st = {"k": 0}
+    # every lane is itself pipelined (bench.pipelined_step: its warps on a stream of their own,
+    # its fusions on the lane's stream); PF_LANE_WARP=0 (A/B runs): warp and fusion in line
+    psteps = None
+    if os.environ.get("PF_LANE_WARP", "1") != "0":
+        psteps = []
+        for f, t, o, c in lanes:  # warps on a stream of their own, fusions on f's stream
+            psteps.append(pipelined_step(f, lay, local, dev, gt, emap, resp, t, o, c, zr))
+
+    def lstep():
+        i = st["k"] % nlanes
+        if psteps is not None:
+            psteps[i]()
+        else:
+            f, t, o, c = lanes[i]
+            f.warp_depth(gt, t, resp)
+            f.merge(emap, t, o, zr, coeffs=c)
+        st["k"] += 1
+
+    return lstep, lanes
 
 
 def timed_steps(step, sync, args, world, dist, device=None):
@@ -526,14 +566,21 @@ def main():
         fz.warp_depth(gt, tiles, resp)
         fz.merge(emap, tiles, out, zr, coeffs=coeffs)
 
-    if args.pipeline:
+    ctxs = [fz]
+    if args.pipeline >= 2:
+        lstep, lanes = lane_steps(fz, lay, local, dev, gt, emap, resp, tiles, out, coeffs, zr,
+                                  args.pipeline)
+        ctxs = [ln[0] for ln in lanes]
+        mine_s, elapsed = timed_steps(lstep, torch.cuda.synchronize, args, world, dist, dev)
+    elif args.pipeline:
         pstep = pipelined_step(fz, lay, local, dev, gt, emap, resp, tiles, out, coeffs, zr)
         mine_s, elapsed = timed_steps(pstep, torch.cuda.synchronize, args, world, dist, dev)
     else:
         mine_s, elapsed = timed_steps(step, torch.cuda.synchronize, args, world, dist, dev)
     # every fusion of the run was valid: raises PF_ETIMEOUT (non-zero exit) if a resident-kernel
     # hand-off wait timed out in any of them
-    fz.synchronize()
+    for c in ctxs:
+        c.synchronize()
     # Per-kernel roofline: the same steps again with the library's hipEvent stage timers on
     # (recorded on the stream the kernels run on).  With the timers on, the library runs each
     # batch unsplit (no half-batch stream overlap), so every stage's time is its own.
@@ -638,7 +685,11 @@ def main():
                                    f"20 tiles of 512x512 (5x4 layout), 512x256 baseline",
                        "global_batch": B * world, "out": "2048x1024", "tiles": "20x512x512",
                        "parallelism": f"dp{world} (panorama sharding, no collective)",
-                       "pipeline": ("warp of batch k+1 on a second stream beside the fusion "
+                       "pipeline": (f"{args.pipeline} fusion lanes: batch k warped, registered "
+                                    f"and fused on lane k % {args.pipeline} (own contexts, streams "
+                                    f"and buffers; each lane warps its next batch on a second "
+                                    f"stream)" if args.pipeline >= 2 else
+                                    "warp of batch k+1 on a second stream beside the fusion "
                                     "of batch k, from the end of its level-0 sweeps"
                                     if args.pipeline else "off"),
                        "layout_caches": "tap maps, warp corner tables and level tables are "
