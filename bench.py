@@ -252,9 +252,28 @@ def c5_measure(args, rank, world, local, dev, steps, warmup):
         fz.merge(emap, full, ref[None], zr, coeffs=torch.zeros_like(coeffs)[None])
         torch.cuda.synchronize()
         bit_exact = bool(torch.equal(ref, out))
+    one_call = None
+    if world == 1:
+        # the same panorama through the library's one-call path (pf_warp_depth + pf_merge on one
+        # context, no per-level host orchestration): hipEvents, median of 5
+        rall = panofuse.make_responses(resp_all, dev)
+        full = torch.zeros_like(tiles)
+        ref = torch.empty_like(out)
+        cz = torch.zeros_like(coeffs)[None]
+        ts_ = []
+        for i in range(7):
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            fz.warp_depth(gt, full, rall)
+            fz.merge(emap, full, ref[None], zr, coeffs=cz)
+            e1.record()
+            torch.cuda.synchronize()
+            if i >= 2:
+                ts_.append(e0.elapsed_time(e1))
+        one_call = sorted(ts_)[len(ts_) // 2]
     nz = int((out != 0).sum().item())
     return {"value": steps / elapsed, "elapsed": elapsed, "mine_s": mine_s,
-            "bit_exact": bit_exact, "nonzero_px": nz}
+            "bit_exact": bit_exact, "nonzero_px": nz, "one_call_ms": one_call}
 
 
 def run_c5(args, rank, world, local, dev):
@@ -633,6 +652,10 @@ def main():
         r5 = c5_measure(args, 0, 1, local, dev, steps=3, warmup=1)
         c5 = {"value": r5["value"], "unit": "panoramas/s", "ms_per_panorama": 1e3 / r5["value"],
               "steps": 3, "bit_exact_vs_one_gpu": r5["bit_exact"],
+              "one_call_ms": r5["one_call_ms"],
+              "one_call": "pf_warp_depth + pf_merge of the same panorama on one context "
+                          "(hipEvents, median of 5): the library path without the sharded "
+                          "path's per-level host orchestration",
               "workload": "C5 on one GPU: one 8192x4096 panorama, 80 tiles of 1024^2 (10x8), "
                           "2048x1024 baseline, 4 levels (bench.py --mode c5 at world 1)"}
 
