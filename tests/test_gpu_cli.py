@@ -25,6 +25,7 @@ import panofuse  # noqa: E402
 import pf_layouts as PL  # noqa: E402
 import pf_synth  # noqa: E402
 import pyoracle as O  # noqa: E402
+import pystb  # noqa: E402
 
 ROOT = os.path.dirname(os.path.dirname(panofuse.LIB_PATH))
 BIN = os.path.join(ROOT, "bin", "panofuse_main")
@@ -162,7 +163,9 @@ def test_export_rgb_tiles(tmp_path):
     and decoded here by libjpeg (PIL), against the oracle's restatement of the GL camera: the
     warp itself is bit-exact (test_gpu_parity.py::test_warp_rgb_bit_exact), so what remains is
     the JPEG round trip's bar (tests/test_io.py), i.e. within 4 levels, mean under 0.5.  OpenGL
-    rasterisation parity is unpinned."""
+    rasterisation parity is unpinned.  Where the reference's stb is built (oracle/_ref/
+    libstbref.so, which travels with the tree), every file must also equal, byte for byte, stb's
+    stbi_write_jpg of the oracle's tile."""
     Image = pytest.importorskip("PIL.Image")
     (tmp_path / "rgb").mkdir()
     h, w = 512, 1024
@@ -187,6 +190,13 @@ def test_export_rgb_tiles(tmp_path):
         assert got.shape == (988, 1024, 3)
         n = 988 * 1024 * 3
         d = np.abs(got.reshape(-1).astype(np.int32) - ref[off:off + n].astype(np.int32))
+        if pystb.available():
+            # the file itself: the reference's own stbi_write_jpg (oracle/_ref/libstbref.so)
+            # applied to the oracle's tile pixels, at the reference's quality argument (the row
+            # stride, Main.cpp:320), gives the same bytes
+            ref_fn = tmp_path / f"stb_{t}.jpg"
+            assert pystb.write_jpg(ref_fn, ref[off:off + n].reshape(988, 1024, 3), 1024 * 3)
+            assert fn.read_bytes() == ref_fn.read_bytes(), t
         off += n
         assert d.max() <= 4 and d.mean() < 0.5, (t, d.max(), d.mean())
 
