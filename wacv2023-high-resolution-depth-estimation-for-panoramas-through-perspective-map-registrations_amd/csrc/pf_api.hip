@@ -825,6 +825,11 @@ struct JacobiTuning {
     double step_overhead = 3.0, lone_cycles = 4.0;  // swept on MI355X (tools/jsweep.sh)
     double c4_eff = 23.0 / 26.0;  // packed C=4 issue per pixel-update relative to C=2
     double pipe_overhead = 1.0;   // pipelined engine: barrier + exchange per step, update units
+    // per pass, in the cost units of best_chunks (~10 ns each at C3): a launch's fixed cost
+    // (dispatch, ramp, drain; a few us).  Without it the planner cut the batch-1 levels into
+    // hundreds of tiny passes (C5 on one GPU: 173 passes, Jacobi 2.11 ms; with it 63 passes,
+    // 1.60 ms; C2 latency 0.97 -> 0.82 ms; the batch-64 plans are unchanged).  PF_JLAUNCH=...
+    double launch_cost = 300.0;
 };
 
 static JacobiTuning jacobi_tuning()
@@ -836,6 +841,7 @@ static JacobiTuning jacobi_tuning()
     if (const char* e = getenv("PF_JOVH")) t.step_overhead = atof(e);
     if (const char* e = getenv("PF_JC1")) t.lone_cycles = atof(e);
     if (const char* e = getenv("PF_JPOVH")) t.pipe_overhead = atof(e);
+    if (const char* e = getenv("PF_JLAUNCH")) t.launch_cost = atof(e);
     if (t.Tmax < 1) t.Tmax = 1;
     return t;
 }
@@ -922,7 +928,7 @@ static std::vector<PassPlan> plan_level(pf_ctx* c, const LevelDims& L, int C, in
     for (int r = 1; r <= L.iters; r++)
         for (int T : menu) {
             if (T > r || T > tcap || !jstream_supported_T(T)) continue;
-            const double v = dp[r - T] + opt[T].cost;
+            const double v = dp[r - T] + opt[T].cost + tune.launch_cost;
             if (v < dp[r]) {
                 dp[r] = v;
                 choice[r] = T;
