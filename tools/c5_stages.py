@@ -1,6 +1,6 @@
-"""Stage times of ONE C5 panorama (8192x4096, 80 tiles, 4 levels) through pf_warp_depth +
-pf_merge on one context (the library's hipEvent stage timers), plus the per-level Jacobi plans
-(PF_JPLAN=1 prints them on stderr)."""
+"""Stage times of ONE panorama through pf_warp_depth + pf_merge on one context (the library's
+hipEvent stage timers), plus the per-level Jacobi plans (PF_JPLAN=1 prints them on stderr).
+    python3 tools/c5_stages.py [C5|C2]   (C5: 8192x4096, 80 tiles, 4 levels; C2: 2048x1024, 20 tiles)"""
 import json
 import os
 import sys
@@ -14,8 +14,9 @@ import pf_layouts as PL  # noqa: E402
 import pf_synth  # noqa: E402
 
 dev = torch.device("cuda:0")
-out_w, ew = PL.CONFIGS["C5"]
-lay = PL.config_layout("C5")
+cfg = sys.argv[1] if len(sys.argv) > 1 else "C5"
+out_w, ew = PL.CONFIGS[cfg] if cfg in PL.CONFIGS else (2048, 512)
+lay = PL.config_layout(cfg)
 zr = PL.ZENITH_RANGE
 seeds = pf_synth.seeds_for(1, 20261015)
 gt = pf_synth.scene_depth(seeds, out_w, out_w // 2, dev).contiguous()
@@ -38,5 +39,6 @@ for _ in range(5):
     res.append(fz.profile_read())
 fz.profile(False)
 med = {k: sorted(r[k][0] for r in res)[2] for k in res[0]}
-print(json.dumps({"stage_ms": med, "levels": [panofuse.level_info(out_w, out_w // 2, zr, l)
-                                               for l in range(4)]}))
+nl = panofuse.level_info(out_w, out_w // 2, zr, 0)[5]
+print(json.dumps({"config": cfg, "stage_ms": med,
+                  "levels": [panofuse.level_info(out_w, out_w // 2, zr, l) for l in range(nl)]}))
