@@ -34,6 +34,7 @@ struct LevelCache {
     int nlevels = 0;
     LevelDims dims[4];
     DevBuf box[4], cols[4], rows[4], tapbox[4], tapmap[4], hcol[4];
+    DevBuf tmask[4];  // per targets patch, the tiles whose box meets it (k_targets_multi)
     // (pixel, tile) pairs of the pixels covered by three or more tiles, sorted by pixel then
     // tile (the sharded fusion recomputes their sums in tile order: pf_fuse_multicover)
     DevBuf mcpairs[4];
@@ -355,6 +356,7 @@ void pf_destroy(pf_ctx* c)
         release(c->lc.cols[l]);
         release(c->lc.rows[l]);
         release(c->lc.tapbox[l]);
+        release(c->lc.tmask[l]);
         release(c->lc.tapmap[l]);
         release(c->lc.hcol[l]);
         release(c->lc.mcpairs[l]);
@@ -738,6 +740,21 @@ static int prepare_levels(pf_ctx* c, int out_w, int out_h, float zr0, float zr1)
         std::vector<GridRow> rows;
         grid_tables(L, cols, rows);
         int rc;
+        {   // per targets patch of this level, mask words of the tiles whose box meets it (the
+            // device's box_meets on the patch rectangle targets_patch uses)
+            const int pw_ = targets_patch_w(), ph_ = targets_patch_h();
+            const int npx = (L.w + pw_ - 1) / pw_, npy = (L.h1 - L.h0 + 1 + ph_ - 1) / ph_;
+            const int nmw = (c->ntiles + 31) / 32;
+            std::vector<uint32_t> tm((size_t)npx * npy * nmw, 0u);
+            for (int pid = 0; pid < npx * npy; pid++) {
+                const int X0 = (pid % npx) * pw_, Y0 = L.h0 + (pid / npx) * ph_;
+                const int X1 = std::min(X0 + pw_ - 1, L.w - 1), Y1 = std::min(Y0 + ph_ - 1, L.h1);
+                for (int p = 0; p < c->ntiles; p++)
+                    if (box_meets(boxes[p], X0, X1, Y0, Y1))
+                        tm[(size_t)pid * nmw + p / 32] |= 1u << (p % 32);
+            }
+            if ((rc = upload(c, lc.tmask[l], tm))) return rc;
+        }
         if ((rc = upload(c, lc.box[l], boxes))) return rc;
         if ((rc = upload(c, lc.hcol[l], hcol))) return rc;
         if ((rc = upload(c, lc.cols[l], cols))) return rc;
@@ -1281,6 +1298,8 @@ static int fuse_range(pf_ctx* c, const float* emap, int ew, int eh, int ec, cons
         for (int l = 0; l < lc.nlevels; l++) {
             const LevelDims& L = lc.dims[l];
             TgtLevel& T = M.lv[l];
+            T.tmask = (const uint32_t*)lc.tmask[l].p;
+            T.nmw = (c->ntiles + 31) / 32;
             T.L = L;
             T.box = (const TileBox*)lc.box[l].p;
             T.tb = (const TapBox*)lc.tapbox[l].p;

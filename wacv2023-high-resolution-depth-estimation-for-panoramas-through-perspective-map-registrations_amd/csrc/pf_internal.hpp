@@ -36,6 +36,15 @@ struct TileBox {
     int x0, x1, y0, y1, xs, pad[3];
 };
 
+// Does the box (X from x0 stepping xs, stopping before x1; rows y0..y1) meet [X0,X1]x[Y0,Y1]?
+// Host (per-patch tile masks of the targets gather) and device alike.
+__host__ __device__ inline bool box_meets(const TileBox& bx, int X0, int X1, int Y0, int Y1)
+{
+    if (bx.y0 > bx.y1 || bx.y1 < Y0 || bx.y0 > Y1) return false;
+    const int lo = bx.xs > 0 ? bx.x0 : bx.x1 + 1, hi = bx.xs > 0 ? bx.x1 - 1 : bx.x0;
+    return lo <= hi && hi >= X0 && lo <= X1;
+}
+
 // Tap-index map extent of one tile at one level: its box plus a one-pixel ring, row-major,
 // starting at element `off` of the level's map.
 struct TapBox {
@@ -124,8 +133,14 @@ __host__ __device__ inline long long tile_index(const TileGeom& g, float x, floa
 // Depth2DepthTransform's per-pixel map (Depth.cpp:256-271).
 __host__ __device__ inline float cubic_map(float X, float a, float b, float c, float d)
 {
-    if (X < 1e-4) X = (float)1e-4;
-    else if (X > (1 - 1e-4)) X = (float)(1 - 1e-4);
+    // Depth2DepthTransform's clamps compare the float X against the double constants 1e-4 and
+    // 1 - 1e-4 (Depth.cpp:245-274).  The float forms below decide identically for every one of
+    // the 2^32 float bit patterns (NaN included; tests/test_cubic_thresholds.py runs the
+    // exhaustive check): (double)X < 1e-4 iff X <= 0x38D1B717 (= (float)1e-4, the largest float
+    // below 1e-4), and (double)X > 1 - 1e-4 iff X > 0x3F7FF972 (= (float)(1 - 1e-4), the largest
+    // float below it).  No f64 conversion or compare per value.
+    if (X <= 9.99999974737875e-05f) X = (float)1e-4;
+    else if (X > 0.99989998340606689f) X = (float)(1 - 1e-4);
     float Y = a * X * X * X + b * X * X + c * X + d;
     if (Y < 0) Y = 0;
     else if (Y > 1) Y = 1;
@@ -217,6 +232,8 @@ void launch_targets_patch(hipStream_t s, const TileGeom* geom, const TileBox* bo
 struct TgtLevel {
     LevelDims L;
     const TileBox* box;
+    const uint32_t* tmask;  // per patch, mask words of the tiles whose box meets it (tile order)
+    int nmw;                // mask words per patch: ceil(ntiles / 32)
     const TapBox* tb;
     const int32_t* map;
     float* lnorm;

@@ -146,19 +146,15 @@ static constexpr int kTGW = kTPW + 2, kTGH = kTPH + 2, kTG = kTGW * kTGH;  // gr
 #define PF_TGT_NB 8
 #endif
 static constexpr int kTNB = PF_TGT_NB;                           // panoramas per block
+#ifndef PF_TGT_DIAG
+#define PF_TGT_DIAG 0  // probes only (wrong output, timing): bit 0 = no tile gathers, bit 1 = no stores
+#endif
 #ifndef PF_TGT_NT
 // nt stores of the target planes keep the tiles' lines in L2 for the neighbouring patches: the
 // stage went 0.629-0.633 -> 0.618-0.623 ms per C3 step (tools/r3_tgt.sh, profiles/r03/tgt/);
 // 4 / 16 panoramas per block measured 0.639-0.651 / 0.730
 #define PF_TGT_NT 1
 #endif
-
-__device__ __forceinline__ bool box_meets(const TileBox& bx, int X0, int X1, int Y0, int Y1)
-{  // does the box (X from x0 stepping xs, stopping before x1; rows y0..y1) meet [X0,X1]x[Y0,Y1]
-    if (bx.y0 > bx.y1 || bx.y1 < Y0 || bx.y0 > Y1) return false;
-    const int lo = bx.xs > 0 ? bx.x0 : bx.x1 + 1, hi = bx.xs > 0 ? bx.x1 - 1 : bx.x0;
-    return lo <= hi && hi >= X0 && lo <= X1;
-}
 
 // One block's work: patch `pid` of level L for panoramas [bgrp*kTNB, +kTNB).
 template <bool XFORM>
@@ -170,7 +166,9 @@ __device__ __forceinline__ void targets_patch(const TileGeom* __restrict__ geom,
                                               const float* __restrict__ coeffs, const LevelDims& L,
                                               int npx, int pid, int bgrp,
                                               float* __restrict__ lnorm, long long lstride,
-                                              int batch, float (*sv)[kTG])
+                                              int batch, float (*sv)[kTG],
+                                              const uint32_t* __restrict__ tmask = nullptr,
+                                              int nmw = 0)
 {
     const int X0 = (pid % npx) * kTPW, Y0 = L.h0 + (pid / npx) * kTPH;
     const int t = threadIdx.x;
@@ -185,9 +183,10 @@ __device__ __forceinline__ void targets_patch(const TileGeom* __restrict__ geom,
         for (int q = 0; q < kTNB; q++) acc[j][q] = 0.0f;
     }
     const int X1 = min(X0 + kTPW - 1, L.w - 1), Y1 = min(Y0 + kTPH - 1, L.h1);
-    for (int p = 0; p < ntiles; p++) {  // tile index order (the reference's accumulation order)
+    // one tile's contribution to the patch (tiles come in index order: the reference's
+    // accumulation order)
+    auto tile = [&](const int p) {
         const TileBox bx = box[p];
-        if (!box_meets(bx, X0, X1, Y0, Y1)) continue;  // block-uniform
         const TapBox B = tb[p];
         const long long toff = geom[p].off;
         float4 k[kTNB];
@@ -207,7 +206,8 @@ __device__ __forceinline__ void targets_patch(const TileGeom* __restrict__ geom,
 #pragma unroll
             for (int q = 0; q < kTNB; q++) {
                 const int b = bbeg + q < batch ? bbeg + q : batch - 1;
-                v[q] = tiles[b * tstride + toff + m];
+                if constexpr ((PF_TGT_DIAG & 1) != 0) v[q] = (float)(m & 1023) * 1e-3f + (float)b;
+                else v[q] = tiles[b * tstride + toff + m];
             }
 #pragma unroll
             for (int q = 0; q < kTNB; q++) {
@@ -238,6 +238,18 @@ __device__ __forceinline__ void targets_patch(const TileGeom* __restrict__ geom,
             }
         }
         __syncthreads();
+    };
+    if (tmask) {  // the host's list of the tiles whose box meets this patch, as mask words
+        for (int w = 0; w < nmw; w++) {
+            uint32_t m = tmask[(long long)pid * nmw + w];  // block-uniform
+            while (m) {
+                tile(w * 32 + __builtin_ctz(m));
+                m &= m - 1;
+            }
+        }
+    } else {
+        for (int p = 0; p < ntiles; p++)
+            if (box_meets(box[p], X0, X1, Y0, Y1)) tile(p);  // block-uniform
     }
 #pragma unroll
     for (int j = 0; j < kTPP; j++) {
@@ -258,8 +270,13 @@ __device__ __forceinline__ void targets_patch(const TileGeom* __restrict__ geom,
             if (n[j] == 0) out = __uint_as_float(PF_NAN_MARKER);
             else if (n[j] == 1) out = acc[j][q];
             else out = acc[j][q] * scale;
-            if constexpr (PF_TGT_NT) __builtin_nontemporal_store(out, &lnorm[b * lstride + o]);
-            else lnorm[b * lstride + o] = out;
+            if constexpr ((PF_TGT_DIAG & 2) != 0) {
+                if (out == -12345.0f) lnorm[b * lstride + o] = out;  // probe: no stores
+            } else if constexpr (PF_TGT_NT) {
+                __builtin_nontemporal_store(out, &lnorm[b * lstride + o]);
+            } else {
+                lnorm[b * lstride + o] = out;
+            }
         }
     }
 }
@@ -306,7 +323,7 @@ __global__ void __launch_bounds__(256) k_targets_multi(const TileGeom* __restric
     const int2 ent = order[e];  // (level, patch)
     const TgtLevel& T = M.lv[ent.x];
     targets_patch<XFORM>(geom, T.box, T.tb, ntiles, T.map, tiles, tstride, coeffs, T.L, T.npx,
-                         ent.y, bgrp, T.lnorm, T.lstride, batch, sv);
+                         ent.y, bgrp, T.lnorm, T.lstride, batch, sv, T.tmask, T.nmw);
 }
 
 int targets_patch_w() { return kTPW; }
