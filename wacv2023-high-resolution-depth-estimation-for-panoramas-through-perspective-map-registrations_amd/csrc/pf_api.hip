@@ -70,6 +70,8 @@ struct pf_ctx {
     std::vector<RegGrid> reg_h;
     long long tile_elems = 0, npix_max = 0, rgb_elems = 0;
     DevBuf geom, reg, rcols, rrows, rgb_off;
+    DevBuf reg_sidx;                       // registration sample indices (k_regidx), for the
+    int reg_sidx_key[3] = {-1, -1, -1};    // (ew, eh, ec) of the baseline they were built for
     std::vector<RgbCam> cams_h;  // GL cameras of the RGB warp (SaveCubeMap), host only
     // RGB warp taps for one panorama size (rgb_taps_host), built on first use
     int rgb_pw = 0, rgb_ph = 0;
@@ -344,7 +346,7 @@ void pf_destroy(pf_ctx* c)
     if (!c) return;
     (void)hipSetDevice(c->device);
     (void)hipStreamSynchronize(c->stream);
-    DevBuf* all[] = {&c->geom, &c->reg, &c->rcols, &c->rrows, &c->rgbtap, &c->rgb_off,
+    DevBuf* all[] = {&c->geom, &c->reg, &c->reg_sidx, &c->rcols, &c->rrows, &c->rgbtap, &c->rgb_off,
                      &c->buf[0], &c->buf[1], &c->buf[2], &c->lnorm, &c->coeffs, &c->lsum_ws,
                      &c->wmap, &c->wfxy, &c->wpatch, &c->metrics_ws, &c->reg_sums,
                      &c->reg_active, &c->sm_box, &c->sm_cols, &c->sm_rows, &c->sm_src,
@@ -616,6 +618,7 @@ static int prepare_registration(pf_ctx* c, float zr0, float zr1)
     const float subd = (float)(1 / 180.0 * PF_MYPI);
     std::vector<GridCol> rcols;
     std::vector<GridRow> rrows;
+    int nsamp_total = 0;
     for (int i = 0; i < c->ntiles; i++) {
         const pf_window& r = c->rng[i];
         RegGrid rg{};
@@ -629,6 +632,7 @@ static int prepare_registration(pf_ctx* c, float zr0, float zr1)
         if (rg.rows < 0) rg.rows = 0;
         rg.col_off = (int)rcols.size();
         rg.row_off = (int)rrows.size();
+        rg.soff = nsamp_total;
         for (int k = 0; k <= rg.cols; k++) {  // :1334
             GridCol e{};
             e.az = r.az_left + (r.az_right - r.az_left) * (float)k / (float)rg.cols;
@@ -642,12 +646,14 @@ static int prepare_registration(pf_ctx* c, float zr0, float zr1)
             rrows.push_back(e);
         }
         c->reg_h[i] = rg;
+        nsamp_total += (rg.cols + 1) * (rg.rows + 1);
     }
     int rc;
     if ((rc = upload(c, c->reg, c->reg_h))) return rc;
     if ((rc = upload(c, c->rcols, rcols))) return rc;
     if ((rc = upload(c, c->rrows, rrows))) return rc;
     c->reg_valid = true;
+    c->reg_sidx_key[0] = -1;  // the sample indices follow the grids
     c->reg_zr0 = b0;
     c->reg_zr1 = b1;
     return PF_OK;
@@ -655,6 +661,30 @@ static int prepare_registration(pf_ctx* c, float zr0, float zr1)
 
 // The tiles that will be solved must have a non-empty sample grid (Depth.cpp:1334-1335 divides
 // by cols and rows); active == nullptr means every tile.
+// The registration samples' indices for this baseline size (k_regidx), rebuilt when the grids
+// or the baseline size change; stream-ordered before the k_register launches that read them.
+static const int2* reg_sample_index(pf_ctx* c, int ew, int eh, int ec)
+{
+    if (c->reg_sidx_key[0] == ew && c->reg_sidx_key[1] == eh && c->reg_sidx_key[2] == ec)
+        return (const int2*)c->reg_sidx.p;
+    long long n = 0;
+    int maxn = 0;
+    for (const RegGrid& g : c->reg_h) {
+        const int k = (g.cols + 1) * (g.rows + 1);
+        n += k;
+        maxn = k > maxn ? k : maxn;
+    }
+    if (n <= 0 || ensure(c, c->reg_sidx, sizeof(int2) * (size_t)n) != PF_OK) return nullptr;
+    launch_regidx(c->stream, (const TileGeom*)c->geom.p, (const RegGrid*)c->reg.p,
+                  (const GridCol*)c->rcols.p, (const GridRow*)c->rrows.p, c->ntiles, maxn, ew,
+                  eh, ec, (int2*)c->reg_sidx.p);
+    if (hipGetLastError() != hipSuccess) return nullptr;
+    c->reg_sidx_key[0] = ew;
+    c->reg_sidx_key[1] = eh;
+    c->reg_sidx_key[2] = ec;
+    return (const int2*)c->reg_sidx.p;
+}
+
 static int check_reg_grids(pf_ctx* c, const int* active)
 {
     for (int i = 0; i < c->ntiles; i++) {
@@ -1473,6 +1503,7 @@ int pf_register(pf_ctx* c, const float* emap, int ew, int eh, int ec, float* til
     }
     double nsamp = 0;
     for (const RegGrid& g : c->reg_h) nsamp += (double)(g.cols + 1) * (g.rows + 1);
+    const int2* sidx = reg_sample_index(c, ew, eh, ec);  // before the stage timer: built once
     {
         StageTimer t(c, PF_STAGE_REGISTER,
                      batch * (8.0 * nsamp + (apply ? 8.0 * (double)c->tile_elems / c->tile_c : 0.0)),
@@ -1480,7 +1511,7 @@ int pf_register(pf_ctx* c, const float* emap, int ew, int eh, int ec, float* til
         launch_register(c->stream, (const TileGeom*)c->geom.p, (const RegGrid*)c->reg.p,
                         (const GridCol*)c->rcols.p, (const GridRow*)c->rrows.p, c->ntiles, emap,
                         ew, eh, ec, (long long)ew * eh * ec, tiles, c->tile_elems, degree,
-                        c->solver, cf, coeffs64, batch);
+                        c->solver, cf, coeffs64, batch, nullptr, nullptr, sidx);
         if (apply)
             launch_apply_cubic(c->stream, (const TileGeom*)c->geom.p, c->ntiles,
                                c->tile_elems / c->tile_c, tiles, c->tile_elems, cf, batch);
@@ -2111,7 +2142,7 @@ int pf_register_joint(pf_ctx* c, const float* emap, int ew, int eh, int ec, cons
                     (const GridCol*)c->rcols.p, (const GridRow*)c->rrows.p, c->ntiles, emap, ew,
                     eh, ec, (long long)ew * eh * ec, tiles, c->tile_elems, degree, c->solver,
                     nullptr, nullptr, batch, (double*)c->reg_sums.p,
-                    (const int*)c->reg_active.p);
+                    (const int*)c->reg_active.p, reg_sample_index(c, ew, eh, ec));
     launch_register_joint(c->stream, (const double*)c->reg_sums.p, (const int*)c->reg_active.p,
                           c->ntiles, batch, degree, c->solver, cf, coeffs64);
     HIPCHK(c, hipGetLastError());

@@ -63,6 +63,7 @@ struct GridRow { float zen, sz, cz, pad; };  // row yy (index yy+1): zen, sin ze
 // Registration grid of one tile (Depth.cpp:1298-1335).
 struct RegGrid {
     int cols, rows, col_off, row_off;  // offsets into the shared GridCol / GridRow tables
+    int soff;                          // first sample of this tile in the sample-index table
 };
 
 // GL camera of SaveCubeMap (Main.cpp:246-269) per tile, evaluated on the host in double.
@@ -289,7 +290,13 @@ void launch_register(hipStream_t s, const TileGeom* geom, const RegGrid* grids,
                      const GridCol* rcols, const GridRow* rrows, int ntiles, const float* emap,
                      int ew, int eh, int ec, long long estride, const float* tiles,
                      long long tstride, int degree, int solver, float* coeffs, double* coeffs64,
-                     int batch, double* sums = nullptr, const int* active = nullptr);
+                     int batch, double* sums = nullptr, const int* active = nullptr,
+                     const int2* sidx = nullptr);
+// the registration samples' tile-element and baseline indices (layout- and baseline-size-only),
+// built once per (layout, zenith range, baseline size) so k_register only gathers
+void launch_regidx(hipStream_t s, const TileGeom* geom, const RegGrid* grids,
+                   const GridCol* rcols, const GridRow* rrows, int ntiles, int max_samples,
+                   int ew, int eh, int ec, int2* sidx);
 int register_sums_per_tile();
 void launch_register_joint(hipStream_t s, const double* sums, const int* active, int ntiles,
                            int batch, int degree, int solver, float* coeffs, double* coeffs64);

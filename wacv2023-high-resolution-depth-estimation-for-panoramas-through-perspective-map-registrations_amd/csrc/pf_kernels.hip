@@ -539,7 +539,7 @@ __global__ void __launch_bounds__(kRegLanes) k_register(
     const float* __restrict__ emap, int ew, int eh, int ec, long long estride,
     const float* __restrict__ tiles, long long tstride, int degree, int solver,
     float* __restrict__ coeffs, double* __restrict__ coeffs64, double* __restrict__ sums,
-    const int* __restrict__ active)
+    const int* __restrict__ active, const int2* __restrict__ sidx)
 {
     __shared__ double part[kRegSums][kRegLanes];
     // one linear grid, XCD-contiguous: the tiles of one panorama run on one XCD, so its emap is
@@ -568,6 +568,12 @@ __global__ void __launch_bounds__(kRegLanes) k_register(
             tv[u] = 0.0f;
             ev[u] = 0.0f;
             if (s >= ns) continue;
+            if (sidx) {  // the cached indices (k_regidx: the same arithmetic as below)
+                const int2 ix = sidx[rg.soff + s];
+                tv[u] = tile[ix.x];
+                ev[u] = em[ix.y];
+                continue;
+            }
             int r = s / ncol, c = s - r * ncol;
             const GridCol cc = rcols[rg.col_off + c];
             const GridRow rr = rrows[rg.row_off + r];
@@ -829,12 +835,52 @@ void launch_register(hipStream_t s, const TileGeom* geom, const RegGrid* grids,
                      const GridCol* rcols, const GridRow* rrows, int ntiles, const float* emap,
                      int ew, int eh, int ec, long long estride, const float* tiles,
                      long long tstride, int degree, int solver, float* coeffs, double* coeffs64,
-                     int batch, double* sums, const int* active)
+                     int batch, double* sums, const int* active, const int2* sidx)
 {
     dim3 grid((unsigned)(ntiles * batch));
     hipLaunchKernelGGL(k_register, grid, dim3(kRegLanes), 0, s, geom, grids, rcols, rrows,
                        ntiles, emap, ew, eh, ec, estride, tiles, tstride, degree, solver, coeffs,
-                       coeffs64, sums, active);
+                       coeffs64, sums, active, sidx);
+}
+
+// One thread per registration sample: the tile element (SphericalTo2D, clamp, Value's index) and
+// the baseline element (ValueAtCoord's index) of sample s of tile p, exactly as k_register's
+// direct path computes them (Depth.cpp:1328-1387).
+__global__ void __launch_bounds__(256) k_regidx(const TileGeom* __restrict__ geom,
+                                                const RegGrid* __restrict__ grids,
+                                                const GridCol* __restrict__ rcols,
+                                                const GridRow* __restrict__ rrows, int ew, int eh,
+                                                int ec, int2* __restrict__ sidx)
+{
+    const int p = blockIdx.y;
+    const TileGeom g = geom[p];
+    const RegGrid rg = grids[p];
+    const int ncol = rg.cols + 1;
+    const int ns = ncol * (rg.rows + 1);
+    for (int s = blockIdx.x * 256 + threadIdx.x; s < ns; s += gridDim.x * 256) {
+        const int r = s / ncol, c = s - r * ncol;
+        const GridCol cc = rcols[rg.col_off + c];
+        const GridRow rr = rrows[rg.row_off + r];
+        float x, y;
+        sph_to_2d(g, rr.sz, rr.cz, cc.ca, cc.sa, x, y);
+        if (x < 0) x = 0;
+        if (x > 1) x = 1;
+        if (y < 0) y = 0;
+        if (y > 1) y = 1;
+        sidx[rg.soff + s] = make_int2((int)tile_index(g, x, y),
+                                      (int)emap_index(cc.az, rr.zen, ew, eh, ec));
+    }
+}
+
+void launch_regidx(hipStream_t s, const TileGeom* geom, const RegGrid* grids,
+                   const GridCol* rcols, const GridRow* rrows, int ntiles, int max_samples,
+                   int ew, int eh, int ec, int2* sidx)
+{
+    unsigned gx = (unsigned)((max_samples + 255) / 256);
+    if (gx < 1) gx = 1;
+    if (gx > 1024) gx = 1024;
+    hipLaunchKernelGGL(k_regidx, dim3(gx, (unsigned)ntiles), dim3(256), 0, s, geom, grids, rcols,
+                       rrows, ew, eh, ec, sidx);
 }
 
 int register_sums_per_tile() { return kRegSums; }
