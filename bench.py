@@ -68,6 +68,10 @@ def parse():
     ap.add_argument("--same-device", action="store_true",
                     help="every rank on cuda:0 (multi-process rehearsal on a one-GPU box; "
                          "use with --backend gloo)")
+    ap.add_argument("--sample-dump", default=None, metavar="DIR",
+                    help="every rank writes DIR/rank<r>.npz: the inputs (ground truth, baseline, "
+                         "depth-net responses) and the fused u16 of one sampled panorama of its "
+                         "batch, for an oracle check outside the bench (tests/test_gpu_c4.py)")
     ap.add_argument("--stand-in", action="store_true",
                     help="test hook (tests/test_bench_dist.py): the launcher, seeding and timing "
                          "path with a CPU stand-in step over gloo; no GPU is touched")
@@ -670,24 +674,40 @@ def main():
     stages = {k: {"ms_per_step": v[0] / nprof,
                   "GBps": (v[1] / (v[0] * 1e-3) / 1e9) if v[0] > 0 else 0.0,
                   "launches_per_step": v[2] / nprof} for k, v in prof.items()}
-    # sanity: outputs are populated, and equal to a fresh one-process fusion of the same batch
+    # sanity, on EVERY rank: its outputs are populated and equal, bit for bit, to a fresh
+    # one-process serial fusion of the same batch on a new context (warp + register + fuse);
+    # the flags of all ranks are gathered into bit_exact_all_ranks
     nz = int((out[0].view(torch.int16) != 0).sum().item())
-    bit_exact = None
-    if rank == 0:
-        fref = panofuse.Fuser(local)
-        fref.set_tiles(lay)
-        t_ref = torch.empty_like(tiles)
-        o_ref = torch.empty_like(out)
-        fref.warp_depth(gt, t_ref, resp)
-        fref.merge(emap, t_ref, o_ref, zr, coeffs=torch.empty_like(coeffs))
-        torch.cuda.synchronize()
-        bit_exact = bool(torch.equal(o_ref, out))
-        del fref, t_ref, o_ref
-    per_rank = None
-    if world > 1:  # each rank's seed block and its own time (the line's value uses the MAX)
+    fref = panofuse.Fuser(local)
+    fref.set_tiles(lay)
+    t_ref = torch.empty_like(tiles)
+    o_ref = torch.empty_like(out)
+    fref.warp_depth(gt, t_ref, resp)
+    fref.merge(emap, t_ref, o_ref, zr, coeffs=torch.empty_like(coeffs))
+    torch.cuda.synchronize()
+    fref.synchronize()
+    bit_exact = bool(torch.equal(o_ref, out))
+    del fref, t_ref, o_ref
+    # one sampled panorama per rank (a different position in each rank's block), hashed; with
+    # --sample-dump its inputs and result are written for the oracle check in the tests
+    import hashlib
+    si = (rank * 37 + 5) % B
+    sample_u16 = out[si].cpu().numpy().view(np.uint16)
+    sample = {"index": si, "seed": seeds[si],
+              "sha256": hashlib.sha256(sample_u16.tobytes()).hexdigest()}
+    if args.sample_dump:
+        os.makedirs(args.sample_dump, exist_ok=True)
+        np.savez(os.path.join(args.sample_dump, f"rank{rank}.npz"), seed=np.int64(seeds[si]),
+                 gt=gt[si].cpu().numpy(), emap=emap[si].cpu().numpy(),
+                 resp=pf_synth.responses([seeds[si]], lay.ntiles), out=sample_u16)
+    per_rank = [{"rank": rank, "seed0": seeds[0], "seedN": seeds[-1], "elapsed_s": mine_s,
+                 "bit_exact": bit_exact, "sample": sample}]
+    if world > 1:  # each rank's seed block, its own time (the line's value uses the MAX), checks
         per_rank = [None] * world
         dist.all_gather_object(per_rank, {"rank": rank, "seed0": seeds[0], "seedN": seeds[-1],
-                                          "elapsed_s": mine_s})
+                                          "elapsed_s": mine_s, "bit_exact": bit_exact,
+                                          "sample": sample})
+    bit_exact_all = all(bool(p["bit_exact"]) for p in per_rank)
 
     if rank == 0:
         line = {
@@ -780,11 +800,14 @@ def main():
             "smoothing_ablation": dict(smooth, note="pf_solve_smoothing (SolveDepthBySmoothing, "
                                        "500 Gauss-Seidel sweeps near tile edges), outside the step"),
             "bit_exact_vs_one_process": bit_exact,
+            # every rank's own batch against a fresh one-process fusion (C4: 8 checks)
+            "bit_exact_all_ranks": bit_exact_all,
             "c2_batch1_ms": c2["median_ms"] if c2 else None,
             "c2_batch1": c2,
             "c5_one_gpu": c5,
             "backend": args.backend if world > 1 else None,
-            "per_rank": per_rank,
+            "per_rank": per_rank if world > 1 else None,
+            "sample_pano": per_rank[0]["sample"],
         }
         if not args.no_cpu_baseline:
             line["cpu_baseline"] = cpu_baseline(args.cpu_seconds)
@@ -792,8 +815,9 @@ def main():
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()
-    if rank == 0 and not bit_exact:
-        sys.exit("the fused batch differs from a fresh one-process fusion")
+    if not bit_exact_all:
+        sys.exit(f"rank {rank}: a rank's fused batch differs from a fresh one-process fusion "
+                 f"({[p['rank'] for p in per_rank if not p['bit_exact']]})")
 
 
 if __name__ == "__main__":

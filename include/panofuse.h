@@ -30,9 +30,10 @@ extern "C" {
 #define PF_EHIP (-3)       /* HIP runtime error */
 #define PF_ESTATE (-4)     /* call order (e.g. no tiles set) */
 #define PF_EDEGENERATE (-5) /* a tile box with x0 == x1 (the reference loops forever there) */
-#define PF_ETIMEOUT (-6)   /* a resident-kernel hand-off wait timed out: the fusion's output is
-                            * invalid (see pf_jres_errors); reported by pf_synchronize, and by
-                            * the next pf_fuse / pf_merge once the timed-out fusion has finished */
+#define PF_ETIMEOUT (-6)   /* a resident-kernel hand-off wait timed out: the output of that
+                            * fusion (or row-band smoothing) is invalid (see pf_jres_errors);
+                            * reported by pf_synchronize, and by the next pf_fuse / pf_merge /
+                            * pf_solve_smoothing once the timed-out call has finished */
 
 typedef struct pf_ctx pf_ctx;
 
@@ -124,7 +125,9 @@ int pf_warp_rgb(pf_ctx* ctx, const uint8_t* pano, int pw, int ph, int batch, uin
  * overwrites an earlier one), 500 in-place Gauss-Seidel smoothing iterations on the pixels within
  * 10 of a tile-box edge in rows [floor(h*zr0/MYPI), ceil(h*zr1/MYPI)], u16 quantisation.
  * tiles: [batch][tile_elems] float (channel 0 read); coeffs: NULL, or [batch][ntiles][4] applied
- * as Depth2DepthTransform on the fly; out: [batch][out_h][out_w] u16.  Bit-exact. */
+ * as Depth2DepthTransform on the fly; out: [batch][out_h][out_w] u16.  Bit-exact.  The
+ * row-band form's hand-off waits are bounded: a timeout makes the output invalid and is reported
+ * as PF_ETIMEOUT by pf_synchronize (or the next call), as for the fusions. */
 int pf_solve_smoothing(pf_ctx* ctx, const float* tiles, const float* coeffs, int batch,
                        int out_w, int out_h, float zr0, float zr1, uint16_t* out);
 
@@ -223,6 +226,11 @@ int pf_jres_errors(pf_ctx* ctx);
  * (spin_log2 in [4, 24]), so the neighbouring blocks time out: the fusion must then report
  * PF_ETIMEOUT.  The launch after that runs normally. */
 int pf_debug_jres_fault(pf_ctx* ctx, int spin_log2);
+/* The same hook for the context's NEXT row-band smoothing launch (pf_solve_smoothing with more
+ * than one row block per panorama): row block 0 never publishes its steps, its neighbour's wait
+ * gives up after 2^spin_log2 polls (and stops waiting for the rest of the launch), and
+ * pf_synchronize / the next call reports PF_ETIMEOUT. */
+int pf_debug_smooth_fault(pf_ctx* ctx, int spin_log2);
 
 /* ---- parity probes (bit-exact index maps) ----
  * For level `level` of out_w: per covered pixel and tap k (5 taps in std::map order), the
@@ -263,11 +271,15 @@ int pf_error_metrics(pf_ctx* ctx, const float* gt, int gw, int gh, int gc, const
                      const uint16_t* given16, int w, int h, int given_c, int batch, float zr0,
                      float zr1, int align_way, int cap_depth, pf_metrics* out);
 /* Summation order of the means (mse, mae, mre, mselog) and of the least-squares sums:
- *   PF_METRICS_SEQUENTIAL (default) -- the reference's: row-major, float accumulators (mse and
- *     mselog through a double add, Depth.cpp:2119-2123, 2178-2186); bit-exact to it.  The
- *     per-pixel terms are computed in parallel, one wave per panorama adds them in order.
- *   PF_METRICS_TREE -- fp64 partial sums in a fixed tree: deterministic, ~10x faster at large
- *     batches, means within 1e-5 relative of exact fp64 sums (not of the reference's floats). */
+ *   PF_METRICS_TREE (default) -- fp64 partial sums in a fixed tree: deterministic, 1.1 ms per
+ *     64 panoramas at C3, means within 1e-5 relative of exact fp64 sums (and within 1e-2 of
+ *     the reference's drifting float sums).
+ *   PF_METRICS_SEQUENTIAL -- opt-in "bit-exact means": the reference's order, row-major float
+ *     accumulators (mse and mselog through a double add, Depth.cpp:2119-2123, 2178-2186);
+ *     bit-exact to it.  The per-pixel terms are computed in parallel, one wave per panorama
+ *     adds them in order: one dependent add chain, ~24 ms per call at any batch.
+ * The facade (include/pf_depth.h) takes PF_METRICS_ORDER=sequential from the environment;
+ * panofuse_main has --metrics-order. */
 #define PF_METRICS_TREE 0
 #define PF_METRICS_SEQUENTIAL 1
 int pf_set_metrics_order(pf_ctx* ctx, int order);

@@ -197,3 +197,12 @@ def cli_jpeg_inputs(d, quality=95):
         names.append(fn)
         off += 512 * 494
     return raw, names, base_fn, gt
+
+
+def export_pano(h=512, w=1024, seed=9):
+    """The RGB panorama of tests/test_gpu_cli.py::test_export_rgb_tiles (and of its stb fixture,
+    tests/golden/export_rgb_stb.json): a horizontal and a vertical ramp plus a noise channel."""
+    rs = np.random.RandomState(seed)
+    yy, xx = np.mgrid[0:h, 0:w]
+    return np.stack([(xx * 255 // (w - 1)), (yy * 255 // (h - 1)),
+                     rs.randint(0, 256, size=(h, w))], -1).astype(np.uint8)

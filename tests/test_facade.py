@@ -25,7 +25,9 @@ PKG = os.path.join(ROOT, "wacv2023-high-resolution-depth-estimation-for-panorama
                          "perspective-map-registrations_amd")
 BIN = os.path.join(PKG, "bin", "pf_facade_check")
 # The same caller built against the reference's own ILMBase.h (IlmBase 2.2 Imath::Vec2/Vec4<float>)
-# by oracle/Makefile where /root/reference exists; it travels to the GPU box in oracle/_ref/.
+# by oracle/Makefile where /root/reference exists.  It stays in this container (oracle/_ref/ is
+# gpurun-ignored): here the link and its undefined symbols are checked (nm), and its GPU runs
+# skip on the GPU box, where the stand-in caller covers the same calls.
 IMATH_BIN = os.path.join(ROOT, "oracle", "_ref", "pf_facade_check_imath")
 CALLERS = ["standin", "imath"]
 ZR = PL.ZENITH_RANGE

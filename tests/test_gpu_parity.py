@@ -1,9 +1,10 @@
 """GPU parity: the HIP path (through the C-ABI) against the CPU oracle on identical inputs.
 
-Bars: bit-exact for tile index maps, level seeds, Laplacian targets,
-Jacobi buffers, registration coefficients and the u16 output; the E->P warps, whose atan2 is
-evaluated on the device in fp64 where the oracle calls glibc atan2f, within 2e-6 absolute (depth)
-and 1 LSB (RGB u8).  Oracle parity against the reference itself is unpinned (pf_oracle.h).
+Bars: bit-exact for everything -- tile index maps, level seeds, Laplacian
+targets, Jacobi buffers, registration coefficients, the u16 output, and the E->P warps (depth
+tiles and RGB tiles: their coordinate maps are built on the host with glibc atan2f / atan2, as
+the reference and the oracle call them, so the warped tiles are array_equal to the oracle's).
+Oracle parity against the reference itself is unpinned (pf_oracle.h).
 """
 import numpy as np
 import pytest

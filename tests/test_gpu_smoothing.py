@@ -105,3 +105,39 @@ def test_smoothing_row_blocks_equal(fuser, nb, monkeypatch):
     if nb == "7":
         r0 = O.solve_smoothing(tiles, np.ascontiguousarray(data[0]), out_w, out_w // 2, ZR)
         assert np.array_equal(got.cpu().numpy().view(np.uint16)[0], r0)
+
+
+def test_smoothing_timeout_is_reported(fuser, monkeypatch):
+    """a row-band hand-off wait that times out must surface as PF_ETIMEOUT on the
+    smoothing call's own report (pf_synchronize, or the next call), not as a silently wrong
+    output or a later fusion's failure.  The fault hook makes row block 0 withhold its step
+    flags in one launch, waits bounded at 2^10 polls; after a timeout a workgroup stops waiting,
+    so the faulty launch still ends quickly.  The launches after it are bit-exact again."""
+    lay, tiles, data, out_w = _tiles("C2", 4, 2)
+    fuser.set_tiles(lay)
+    t = torch.from_numpy(data).to(DEV)
+    monkeypatch.setenv("PF_SMOOTH_BAND", "7")
+    ref = torch.zeros((2, out_w // 2, out_w), dtype=torch.int16, device=DEV)
+    fuser.solve_smoothing(t, ref, ZR)
+    fuser.synchronize()
+    # 1. reported by pf_synchronize
+    got = torch.zeros_like(ref)
+    fuser.debug_smooth_fault(10)
+    fuser.solve_smoothing(t, got, ZR)
+    with pytest.raises(panofuse.PanofuseError) as e:
+        fuser.synchronize()
+    assert e.value.code == panofuse.PF_ETIMEOUT and "timed out" in str(e.value)
+    # 2. the next launch runs normally and is bit-exact
+    fuser.solve_smoothing(t, got, ZR)
+    fuser.synchronize()
+    assert torch.equal(got, ref)
+    # 3. reported by the next smoothing call once the faulty one has finished
+    fuser.debug_smooth_fault(10)
+    fuser.solve_smoothing(t, got, ZR)
+    torch.cuda.synchronize()
+    with pytest.raises(panofuse.PanofuseError) as e:
+        fuser.solve_smoothing(t, got, ZR)
+    assert e.value.code == panofuse.PF_ETIMEOUT
+    fuser.solve_smoothing(t, got, ZR)
+    fuser.synchronize()
+    assert torch.equal(got, ref)

@@ -38,6 +38,34 @@ def main():
     np.savez_compressed(dst, **out)
     print(dst, os.path.getsize(dst), "bytes,", len(out), "arrays")
     cli_fixture()
+    export_fixture()
+
+
+def export_fixture():
+    """SHA-256 of the reference's own stbi_write_jpg (quality argument = the row stride,
+    Main.cpp:320) applied to the oracle's RGB tiles of tests/test_gpu_cli.py::
+    test_export_rgb_tiles (LeReS layout at 1024 x 988, panorama codec_cases.export_pano()):
+    tests/golden/export_rgb_stb.json.  The GPU test compares its exported files with these
+    hashes, so the reference-built codec never has to travel to the GPU box."""
+    import hashlib
+    import json
+    sys.path.insert(0, os.path.join(ROOT, "wacv2023-high-resolution-depth-estimation-for-"
+                                          "panoramas-through-perspective-map-registrations_amd"))
+    import pf_layouts as PL
+    import pyoracle as O
+    lay = PL.leres_layout(1024, 988)
+    tiles_o, _ = O.make_tiles(lay)
+    ref = O.warp_rgb(CC.export_pano(), tiles_o)
+    n = 988 * 1024 * 3
+    rec = {"layout": "LeReS 1024x988", "quality": 1024 * 3, "tiles": []}
+    with tempfile.TemporaryDirectory() as d:
+        for t in range(lay.ntiles):
+            fn = os.path.join(d, "t.jpg")
+            assert pystb.write_jpg(fn, ref[t * n:(t + 1) * n].reshape(988, 1024, 3), 1024 * 3)
+            rec["tiles"].append(hashlib.sha256(open(fn, "rb").read()).hexdigest())
+    dst = os.path.join(ROOT, "tests", "golden", "export_rgb_stb.json")
+    json.dump(rec, open(dst, "w"), indent=1)
+    print(dst, len(rec["tiles"]), "tiles")
 
 
 def cli_fixture():
@@ -65,4 +93,9 @@ def cli_fixture():
 
 
 if __name__ == "__main__":
-    main()
+    if sys.argv[1:] == ["export"]:  # only the export-tile hashes
+        if not pystb.available():
+            sys.exit("oracle/_ref/libstbref.so not built (needs /root/reference)")
+        export_fixture()
+    else:
+        main()

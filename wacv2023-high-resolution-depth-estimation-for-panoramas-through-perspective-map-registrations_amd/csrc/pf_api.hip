@@ -62,7 +62,7 @@ struct pf_ctx {
     // layout
     int ntiles = 0, tile_c = 1;
     int solver = PF_SOLVER_LM;  // degree-3 registration solver (pf_set_solver)
-    int metrics_order = PF_METRICS_SEQUENTIAL;  // pf_set_metrics_order
+    int metrics_order = PF_METRICS_TREE;  // pf_set_metrics_order
     std::vector<pf_window> fov, rng;
     std::vector<int> tw_h, th_h;
     bool layout_ok = false;  // the stored layout was set completely
@@ -108,6 +108,7 @@ struct pf_ctx {
     // jres_check reports a raised flag once as PF_ETIMEOUT and lowers it
     uint32_t* jres_err_h = nullptr;
     int jres_fault = 0;  // pf_debug_jres_fault: spin_log2 for the next resident launch (0: off)
+    int smooth_fault = 0;  // pf_debug_smooth_fault: spin_log2 for the next row-band smoothing
     int seed_key[5] = {0, 0, 0, 0, 0};
     // stage profiling
     struct Span {
@@ -408,6 +409,26 @@ static int jres_check(pf_ctx* c)
     return fail(c, PF_ETIMEOUT, "resident kernel (Jacobi level or row-band smoothing): "
                 "hand-off wait(s) timed out (%d resident-Jacobi timeouts so far on this context, "
                 "pf_jres_errors); the output of that call is invalid", pf_jres_errors(c));
+}
+
+// The coherent pinned PF_ETIMEOUT flag shared by the resident Jacobi kernel and the row-band
+// smoothing kernel: allocated and zeroed once (hipHostMalloc does not promise zeroed memory);
+// PF_JRES_ERRHOST=0 leaves it out (timeouts then only count into pf_jres_errors).
+static int ensure_err_host(pf_ctx* c)
+{
+    static const bool errhost = !(getenv("PF_JRES_ERRHOST") && atoi(getenv("PF_JRES_ERRHOST")) == 0);
+    if (c->jres_err_h || !errhost) return PF_OK;
+    HIPCHK(c, hipHostMalloc((void**)&c->jres_err_h, sizeof(uint32_t),
+                            hipHostMallocMapped | hipHostMallocCoherent));
+    __atomic_store_n(c->jres_err_h, 0u, __ATOMIC_RELEASE);
+    return PF_OK;
+}
+
+int pf_debug_smooth_fault(pf_ctx* c, int spin_log2)
+{
+    if (!c || spin_log2 < 4 || spin_log2 > 24) return PF_EINVAL;
+    c->smooth_fault = spin_log2;
+    return PF_OK;
 }
 
 int pf_debug_jres_fault(pf_ctx* c, int spin_log2)
@@ -1103,12 +1124,7 @@ static int jres_prepare(pf_ctx* c, const LevelDims& L, int batch, const JresPlan
                       (size_t)jp.K * L.w;
     if ((rc = ensure(c, c->jres_x, xb))) return rc;
     const size_t sb = sizeof(uint32_t) * (2 + (size_t)batch * jp.nb * jres_flags_per_block(jp.K));
-    static const bool errhost = !(getenv("PF_JRES_ERRHOST") && atoi(getenv("PF_JRES_ERRHOST")) == 0);
-    if (!c->jres_err_h && errhost) {
-        HIPCHK(c, hipHostMalloc((void**)&c->jres_err_h, sizeof(uint32_t),
-                                hipHostMallocMapped | hipHostMallocCoherent));
-        __atomic_store_n(c->jres_err_h, 0u, __ATOMIC_RELEASE);
-    }
+    if ((rc = ensure_err_host(c))) return rc;
     if (c->jres_sync.bytes < sb) {
         if ((rc = ensure(c, c->jres_sync, sb))) return rc;
         HIPCHK(c, hipMemsetAsync(c->jres_sync.p, 0, sb, c->stream));
@@ -1556,6 +1572,7 @@ int pf_solve_smoothing(pf_ctx* c, const float* tiles, const float* coeffs, int b
 {  // SolveDepthBySmoothing (Depth.cpp:1773-1878)
     int rc;
     if ((rc = check_common(c, batch))) return rc;
+    if ((rc = jres_check(c))) return rc;  // an earlier call's timeout, once it has landed
     if (!tiles || !out) return fail(c, PF_EINVAL, "tiles/out is NULL");
     if (out_w < 3 || out_h < 3 || (long long)out_w * out_h >= (1LL << 31))
         return fail(c, PF_EINVAL, "output %dx%d out of range", out_w, out_h);
@@ -1703,9 +1720,7 @@ int pf_solve_smoothing(pf_ctx* c, const float* tiles, const float* coeffs, int b
                     c->sm_tk = 0;
                     c->sm_fb = 1;
                 }
-                if (!c->jres_err_h)
-                    HIPCHK(c, hipHostMalloc((void**)&c->jres_err_h, sizeof(uint32_t),
-                                            hipHostMallocMapped | hipHostMallocCoherent));
+                if ((rc = ensure_err_host(c))) return rc;
                 SmoothSync S{};
                 uint32_t* w32 = (uint32_t*)c->sm_sync.p;
                 S.ticket = w32;
@@ -1714,6 +1729,12 @@ int pf_solve_smoothing(pf_ctx* c, const float* tiles, const float* coeffs, int b
                 S.err_host = c->jres_err_h;
                 S.tbase = c->sm_tk;
                 S.fbase = c->sm_fb;
+                S.spin_log2 = 22;
+                if (c->smooth_fault) {  // pf_debug_smooth_fault: this launch only
+                    S.fault = 1;
+                    S.spin_log2 = c->smooth_fault;
+                    c->smooth_fault = 0;
+                }
                 c->sm_tk += (uint32_t)(batch * nb);
                 c->sm_fb += (uint32_t)(c->sm_smax - c->sm_smin + 2);
                 launch_smooth_band(c->stream, (const int*)c->sm_list.p, (const int*)c->sm_off.p,
@@ -1744,18 +1765,31 @@ int pf_warp_depth(pf_ctx* c, const float* pano, int pw, int ph, int batch,
     if (c->wmap_pw != pw || c->wmap_ph != ph) {
         if ((rc = ensure(c, c->wmap, sizeof(uint32_t) * npix))) return rc;
         if ((rc = ensure(c, c->wfxy, sizeof(float) * 2 * npix))) return rc;
-        // corners and weights on the host (glibc atan2f: the reference's bits), tile by tile
-        std::vector<uint32_t> wxy((size_t)c->npix_max);
-        std::vector<float> wf(2 * (size_t)c->npix_max);
-        for (int p = 0; p < c->ntiles; p++) {
-            const TileGeom& g = c->geom_h[p];
-            const size_t n = (size_t)g.w * g.h;
-            warp_coords_host(g, pw, ph, wxy.data(), wf.data());
-            HIPCHK(c, hipMemcpyAsync((uint32_t*)c->wmap.p + g.pix_off, wxy.data(), 4 * n,
+        // corners and weights on the host (glibc atan2f: the reference's bits).  Tiles are
+        // built into one host staging run of up to kStagePix pixels (C3's whole layout; C5 in
+        // 6 runs), uploaded with one copy per array and one synchronisation per run.  This first
+        // call per panorama size blocks the host (the staging memory is reused).
+        const size_t kStagePix = (size_t)1 << 24;
+        const size_t cap = std::max((size_t)c->npix_max, std::min((size_t)npix, kStagePix));
+        std::vector<uint32_t> wxy(cap);
+        std::vector<float> wf(2 * cap);
+        for (int p0 = 0; p0 < c->ntiles;) {
+            const size_t off0 = (size_t)c->geom_h[p0].pix_off;
+            size_t n = 0;
+            int p1 = p0;
+            for (; p1 < c->ntiles; p1++) {
+                const TileGeom& g = c->geom_h[p1];
+                const size_t m = (size_t)g.w * g.h;
+                if (p1 > p0 && n + m > cap) break;
+                warp_coords_host(g, pw, ph, wxy.data() + n, wf.data() + 2 * n);
+                n += m;
+            }
+            HIPCHK(c, hipMemcpyAsync((uint32_t*)c->wmap.p + off0, wxy.data(), 4 * n,
                                      hipMemcpyHostToDevice, c->stream));
-            HIPCHK(c, hipMemcpyAsync((float*)c->wfxy.p + 2 * (size_t)g.pix_off, wf.data(), 8 * n,
+            HIPCHK(c, hipMemcpyAsync((float*)c->wfxy.p + 2 * off0, wf.data(), 8 * n,
                                      hipMemcpyHostToDevice, c->stream));
-            HIPCHK(c, hipStreamSynchronize(c->stream));  // the host rows are reused
+            HIPCHK(c, hipStreamSynchronize(c->stream));  // the staging run is reused
+            p0 = p1;
         }
         launch_warp_boxes(c->stream, (const TileGeom*)c->geom.p, (WarpPatch*)c->wpatch.p,
                           c->npatch, pw, ph, (uint32_t*)c->wmap.p);
@@ -1784,14 +1818,26 @@ int pf_warp_rgb(pf_ctx* c, const uint8_t* pano, int pw, int ph, int batch, uint8
     if (c->rgb_pw != pw || c->rgb_ph != ph) {  // the taps of this size, on the host (glibc)
         const long long npix = c->tile_elems / c->tile_c;
         if ((rc = ensure(c, c->rgbtap, sizeof(RgbTap) * npix))) return rc;
-        std::vector<RgbTap> taps((size_t)c->npix_max);
-        for (int p = 0; p < c->ntiles; p++) {
-            const TileGeom& g = c->geom_h[p];
-            rgb_taps_host(c->cams_h[p], g.w, g.h, pw, ph, taps.data());
-            HIPCHK(c, hipMemcpyAsync((RgbTap*)c->rgbtap.p + g.pix_off, taps.data(),
-                                     sizeof(RgbTap) * (size_t)g.w * g.h, hipMemcpyHostToDevice,
-                                     c->stream));
+        // staged as the depth warp's corner tables: runs of up to 2^24 pixels, one copy and
+        // one synchronisation per run (this first call per panorama size blocks the host)
+        const size_t kStagePix = (size_t)1 << 24;
+        const size_t cap = std::max((size_t)c->npix_max, std::min((size_t)npix, kStagePix));
+        std::vector<RgbTap> taps(cap);
+        for (int p0 = 0; p0 < c->ntiles;) {
+            const size_t off0 = (size_t)c->geom_h[p0].pix_off;
+            size_t n = 0;
+            int p1 = p0;
+            for (; p1 < c->ntiles; p1++) {
+                const TileGeom& g = c->geom_h[p1];
+                const size_t m = (size_t)g.w * g.h;
+                if (p1 > p0 && n + m > cap) break;
+                rgb_taps_host(c->cams_h[p1], g.w, g.h, pw, ph, taps.data() + n);
+                n += m;
+            }
+            HIPCHK(c, hipMemcpyAsync((RgbTap*)c->rgbtap.p + off0, taps.data(),
+                                     sizeof(RgbTap) * n, hipMemcpyHostToDevice, c->stream));
             HIPCHK(c, hipStreamSynchronize(c->stream));
+            p0 = p1;
         }
         c->rgb_pw = pw;
         c->rgb_ph = ph;

@@ -45,6 +45,11 @@ pf_ctx* facade_ctx()
         std::cout << "[panofuse] pf_create(" << dev << ") failed: no usable HIP device" << std::endl;
         return nullptr;
     }
+    // ErrorData / ErrorEmap summation order: the fast fp64 tree by default;
+    // PF_METRICS_ORDER=sequential gives the reference's row-major float sums (bit-exact means,
+    // ~24 ms per call: one dependent add chain; panofuse_main --metrics-order sequential)
+    const char* mo = std::getenv("PF_METRICS_ORDER");
+    if (mo && std::strcmp(mo, "sequential") == 0) pf_set_metrics_order(c, PF_METRICS_SEQUENTIAL);
     ctxs[dev] = c;
     return c;
 }
@@ -536,6 +541,9 @@ bool SolveDepthBySmoothing(std::vector<PerspectiveMap>& pmaps, unsigned short* d
                                      zr[1], dout.as<uint16_t>()),
                "pf_solve_smoothing"))
         return false;
+    // a row-band hand-off that timed out makes the result invalid: report it here, on this
+    // call (PF_ETIMEOUT), as SolveDepthAll does for the fusion
+    if (!pf_ok(c, pf_synchronize(c), "SolveDepthBySmoothing")) return false;
     return hip_ok(hipMemcpy(data, dout.p, no * 2, hipMemcpyDeviceToHost), "download");
 }
 

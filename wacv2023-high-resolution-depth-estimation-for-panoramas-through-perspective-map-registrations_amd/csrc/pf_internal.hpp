@@ -334,6 +334,8 @@ struct SmoothSync {
     uint32_t* err;
     uint32_t* err_host;  // coherent pinned flag (PF_ETIMEOUT), may be null
     uint32_t tbase, fbase;
+    int spin_log2;       // a neighbour wait gives up (counted, flagged) after 2^spin_log2 polls
+    int fault;           // pf_debug_smooth_fault: row block 0 never publishes its steps
 };
 void launch_smooth_band(hipStream_t s, const int* list, const int* off, int nk, int nb, int w,
                         int h, int smin, int smax, int iters, float* buf, int batch,

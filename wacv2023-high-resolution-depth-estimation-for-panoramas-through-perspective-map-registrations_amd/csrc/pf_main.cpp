@@ -1,12 +1,16 @@
 // panofuse_main -- the reference's command line (Main.cpp:864-895) for the fusion path:
 //   panofuse_main 0 <rgb_dir> <gt_dir> <baseline_dir> <result_dir> [--tiles DIR]
 //                 [--ext auto|jpg|png] [--width W] [--device D] [--shard R/N]
+//                 [--metrics-order tree|sequential]
 //   panofuse_main export <rgb_dir> <tile_dir> [--device D]
 // "export" is the tile render of mode 0 (Main.cpp:399-430, SaveCubeMap :242-326) on the GPU:
 // each RGB panorama becomes the 15 LeReS perspective tiles the depth network consumes.
 // Mode 0 = CreateDepthPanoramas (Main.cpp:331-687) minus the OpenGL tile export: the perspective
 // depth tiles are read from --tiles (default "test_images", the reference's LeReS folder) named
 // <raw>.<a0>_<a1>_<z0>_<z1>.<ext>; "auto" takes .jpg when present, else .png (MiDaS naming).
+// --metrics-order: the .aligned.txt means in the fast fp64-tree order (default) or in the
+// reference's row-major float order (sequential: the reference's printed digits, ~24 ms more
+// per ErrorData call).
 #include "../../include/pf_depth.h"
 
 #include <hip/hip_runtime.h>
@@ -21,7 +25,8 @@ int main(int argc, char* argv[])
     if (argc < 2) {
         std::cout << "usage: " << argv[0]
                   << " 0 <rgb_dir> <gt_dir> <baseline_dir> <result_dir> [--tiles DIR]"
-                     " [--ext auto|jpg|png] [--width W] [--device D] [--shard R/N]\n       "
+                     " [--ext auto|jpg|png] [--width W] [--device D] [--shard R/N]"
+                     " [--metrics-order tree|sequential]\n       "
                   << argv[0] << " export <rgb_dir> <tile_dir> [--device D]" << std::endl;
         return 0;
     }
@@ -52,6 +57,13 @@ int main(int argc, char* argv[])
         else if (k == "--ext") ext = v;
         else if (k == "--width") width = std::atoi(v.c_str());
         else if (k == "--device") device = std::atoi(v.c_str());
+        else if (k == "--metrics-order") {
+            if (v != "tree" && v != "sequential") {
+                std::cout << "bad --metrics-order " << v << " (want tree or sequential)" << std::endl;
+                return 2;
+            }
+            setenv("PF_METRICS_ORDER", v.c_str(), 1);  // read when the facade's context is made
+        }
         else if (k == "--shard") {  // R/N: one process per GPU over the sorted folder
             if (std::sscanf(v.c_str(), "%d/%d", &shard, &nshards) != 2 || nshards < 1 ||
                 shard < 0 || shard >= nshards) {

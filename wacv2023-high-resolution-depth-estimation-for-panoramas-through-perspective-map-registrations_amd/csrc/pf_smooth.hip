@@ -182,7 +182,9 @@ __global__ void __launch_bounds__(kSB) k_smooth_band(float* __restrict__ buf,
                                                      int iters, SmoothSync S)
 {
     __shared__ uint32_t lds_ticket;
+    __shared__ int lds_gave_up;
     const int tid = threadIdx.x;
+    if (tid == 0) lds_gave_up = 0;
     if (tid == 0) lds_ticket = __hip_atomic_fetch_add(S.ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     __syncthreads();
     const uint32_t tk = __builtin_amdgcn_readfirstlane(lds_ticket - S.tbase);
@@ -190,8 +192,11 @@ __global__ void __launch_bounds__(kSB) k_smooth_band(float* __restrict__ buf,
     const auto B = smooth_rsrc(buf + (long long)pano * npx, (uint32_t)(npx * 4));
     uint32_t* const flags = S.flags + (long long)pano * nb;
     const int* const offb = off + (long long)blk * 2 * (nk + 1);
+    // after one timed-out wait this workgroup stops waiting: the call's output is already invalid
+    // (reported as PF_ETIMEOUT), and every later step would otherwise wait out its own limit
+    bool gave_up = false;
     for (int s = smin; s <= smax; s++) {
-        if (s > smin) {  // both neighbouring blocks finished step s-1
+        if (s > smin && !gave_up) {  // both neighbouring blocks finished step s-1
             if (tid == 0) {
                 const uint32_t want = S.fbase + (uint32_t)(s - smin);  // step s-1 done
                 for (int nbj = blk - 1; nbj <= blk + 1; nbj += 2) {
@@ -199,15 +204,17 @@ __global__ void __launch_bounds__(kSB) k_smooth_band(float* __restrict__ buf,
                     int spins = 0;
                     while ((int)(__hip_atomic_load(&flags[nbj], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) - want) < 0) {
                         __builtin_amdgcn_s_sleep(1);
-                        if (++spins > (1 << 22)) {
+                        if (++spins > (1 << S.spin_log2)) {
                             __hip_atomic_fetch_add(S.err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                             if (S.err_host) __hip_atomic_store(S.err_host, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                            lds_gave_up = 1;
                             break;
                         }
                     }
                 }
             }
             __syncthreads();
+            gave_up = lds_gave_up != 0;  // uniform: read after the barrier
         }
         const int p = s & 1;
         const int dlo = s - 2 * (iters - 1);
@@ -227,7 +234,7 @@ __global__ void __launch_bounds__(kSB) k_smooth_band(float* __restrict__ buf,
         }
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
-        if (tid == 0) {
+        if (tid == 0 && !(S.fault && blk == 0)) {  // fault hook: block 0 withholds its flag
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             __hip_atomic_store(&flags[blk], S.fbase + (uint32_t)(s - smin) + 1u, __ATOMIC_RELAXED,
                                __HIP_MEMORY_SCOPE_AGENT);

@@ -29,9 +29,10 @@ EXPORTS = [
     "pf_fuse_border", "pf_fuse_band_plan", "pf_fuse_band_pass", "pf_fuse_multicover",
     "pf_fuse_multicover_patch", "pf_solve_smoothing", "pf_set_metrics_order",
     "pf_jres_errors", "pf_set_jacobi_engine", "pf_stream_wait_level", "pf_debug_jres_fault",
-    "pf_probe_warp_coords", "pf_probe_rgb_taps",
+    "pf_probe_warp_coords", "pf_probe_rgb_taps", "pf_debug_smooth_fault",
 ]
-NEW_R4 = {"pf_debug_jres_fault", "pf_probe_warp_coords", "pf_probe_rgb_taps"}
+NEW_R4 = {"pf_debug_jres_fault", "pf_probe_warp_coords", "pf_probe_rgb_taps",
+          "pf_debug_smooth_fault"}
 METRICS_ORDERS = {"tree": 0, "sequential": 1}  # PF_METRICS_*; "sequential" = the reference's
 SOLVERS = {"normal": 0, "lm": 1}  # PF_SOLVER_*; "lm" = the reference's Ceres LM (default)
 
@@ -105,7 +106,7 @@ def load():
     L.pf_profile_enable.argtypes = [vp, ip]
     L.pf_jres_errors.argtypes = [vp]
     # (entry points added after round 3: an A/B variant built from older sources may lack them)
-    for name, at in (("pf_debug_jres_fault", [vp, ip]),
+    for name, at in (("pf_debug_jres_fault", [vp, ip]), ("pf_debug_smooth_fault", [vp, ip]),
                      ("pf_probe_warp_coords", [C.POINTER(Window), ip, ip, ip, ip, vp, vp]),
                      ("pf_probe_rgb_taps", [C.POINTER(Window), ip, ip, ip, ip, vp])):
         if hasattr(L, name):
@@ -232,8 +233,8 @@ class Fuser:
                                     float(zr[0]), float(zr[1]), _ptr(coeffs), _ptr(out)))
 
     def set_metrics_order(self, order):
-        """"sequential" (default): the reference's float summation order, bit-exact; "tree":
-        fp64 partial sums (fast, means within 1e-5 of exact sums)."""
+        """"tree" (default): fp64 partial sums (fast, means within 1e-5 of exact sums);
+        "sequential": the reference's float summation order, bit-exact means (~24 ms a call)."""
         self._check(self.L.pf_set_metrics_order(self.h, METRICS_ORDERS[order]))
 
     def solve_smoothing(self, tiles, out, zr, coeffs=None):
@@ -402,6 +403,11 @@ class Fuser:
         """Test hook: the next resident launch withholds row block 0's hand-off flag with waits
         bounded at 2^spin_log2 polls, so that fusion must report PF_ETIMEOUT."""
         self._check(self.L.pf_debug_jres_fault(self.h, int(spin_log2)))
+
+    def debug_smooth_fault(self, spin_log2=10):
+        """Test hook: in the next row-band smoothing, row block 0 never publishes its steps and
+        the waits give up after 2^spin_log2 polls, so that call must report PF_ETIMEOUT."""
+        self._check(self.L.pf_debug_smooth_fault(self.h, int(spin_log2)))
 
 
 def warp_coords(fov, tile_w, tile_h, pw, ph):
