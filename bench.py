@@ -177,10 +177,11 @@ def _metrics_traffic():
 def c5_measure(args, rank, world, local, dev, steps, warmup):
     """BASELINE config C5: one 8192x4096 panorama, 80 tiles of 1024^2 sharded over the ranks.
     Each rank warps and registers its own tiles (a sub-layout context writing into its slice of
-    the full tile block), scatters their targets per level (pf_fuse_partial); the (sum L, n) grids
-    are all-reduced over RCCL and every rank sweeps its row band with halo exchange per pass
-    (--c5-shard rows, pf_dist.fuse_row_sharded), or rank 0 sweeps the whole level (--c5-shard
-    tiles, pf_dist.fuse_tile_sharded).
+    the full tile block).  --c5-shard rows (pf_dist.fuse_row_sharded): per level each rank sums
+    its tiles' targets on the rows it sweeps and the rows its neighbours read, sends those rows
+    (a sparse reduce-scatter by band rows), sweeps its row band with a halo exchange per pass,
+    and the u16 rows are gathered to rank 0; --c5-shard tiles (pf_dist.fuse_tile_sharded): the
+    (sum L, n) grids are reduced to rank 0, which sweeps the whole level.
     One step = one panorama end to end; value = panoramas/s of the whole job."""
     import torch
     import torch.distributed as dist
@@ -213,6 +214,8 @@ def c5_measure(args, rank, world, local, dev, steps, warmup):
     out = torch.empty((out_w // 2, out_w), dtype=torch.int16, device=dev)
     nlevels = panofuse.level_info(out_w, out_w // 2, zr, 0)[5]
 
+    logs = []
+
     def step():
         if fs is not None:
             mine = tiles[:, off0:off1]
@@ -221,7 +224,8 @@ def c5_measure(args, rank, world, local, dev, steps, warmup):
         comm = pf_dist.TorchComm(dist, stage_host=args.backend == "gloo") if world > 1 else None
         if args.c5_shard == "rows":
             be = pf_dist.HipRowShardBackend(fz, emap, tiles, coeffs, out_w, zr, out.view(-1))
-            pf_dist.fuse_row_sharded(be, nlevels, lay.ntiles, rank, world, comm)
+            logs.append(pf_dist.ExchangeLog())
+            pf_dist.fuse_row_sharded(be, nlevels, lay.ntiles, rank, world, comm, logs[-1])
         else:
             be = pf_dist.HipTileShardBackend(fz, emap, tiles, coeffs, out_w, zr, out)
             pf_dist.fuse_tile_sharded(be, nlevels, lay.ntiles, rank, world, comm)
@@ -275,9 +279,31 @@ def c5_measure(args, rank, world, local, dev, steps, warmup):
             if i >= 2:
                 ts_.append(e0.elapsed_time(e1))
         one_call = sorted(ts_)[len(ts_) // 2]
+    model8 = None
+    if world == 1 and args.c5_shard == "rows":
+        # the bytes each of 8 ranks would send per panorama, from the same
+        # row arithmetic as the flow (pf_dist.exchange_model) with this GPU's band plans
+        be = pf_dist.HipRowShardBackend(fz, emap, tiles, coeffs, out_w, zr, out.view(-1))
+        dims = [be.dims(lv) for lv in range(nlevels)]
+        plans = [be.plan(lv, 8) for lv in range(nlevels)]
+        ext = [[be.tile_rows(lv, *pf_dist.shard_range(lay.ntiles, r, 8)) for r in range(8)]
+               for lv in range(nlevels)]
+        mc = [be.multicover_count(lv) for lv in range(nlevels)]
+        per = pf_dist.exchange_model(dims, plans, ext, 8, mc)
+        tot = [sum(d.values()) for d in per]
+        model8 = {"plans": plans, "per_rank": per, "max_rank_bytes": max(tot),
+                  "total_bytes": sum(tot),
+                  "bounds": [pf_dist.band_bounds(d[2], d[3], 8, e, max(p) + 1)
+                             for d, e, p in zip(dims, ext, plans)]}
     nz = int((out != 0).sum().item())
+    sent = logs[-1].sent if logs else None  # this rank's bytes of the last step, by kind
+    if world > 1 and sent is not None:
+        per = [None] * world
+        dist.all_gather_object(per, sent)
+        sent = per
     return {"value": steps / elapsed, "elapsed": elapsed, "mine_s": mine_s,
-            "bit_exact": bit_exact, "nonzero_px": nz, "one_call_ms": one_call}
+            "bit_exact": bit_exact, "nonzero_px": nz, "one_call_ms": one_call,
+            "bytes_sent_per_rank": sent, "model_8_ranks": model8}
 
 
 def run_c5(args, rank, world, local, dev):
@@ -294,12 +320,18 @@ def run_c5(args, rank, world, local, dev):
             "scaling": "strong", "vs_baseline": None, "dtype": "f32",
             "data": "synthetic (box-room scene, synthetic depth-net response)",
             "config": {"workload": "C5: one 8192x4096 panorama, 80 tiles of 1024x1024 (10x8), "
-                                   "2048x1024 baseline; tiles sharded over ranks, per-level "
-                                   + ("(sum L, n) all-reduce (RCCL), row-band Jacobi per rank "
-                                      "with halo exchange per pass" if args.c5_shard == "rows"
+                                   "2048x1024 baseline; tiles sharded over ranks, per level "
+                                   + ("the partial target rows each row band reads sent by their "
+                                      "tiles' rank (sparse reduce-scatter), row-band Jacobi per "
+                                      "rank with a halo exchange per pass, the previous level's "
+                                      "halo rows per level, u16 rows gathered to rank 0"
+                                      if args.c5_shard == "rows"
                                       else "(sum L, n) reduce to rank 0 (RCCL), Jacobi on rank 0"),
                        "parallelism": f"{'row-band' if args.c5_shard == 'rows' else 'tile'}-sharded x{world}"},
             "nonzero_px": nz, "bit_exact_vs_one_gpu": bit_exact,
+            "bytes_sent_per_rank": r["bytes_sent_per_rank"],
+            "model_8_ranks": r["model_8_ranks"],
+            "one_call_ms": r["one_call_ms"],
             "backend": args.backend if world > 1 else None,
             "elapsed_rank0_s": mine_s}), flush=True)
     if world > 1:
@@ -342,6 +374,46 @@ def c2_latency(local, dev, lay, zr, reps=7):
     return {"median_ms": times[len(times) // 2], "min_ms": times[0], "reps": reps,
             "workload": "C2: one 2048x1024 panorama, 20 tiles of 512^2: warp + registration + "
                         "3-level fusion + u16, hipEvents around each run (median)"}
+
+
+def rgb_warp_measure(local, dev, lay, B, reps=7):
+    """The E->P RGB warp (a18: SaveCubeMap's tile render, Main.cpp:242-326) at C3's shape: a
+    batch of B u8 RGB 2048x1024 panoramas into the 20 u8 RGB tiles of 512^2 each (pf_warp_rgb,
+    k_warp_rgb_box), hipEvents on the context's stream around each launch, median of `reps`
+    after a first call that builds the layout's taps and patch boxes.  Algorithmic bytes per
+    launch = B x (panorama read 3*pw*ph + tile write 3*sum(tw*th))."""
+    import torch
+
+    import panofuse
+    pw, ph = 2048, 1024
+    g = torch.Generator(device=dev).manual_seed(4242)
+    pano = torch.randint(0, 256, (B, ph, pw, 3), dtype=torch.uint8, device=dev, generator=g)
+    n = sum(int(lay.tile_w[i]) * int(lay.tile_h[i]) * 3 for i in range(lay.ntiles))
+    tiles = torch.empty((B, n), dtype=torch.uint8, device=dev)
+    f = panofuse.Fuser(local)
+    f.set_tiles(lay)
+    f.warp_rgb(pano, tiles)
+    torch.cuda.synchronize()
+    times = []
+    for _ in range(reps):
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        f.warp_rgb(pano, tiles)
+        e1.record()
+        torch.cuda.synchronize()
+        times.append(e0.elapsed_time(e1))
+    f.close()
+    times.sort()
+    ms = times[len(times) // 2]
+    nbytes = B * (3 * pw * ph + n)
+    ach = nbytes / (ms * 1e-3) / 1e9
+    del pano, tiles
+    return {"bound": "hbm", "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": ach / HBM_PEAK_GBS, "traffic": pmc_traffic("pf::k_warp_rgb_box"),
+            "kernel": "k_warp_rgb_box", "avg_launch_us": ms * 1e3, "min_launch_us": times[0] * 1e3,
+            "bytes_per_launch": nbytes,
+            "workload": f"C3 shape: {B} u8 RGB panoramas 2048x1024 -> 20 u8 RGB tiles of 512^2 "
+                        f"(pf_warp_rgb; outside the step, which warps depth)"}
 
 
 def rank_seeds(batch, rank):
@@ -649,6 +721,8 @@ def main():
         smooth[f"batch{nb}_ms"] = e0.elapsed_time(e1)
         del o_s
 
+    # the E->P RGB warp (the reference's own split, a18), outside the step, at C3's shape
+    rgbw = rgb_warp_measure(local, dev, lay, B) if not args.no_extra_configs else None
     # the other single-GPU BASELINE configs, for the record (outside the timed steps)
     c2 = c2_latency(local, dev, lay, zr) if not args.no_extra_configs else None
     c5 = None
@@ -657,6 +731,7 @@ def main():
         c5 = {"value": r5["value"], "unit": "panoramas/s", "ms_per_panorama": 1e3 / r5["value"],
               "steps": 3, "bit_exact_vs_one_gpu": r5["bit_exact"],
               "one_call_ms": r5["one_call_ms"],
+              "model_8_ranks": r5["model_8_ranks"],
               "one_call": "pf_warp_depth + pf_merge of the same panorama on one context "
                           "(hipEvents, median of 5): the library path without the sharded "
                           "path's per-level host orchestration",
@@ -781,6 +856,8 @@ def main():
                               "kernel": "k_warp_depth",
                               "avg_launch_us": (wms / wlaunch * 1e3) if wlaunch else None,
                               "bytes_per_launch": (wbytes / wlaunch) if wlaunch else None},
+            # the reference's E->P RGB tile render (a18) on the RGB panorama, outside the step
+            "roofline_warp_rgb": rgbw,
             "stages": stages,
             # metrics stage (outside the timed step): algorithmic bytes = one read of the
             # compared band of gt (4 B) and result (2 B) per pixel; the kernels make 4 passes

@@ -184,6 +184,28 @@ int pf_fuse_band_pass(pf_ctx* ctx, const float* emap, int ew, int eh, int ec, co
                       const float* lnorm, int src_mode, const float* src, float* dst,
                       uint16_t* out, int out_w, int out_h, float zr0, float zr1, int level, int T,
                       int row0, int row1);
+/* Row-restricted pieces of the sharded fusion (round 5): a rank computes only the rows it sweeps
+ * plus their halo, and the rows its own tiles contribute to its neighbours'.
+ * pf_fuse_partial_rows: pf_fuse_partial's sums of tiles [t0, t1) on rows [row0, row1) of the
+ *   level only (clipped to the band [h0, h1]; nothing is zeroed elsewhere).
+ * pf_fuse_coverage_rows: the coverage count n of ALL tiles on rows [row0, row1) (layout-only:
+ *   a rank counts its rows itself instead of receiving the other ranks' counts).
+ * pf_fuse_normalize_rows: pf_fuse_normalize on rows [row0, row1) only.
+ * pf_fuse_tile_rows: [*ymin, *ymax] = the rows where tiles [t0, t1) have non-zero partial sums at
+ *   this level (*ymin > *ymax when none); host only, from the cached boxes.
+ * pf_rows_add: dst[i] += src[i], i < n (a received partial-sum segment; exact where a pixel is
+ *   covered by at most two tiles -- the rest is pf_fuse_multicover's). */
+int pf_fuse_partial_rows(pf_ctx* ctx, const float* tiles, const float* coeffs, int t0, int t1,
+                         int out_w, int out_h, float zr0, float zr1, int level, int row0,
+                         int row1, float* lsum, float* cnt);
+int pf_fuse_coverage_rows(pf_ctx* ctx, int out_w, int out_h, float zr0, float zr1, int level,
+                          int row0, int row1, float* cnt);
+int pf_fuse_normalize_rows(pf_ctx* ctx, const float* lsum, const float* cnt, int out_w,
+                           int out_h, float zr0, float zr1, int level, int row0, int row1,
+                           float* lnorm);
+int pf_fuse_tile_rows(pf_ctx* ctx, int out_w, int out_h, float zr0, float zr1, int level, int t0,
+                      int t1, int* ymin, int* ymax);
+int pf_rows_add(pf_ctx* ctx, float* dst, const float* src, long long n);
 
 /* ---- stage timing (hipEvents on the context stream; replaces the reference's timeGetTime
  * brackets around registration and fusion, Depth.cpp:792-808, 907-916) ----

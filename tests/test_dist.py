@@ -149,10 +149,53 @@ class OracleRowBackend(OracleBackend):
         lv = self._lv(level)
         return torch.zeros(lv.w * lv.h, dtype=torch.float32)
 
-    def normalize(self, level, lsum, cnt):
+    def scratch(self, n):
+        return torch.zeros(n, dtype=torch.float32)
+
+    def _subset(self, level, t0, t1):
+        key = (level, t0, t1)
+        if not hasattr(self, "_sub"):
+            self._sub = {}
+        if key not in self._sub:
+            lv = self._lv(level)
+            if t1 > t0:
+                Ls, n = self.O.targets_subset(self.tiles, t0, t1, self.data, lv)
+            else:
+                Ls, n = np.zeros((lv.h, lv.w), np.float32), np.zeros((lv.h, lv.w), np.int32)
+            self._sub[key] = (np.ascontiguousarray(Ls).ravel(), np.ascontiguousarray(n).ravel())
+        return self._sub[key]
+
+    def _rows(self, level, row0, row1):
         lv = self._lv(level)
-        Ln = self.O.normalize(lsum.numpy(), cnt.numpy().astype(np.int32), lv)
-        return torch.from_numpy(np.ascontiguousarray(Ln).ravel().copy())
+        a, b = max(row0, lv.h0), min(row1, lv.h1 + 1)
+        return slice(a * lv.w, max(a, b) * lv.w)
+
+    def tile_rows(self, level, t0, t1):
+        lv = self._lv(level)
+        rows = np.nonzero(self._subset(level, t0, t1)[1].reshape(lv.h, lv.w).any(1))[0]
+        return (int(rows[0]), int(rows[-1])) if rows.size else (0, -1)
+
+    def partial_rows(self, level, t0, t1, row0, row1, lsum, cnt):
+        Ls, n = self._subset(level, t0, t1)
+        sl = self._rows(level, row0, row1)
+        lsum[sl] = torch.from_numpy(Ls[sl].copy())
+        cnt[sl] = torch.from_numpy(n[sl].astype(np.float32))
+
+    def coverage_rows(self, level, row0, row1, cnt):
+        _, n = self._subset(level, 0, len(self.tiles))
+        sl = self._rows(level, row0, row1)
+        cnt[sl] = torch.from_numpy(n[sl].astype(np.float32))
+
+    def rows_add(self, dst, src):
+        dst += src
+
+    def normalize_rows(self, level, lsum, cnt, row0, row1, lnorm):
+        lv = self._lv(level)
+        Ln = np.ascontiguousarray(self.O.normalize(lsum.numpy().reshape(lv.h, lv.w),
+                                                   cnt.numpy().astype(np.int32).reshape(lv.h, lv.w),
+                                                   lv)).ravel()
+        sl = self._rows(level, row0, row1)
+        lnorm[sl] = torch.from_numpy(Ln[sl].copy())
 
     def plan(self, level, nbands):
         it = self._lv(level).iters
@@ -198,9 +241,21 @@ def _row_worker(rank, world, port, q):
         emap = pf_synth.baseline_emap(seeds, 128, 64)[0].numpy()
         data = np.random.RandomState(9).rand(total).astype(np.float32)
         be = OracleRowBackend(O, PL, 512, emap, tiles, data)
-        pf_dist.fuse_row_sharded(be, 3, lay.ntiles, rank, world, pf_dist.TorchComm(dist))
-        ref, _ = O.solve_depth_all(emap, tiles, data, 512, PL.ZENITH_RANGE)
-        q.put((rank, bool(np.array_equal(be.out.numpy().view(np.uint16).reshape(256, 512), ref))))
+        log = pf_dist.ExchangeLog()
+        pf_dist.fuse_row_sharded(be, 3, lay.ntiles, rank, world, pf_dist.TorchComm(dist), log)
+        # the bytes this rank sent are those of the exchange model
+        dims = [be.dims(lv) for lv in range(3)]
+        plans = [be.plan(lv, world) for lv in range(3)]
+        ext = [[be.tile_rows(lv, *pf_dist.shard_range(lay.ntiles, r, world))
+                for r in range(world)] for lv in range(3)]
+        model = pf_dist.exchange_model(dims, plans, ext, world)[rank]
+        same = all(model.get(k, 0) == v for k, v in log.sent.items()) and \
+            all(log.sent.get(k, 0) == v for k, v in model.items())
+        ok = True
+        if rank == 0:  # the u16 result is gathered to rank 0 only
+            ref, _ = O.solve_depth_all(emap, tiles, data, 512, PL.ZENITH_RANGE)
+            ok = bool(np.array_equal(be.out.numpy().view(np.uint16).reshape(256, 512), ref))
+        q.put((rank, ok and same, log.sent, model))
     finally:
         dist.destroy_process_group()
 
@@ -218,5 +273,13 @@ def test_row_sharded_fusion_gloo(world):
     for p in procs:
         p.join(240)
         assert p.exitcode == 0
-    res = sorted(q.get() for _ in range(world))
-    assert res == [(r, True) for r in range(world)]
+    res = sorted((q.get() for _ in range(world)), key=lambda x: x[0])
+    assert [(r, ok) for r, ok, _, _ in res] == [(r, True) for r in range(world)], res
+    # world 2 deals the C1 layout band by band (tiles 0-2 = the upper zenith band), so only
+    # halo-sized rows travel: per rank the target rows it sends are at most its neighbour's halo
+    # plus the shared boundary row (K + 1 <= 12 rows of <= 512 floats, 3 levels), far below a
+    # full plane.  (World 3 deals 2 tiles per rank across the bands: the bands fall back to an
+    # even split and more rows travel -- still exactly the model's bytes.)
+    if world == 2:
+        for _, _, sent, _ in res:
+            assert 0 < sent.get("targets", 0) <= 3 * 12 * 512 * 4, sent

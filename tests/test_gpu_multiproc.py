@@ -4,9 +4,11 @@ tensors (RCCL refuses two ranks on one device; on a node every rank has its own 
 same code paths run over RCCL).  Readiness only -- the driver's 8-GPU node measures scaling.
 
 * C5 (--mode c5 --c5-shard rows): tiles and sweep row bands sharded over the 2 ranks, the
-  (sum L, n) grids all-reduced, halo rows exchanged before every pass, bands broadcast; rank 0
-  then fuses the same panorama alone (every tile warped and registered on its GPU) and the
-  sharded u16 must equal it bit for bit (bench.py's bit_exact_vs_one_gpu).
+  partial target rows each band reads sent by the rank that owns the tiles (a sparse
+  reduce-scatter), halo rows exchanged before every pass, the previous level's halo rows before
+  each level, the u16 rows gathered to rank 0; rank 0 then fuses the same panorama alone (every
+  tile warped and registered on its GPU) and the sharded u16 must equal it bit for bit
+  (bench.py's bit_exact_vs_one_gpu).
 * Batch (--mode batch, config C4's shape at a small batch): each rank its own contiguous seed
   block, disjoint; the line's value is the whole job over the MAX of the ranks' times; rank 0's
   fused batch equals a fresh one-process fusion of the same panoramas.

@@ -229,6 +229,35 @@ def test_warp_rgb_bit_exact(fuser):
     assert d.max() == 0  # host-built taps (glibc atan2), fp32 GL_LINEAR as the oracle
 
 
+@pytest.mark.parametrize("pw,ph,B", [(2048, 1024, 18), (1000, 500, 3), (1024, 512, 1)])
+def test_warp_rgb_staged_bit_exact(pw, ph, B, monkeypatch):
+    """The RGB warp at the C2/C3 layout (20 tiles of 512^2): the LDS-staged kernel
+    (k_warp_rgb_box; 64x16 patches, 16 panoramas per block, so batch 18 crosses a block's
+    panorama chunk) equals the oracle's GL-camera restatement for every byte, and equals the
+    per-pixel kernel (PF_WARP_RGB_NAIVE=1) on the whole batch.  pw = 1000 (3*pw not a multiple
+    of 16) takes the per-pixel kernel; both must agree with the oracle."""
+    lay = PL.config_layout("C2")
+    tiles, _ = O.make_tiles(lay)
+    rs = np.random.RandomState(pw + B)
+    pano = rs.randint(0, 256, size=(B, ph, pw, 3)).astype(np.uint8)
+    pano[0, :, :, 0] = (np.arange(pw) * 255 // (pw - 1)).astype(np.uint8)[None, :]
+    outs = []
+    for naive in ("0", "1"):
+        monkeypatch.setenv("PF_WARP_RGB_NAIVE", naive)
+        f = panofuse.Fuser(0)  # a new context rebuilds the taps under this setting
+        f.set_tiles(lay)
+        n = sum(int(lay.tile_w[i]) * int(lay.tile_h[i]) * 3 for i in range(lay.ntiles))
+        out = torch.zeros((B, n), dtype=torch.uint8, device=DEV)
+        f.warp_rgb(_dev(pano), out)
+        torch.cuda.synchronize()
+        outs.append(out.cpu().numpy())
+        f.close()
+    assert np.array_equal(outs[0], outs[1])
+    for b in sorted({0, B - 1}):
+        ref = O.warp_rgb(pano[b], tiles)
+        assert np.array_equal(outs[0][b], ref), b
+
+
 def test_sharded_partial_sum_equals_full(fuser):
     """C5-style tile sharding: per-shard (sum L, n) grids summed == all tiles at once."""
     lay, emap, gt, tiles, total, data, _ = _inputs("C2")

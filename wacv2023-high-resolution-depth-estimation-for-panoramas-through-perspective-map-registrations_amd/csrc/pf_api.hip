@@ -76,6 +76,10 @@ struct pf_ctx {
     // RGB warp taps for one panorama size (rgb_taps_host), built on first use
     int rgb_pw = 0, rgb_ph = 0;
     DevBuf rgbtap;
+    // LDS-staged RGB warp (k_warp_rgb_box): patch boxes, per-pixel box index and weights
+    DevBuf rgbpatch, rgbunits, rgbloc, rgbw;
+    int n_rgbpatch = 0;
+    bool rgb_staged = false;
     LevelCache lc;
     bool reg_valid = false;
     uint32_t reg_zr0 = 0, reg_zr1 = 0;
@@ -347,7 +351,7 @@ void pf_destroy(pf_ctx* c)
     if (!c) return;
     (void)hipSetDevice(c->device);
     (void)hipStreamSynchronize(c->stream);
-    DevBuf* all[] = {&c->geom, &c->reg, &c->reg_sidx, &c->rcols, &c->rrows, &c->rgbtap, &c->rgb_off,
+    DevBuf* all[] = {&c->geom, &c->reg, &c->reg_sidx, &c->rcols, &c->rrows, &c->rgbtap, &c->rgb_off, &c->rgbpatch, &c->rgbunits, &c->rgbloc, &c->rgbw,
                      &c->buf[0], &c->buf[1], &c->buf[2], &c->lnorm, &c->coeffs, &c->lsum_ws,
                      &c->wmap, &c->wfxy, &c->wpatch, &c->metrics_ws, &c->reg_sums,
                      &c->reg_active, &c->sm_box, &c->sm_cols, &c->sm_rows, &c->sm_src,
@@ -1818,11 +1822,25 @@ int pf_warp_rgb(pf_ctx* c, const uint8_t* pano, int pw, int ph, int batch, uint8
     if (c->rgb_pw != pw || c->rgb_ph != ph) {  // the taps of this size, on the host (glibc)
         const long long npix = c->tile_elems / c->tile_c;
         if ((rc = ensure(c, c->rgbtap, sizeof(RgbTap) * npix))) return rc;
+        // the LDS-staged kernel needs 16-B units that never straddle the row wrap, 12-B
+        // stores of 4 whole pixels, and 32-bit byte offsets (else the per-pixel kernel runs)
+        const bool naive = getenv("PF_WARP_RGB_NAIVE") && atoi(getenv("PF_WARP_RGB_NAIVE"));
+        bool staged = !naive && (3 * pw) % 16 == 0 && 3LL * pw * ph < (1LL << 31) &&
+                      c->rgb_elems < (1LL << 31);
+        for (int p = 0; staged && p < c->ntiles; p++) staged = c->geom_h[p].w % 4 == 0;
+        if (staged) {
+            if ((rc = ensure(c, c->rgbloc, sizeof(uint32_t) * npix))) return rc;
+            if ((rc = ensure(c, c->rgbw, sizeof(float) * 2 * npix))) return rc;
+        }
         // staged as the depth warp's corner tables: runs of up to 2^24 pixels, one copy and
         // one synchronisation per run (this first call per panorama size blocks the host)
         const size_t kStagePix = (size_t)1 << 24;
         const size_t cap = std::max((size_t)c->npix_max, std::min((size_t)npix, kStagePix));
         std::vector<RgbTap> taps(cap);
+        std::vector<uint32_t> loc(staged ? cap : 0);
+        std::vector<float> wts(staged ? 2 * cap : 0);
+        std::vector<RgbPatch> patches;
+        std::vector<uint32_t> units;
         for (int p0 = 0; p0 < c->ntiles;) {
             const size_t off0 = (size_t)c->geom_h[p0].pix_off;
             size_t n = 0;
@@ -1832,20 +1850,62 @@ int pf_warp_rgb(pf_ctx* c, const uint8_t* pano, int pw, int ph, int batch, uint8
                 const size_t m = (size_t)g.w * g.h;
                 if (p1 > p0 && n + m > cap) break;
                 rgb_taps_host(c->cams_h[p1], g.w, g.h, pw, ph, taps.data() + n);
+                if (staged)
+                    rgb_patches_host(g, p1, taps.data() + n, pw, ph, patches, units,
+                                     loc.data() + n, wts.data() + 2 * n);
                 n += m;
             }
             HIPCHK(c, hipMemcpyAsync((RgbTap*)c->rgbtap.p + off0, taps.data(),
                                      sizeof(RgbTap) * n, hipMemcpyHostToDevice, c->stream));
+            if (staged) {
+                HIPCHK(c, hipMemcpyAsync((uint32_t*)c->rgbloc.p + off0, loc.data(), 4 * n,
+                                         hipMemcpyHostToDevice, c->stream));
+                HIPCHK(c, hipMemcpyAsync((float*)c->rgbw.p + 2 * off0, wts.data(), 8 * n,
+                                         hipMemcpyHostToDevice, c->stream));
+            }
             HIPCHK(c, hipStreamSynchronize(c->stream));
             p0 = p1;
         }
+        if (staged) {
+            // footprint order (32-row bands of the first staged unit, then azimuth), as the
+            // depth warp's patches: the blocks resident on one XCD stage overlapping footprints
+            // and re-read them from its L2.  Each patch carries its unit-table row along.
+            const uint32_t rowb = (uint32_t)(3 * pw);
+            std::vector<long long> keys(patches.size());
+            for (size_t q = 0; q < patches.size(); q++) {
+                const uint32_t u = units[q * kRgbUnits];
+                keys[q] = (long long)(u / rowb / 32) * 65536 + (u % rowb) / 3;
+            }
+            std::vector<size_t> ord(patches.size());
+            for (size_t q = 0; q < ord.size(); q++) ord[q] = q;
+            std::stable_sort(ord.begin(), ord.end(),
+                             [&](size_t a, size_t b) { return keys[a] < keys[b]; });
+            std::vector<RgbPatch> sp(patches.size());
+            std::vector<uint32_t> su(units.size());
+            for (size_t q = 0; q < ord.size(); q++) {
+                sp[q] = patches[ord[q]];
+                std::copy(units.begin() + ord[q] * kRgbUnits,
+                          units.begin() + (ord[q] + 1) * kRgbUnits, su.begin() + q * kRgbUnits);
+            }
+            if ((rc = upload(c, c->rgbpatch, sp))) return rc;
+            if ((rc = upload(c, c->rgbunits, su))) return rc;
+            c->n_rgbpatch = (int)patches.size();
+        }
+        c->rgb_staged = staged;
         c->rgb_pw = pw;
         c->rgb_ph = ph;
     }
     StageTimer t(c, PF_STAGE_WARP, batch * (3.0 * pw * ph + (double)c->rgb_elems), 1);
-    launch_warp_rgb(c->stream, (const RgbTap*)c->rgbtap.p, (const TileGeom*)c->geom.p, c->ntiles,
-                    c->npix_max, (const long long*)c->rgb_off.p, pano, pw, ph,
-                    (long long)pw * ph * 3, tiles, c->rgb_elems, batch);
+    if (c->rgb_staged)
+        launch_warp_rgb_box(c->stream, (const TileGeom*)c->geom.p, (const RgbPatch*)c->rgbpatch.p,
+                            c->n_rgbpatch, (const uint32_t*)c->rgbunits.p,
+                            (const uint32_t*)c->rgbloc.p, (const float*)c->rgbw.p,
+                            (const RgbTap*)c->rgbtap.p, (const long long*)c->rgb_off.p, pano, pw,
+                            ph, (long long)pw * ph * 3, tiles, c->rgb_elems, batch);
+    else
+        launch_warp_rgb(c->stream, (const RgbTap*)c->rgbtap.p, (const TileGeom*)c->geom.p,
+                        c->ntiles, c->npix_max, (const long long*)c->rgb_off.p, pano, pw, ph,
+                        (long long)pw * ph * 3, tiles, c->rgb_elems, batch);
     HIPCHK(c, hipGetLastError());
     return PF_OK;
 }
@@ -1865,9 +1925,107 @@ int pf_fuse_partial(pf_ctx* c, const float* tiles, const float* coeffs, int t0, 
     const LevelDims& L = lc.dims[level];
     HIPCHK(c, hipMemsetAsync(lsum, 0, sizeof(float) * L.w * L.h, c->stream));
     HIPCHK(c, hipMemsetAsync(cnt, 0, sizeof(float) * L.w * L.h, c->stream));
-    launch_targets_partial(c->stream, (const TileGeom*)c->geom.p, (const TileBox*)lc.box[level].p,
-                           t0, t1, (const GridCol*)lc.cols[level].p,
-                           (const GridRow*)lc.rows[level].p, tiles, coeffs, L, lsum, cnt);
+    launch_targets_map_partial(c->stream, (const TileGeom*)c->geom.p,
+                               (const TileBox*)lc.box[level].p, (const TapBox*)lc.tapbox[level].p,
+                               t0, t1, (const int32_t*)lc.tapmap[level].p, tiles, coeffs, L, lsum,
+                               cnt, L.h0, L.h1 + 1);
+    HIPCHK(c, hipGetLastError());
+    return PF_OK;
+}
+
+// Row-restricted pieces of the sharded fusion (pf_dist.fuse_row_sharded): a rank computes only
+// the rows it sweeps (plus halo) and the rows its tiles send to its neighbours.
+static int level_rows(pf_ctx* c, int out_w, int out_h, float zr0, float zr1, int level, int& row0,
+                      int& row1, const LevelDims** Lp)
+{
+    int rc;
+    if ((rc = check_common(c, 1))) return rc;
+    if ((rc = prepare_levels(c, out_w, out_h, zr0, zr1))) return rc;
+    if (level < 0 || level >= c->lc.nlevels) return fail(c, PF_EINVAL, "bad level %d", level);
+    const LevelDims& L = c->lc.dims[level];
+    if (row0 < 0 || row1 > L.h || row0 > row1)
+        return fail(c, PF_EINVAL, "rows [%d,%d) outside [0,%d)", row0, row1, L.h);
+    row0 = std::max(row0, L.h0);  // the band: rows outside it are never targets
+    row1 = std::min(row1, L.h1 + 1);
+    *Lp = &L;
+    return PF_OK;
+}
+
+int pf_fuse_partial_rows(pf_ctx* c, const float* tiles, const float* coeffs, int t0, int t1,
+                         int out_w, int out_h, float zr0, float zr1, int level, int row0,
+                         int row1, float* lsum, float* cnt)
+{
+    int rc;
+    const LevelDims* L = nullptr;
+    if ((rc = level_rows(c, out_w, out_h, zr0, zr1, level, row0, row1, &L))) return rc;
+    if (!tiles || !lsum || !cnt) return fail(c, PF_EINVAL, "NULL buffer");
+    if (t0 < 0 || t1 > c->ntiles || t0 > t1)
+        return fail(c, PF_EINVAL, "tile range [%d,%d) outside [0,%d)", t0, t1, c->ntiles);
+    const LevelCache& lc = c->lc;
+    launch_targets_map_partial(c->stream, (const TileGeom*)c->geom.p,
+                               (const TileBox*)lc.box[level].p, (const TapBox*)lc.tapbox[level].p,
+                               t0, t1, (const int32_t*)lc.tapmap[level].p, tiles, coeffs, *L, lsum,
+                               cnt, row0, std::max(row0, row1));
+    HIPCHK(c, hipGetLastError());
+    return PF_OK;
+}
+
+int pf_fuse_coverage_rows(pf_ctx* c, int out_w, int out_h, float zr0, float zr1, int level,
+                          int row0, int row1, float* cnt)
+{
+    int rc;
+    const LevelDims* L = nullptr;
+    if ((rc = level_rows(c, out_w, out_h, zr0, zr1, level, row0, row1, &L))) return rc;
+    if (!cnt) return fail(c, PF_EINVAL, "NULL buffer");
+    launch_coverage_rows(c->stream, (const TileBox*)c->lc.box[level].p, c->ntiles, *L, cnt, row0,
+                         row1);
+    HIPCHK(c, hipGetLastError());
+    return PF_OK;
+}
+
+int pf_fuse_normalize_rows(pf_ctx* c, const float* lsum, const float* cnt, int out_w, int out_h,
+                           float zr0, float zr1, int level, int row0, int row1, float* lnorm)
+{
+    int rc;
+    const LevelDims* L = nullptr;
+    if ((rc = level_rows(c, out_w, out_h, zr0, zr1, level, row0, row1, &L))) return rc;
+    if (!lsum || !cnt || !lnorm) return fail(c, PF_EINVAL, "NULL buffer");
+    if (row1 > row0) launch_normalize(c->stream, lsum, cnt, *L, lnorm, row0, row1);
+    HIPCHK(c, hipGetLastError());
+    return PF_OK;
+}
+
+int pf_fuse_tile_rows(pf_ctx* c, int out_w, int out_h, float zr0, float zr1, int level, int t0,
+                      int t1, int* ymin, int* ymax)
+{
+    int rc;
+    if ((rc = check_common(c, 1))) return rc;
+    if (!ymin || !ymax) return fail(c, PF_EINVAL, "NULL output");
+    if ((rc = prepare_levels(c, out_w, out_h, zr0, zr1))) return rc;
+    if (level < 0 || level >= c->lc.nlevels) return fail(c, PF_EINVAL, "bad level %d", level);
+    if (t0 < 0 || t1 > c->ntiles || t0 > t1)
+        return fail(c, PF_EINVAL, "tile range [%d,%d) outside [0,%d)", t0, t1, c->ntiles);
+    const LevelDims& L = c->lc.dims[level];
+    int lo = INT32_MAX, hi = INT32_MIN;
+    for (int p = t0; p < t1; p++) {  // rows where k_targets_map_partial can write a non-zero sum
+        const TileBox& b = c->lc.box_h[level][p];
+        const int a = std::max(std::min(b.y0, b.y1), L.h0 + 1);
+        const int z = std::min(std::max(b.y0, b.y1), L.h1 - 1);
+        if (a > z) continue;
+        lo = std::min(lo, a);
+        hi = std::max(hi, z);
+    }
+    *ymin = lo == INT32_MAX ? 0 : lo;
+    *ymax = lo == INT32_MAX ? -1 : hi;
+    return PF_OK;
+}
+
+int pf_rows_add(pf_ctx* c, float* dst, const float* src, long long n)
+{
+    int rc;
+    if ((rc = check_common(c, 1))) return rc;
+    if (n < 0 || (n > 0 && (!dst || !src))) return fail(c, PF_EINVAL, "bad rows add");
+    launch_rows_add(c->stream, dst, src, n);
     HIPCHK(c, hipGetLastError());
     return PF_OK;
 }

@@ -10,6 +10,7 @@
 
 #include <hip/hip_runtime.h>
 #include <cstdint>
+#include <vector>
 
 #include "../../include/panofuse.h"
 
@@ -78,6 +79,21 @@ struct RgbTap {
     uint32_t x0y0, x1y1;
     float ax, ay;
 };
+
+// One patch of an RGB tile for the LDS-staged RGB warp (k_warp_rgb_box): 64 pixels wide and
+// nrow <= 16 rows (fewer where the footprint is large, near the poles).  Its corners' panorama
+// footprint is staged as whole 16-B units of the u8 RGB rows it touches, each row only over the
+// bytes its pixels use (a ragged footprint, not a bounding box); the host lists the units'
+// byte offsets (rgb unit table, kRgbUnits per patch).
+struct RgbPatch {
+    int tile, X0, Y0, nrow;
+    int units;  // staged 16-B units (<= kRgbUnits)
+    int wide;   // even one row's footprint exceeds the LDS slot: direct corner gathers
+    int pad[2];
+};
+static constexpr int kRgbPW = 64, kRgbPH = 16;  // RGB warp patch (4 pixels per thread)
+static constexpr int kRgbUnits = 256;            // 16-B units per patch: 4 KB of u8 = 4096 floats
+static constexpr int kRgbCap = 16 * kRgbUnits;   // LDS floats per parity (bytes widened to fp32)
 
 // Synthetic depth-net response (same layout as pf_response in panofuse.h).
 struct Resp {
@@ -269,12 +285,16 @@ void launch_targets(hipStream_t s, const TileGeom* geom, const TileBox* box, int
                     const GridCol* cols, const GridRow* rows, const float* tiles,
                     long long tstride, const float* coeffs, int ntiles_total, LevelDims L,
                     float* lnorm, long long lstride, int batch);
-void launch_targets_partial(hipStream_t s, const TileGeom* geom, const TileBox* box, int t0,
-                            int t1, const GridCol* cols, const GridRow* rows,
-                            const float* tiles, const float* coeffs, LevelDims L, float* lsum,
-                            float* cnt);
+ // rows [r0,r1), -1: band
+void launch_targets_map_partial(hipStream_t s, const TileGeom* geom, const TileBox* box,
+                                const TapBox* tb, int t0, int t1, const int32_t* map,
+                                const float* tiles, const float* coeffs, LevelDims L, float* lsum,
+                                float* cnt, int r0, int r1);
+void launch_coverage_rows(hipStream_t s, const TileBox* box, int ntiles, LevelDims L, float* cnt,
+                          int r0, int r1);
+void launch_rows_add(hipStream_t s, float* dst, const float* src, long long n);
 void launch_normalize(hipStream_t s, const float* lsum, const float* cnt, LevelDims L,
-                      float* lnorm);
+                      float* lnorm, int r0 = -1, int r1 = -1);
 void launch_multicover(hipStream_t s, const TileGeom* geom, const int2* pairs, int npairs,
                        int t0, int t1, const GridCol* cols, const GridRow* rows,
                        const float* tiles, const float* coeffs, LevelDims L, float* contrib);
@@ -307,6 +327,18 @@ int warp_patch_height();
 // host tables (pf_warp.hip): wxy/wfxy of one tile's pixels; the RGB taps of one tile
 void warp_coords_host(const TileGeom& g, int pw, int ph, uint32_t* wxy, float* wfxy);
 void rgb_taps_host(const RgbCam& cam, int W, int H, int pw, int ph, RgbTap* taps);
+// The RGB warp's patches of one tile (its taps at `taps`), appended to `patches`; their staged
+// units' byte offsets to `units` (kRgbUnits per patch); per pixel the LDS float indices of its
+// top and bottom corner pairs (loc: top | bottom << 16) and the GL_LINEAR weights (wts: ax, ay).
+// Needs (3 * pw) % 16 == 0, 3 * pw * ph < 2^32 and tile width % 4 == 0.
+void rgb_patches_host(const TileGeom& g, int tile, const RgbTap* taps, int pw, int ph,
+                      std::vector<RgbPatch>& patches, std::vector<uint32_t>& units,
+                      uint32_t* loc, float* wts);
+void launch_warp_rgb_box(hipStream_t s, const TileGeom* geom, const RgbPatch* patches,
+                         int npatch, const uint32_t* units, const uint32_t* loc, const float* wts,
+                         const RgbTap* taps,
+                         const long long* rgb_off, const uint8_t* pano, int pw, int ph,
+                         long long pstride, uint8_t* tiles, long long tstride, int batch);
 // patch footprint boxes and in-box corner indices from the uploaded wxy (in place over wloc)
 void launch_warp_boxes(hipStream_t s, const TileGeom* geom, WarpPatch* patches, int npatch,
                        int pw, int ph, uint32_t* wloc);

@@ -138,43 +138,15 @@ __global__ void __launch_bounds__(kBlock) k_targets(const TileGeom* __restrict__
     lnorm[b * lstride + (long long)Y * L.w + X] = out;
 }
 
-// Partial scatter for the sharded single-panorama case: (sum L, n) of tiles [t0, t1).
-__global__ void __launch_bounds__(kBlock) k_targets_partial(
-    const TileGeom* __restrict__ geom, const TileBox* __restrict__ box, int t0, int t1,
-    const GridCol* __restrict__ cols, const GridRow* __restrict__ rows,
-    const float* __restrict__ tiles, const float* __restrict__ coeffs, LevelDims L,
-    float* __restrict__ lsum, float* __restrict__ cnt)
-{
-    long long i = (long long)blockIdx.x * kBlock + threadIdx.x;
-    long long nband = (long long)L.w * (L.h1 - L.h0 + 1);
-    if (i >= nband) return;
-    int Y = (int)(i / L.w) + L.h0, X = (int)(i - (long long)(Y - L.h0) * L.w);
-    float acc = 0.0f, n = 0.0f;
-    if (Y > L.h0 && Y < L.h1) {
-        for (int p = t0; p < t1; p++) {
-            TileBox bx = box[p];
-            if (!in_box(bx, X, Y)) continue;
-            const TileGeom& g = geom[p];
-            float4 abcd = make_float4(0, 0, 0, 0);
-            bool xf = coeffs != nullptr;
-            if (xf) abcd = *reinterpret_cast<const float4*>(coeffs + (long long)p * 4);
-            acc += target_one(g, tiles + g.off, cols, rows, X, Y, xf, abcd);
-            n += 1.0f;
-        }
-    }
-    long long o = (long long)Y * L.w + X;
-    lsum[o] = acc;
-    cnt[o] = n;
-}
-
 __global__ void __launch_bounds__(kBlock) k_normalize(const float* __restrict__ lsum,
                                                       const float* __restrict__ cnt,
-                                                      LevelDims L, float* __restrict__ lnorm)
-{
+                                                      LevelDims L, float* __restrict__ lnorm,
+                                                      int r0, int r1)
+{  // rows [r0, r1) of the band
     long long i = (long long)blockIdx.x * kBlock + threadIdx.x;
-    long long nband = (long long)L.w * (L.h1 - L.h0 + 1);
+    long long nband = (long long)L.w * (r1 - r0);
     if (i >= nband) return;
-    long long o = (long long)L.h0 * L.w + i;
+    long long o = (long long)r0 * L.w + i;
     int Y = (int)(o / L.w);
     float n = cnt[o];
     float out;
@@ -182,6 +154,40 @@ __global__ void __launch_bounds__(kBlock) k_normalize(const float* __restrict__ 
     else if (n == 1.0f) out = lsum[o];
     else out = lsum[o] * (1.0f / n);
     lnorm[o] = out;
+}
+
+// Coverage count of rows [r0, r1) of the band by ALL tiles (the n of pf_fuse_partial over every
+// tile, from the boxes alone): layout-only, so a rank of the sharded fusion counts its own rows
+// instead of receiving the other ranks' counts.
+__global__ void __launch_bounds__(kBlock) k_coverage_rows(const TileBox* __restrict__ box,
+                                                          int ntiles, LevelDims L,
+                                                          float* __restrict__ cnt, int r0, int r1)
+{
+    long long i = (long long)blockIdx.x * kBlock + threadIdx.x;
+    long long n = (long long)L.w * (r1 - r0);
+    if (i >= n) return;
+    const int Y = (int)(i / L.w) + r0, X = (int)(i - (long long)(Y - r0) * L.w);
+    float c = 0.0f;
+    if (Y > L.h0 && Y < L.h1)
+        for (int p = 0; p < ntiles; p++) c += in_box(box[p], X, Y) ? 1.0f : 0.0f;
+    cnt[(long long)Y * L.w + X] = c;
+}
+
+// dst[i] += src[i]: a received partial-target segment added into this rank's sums.  Exact for
+// pixels covered by at most two tiles (one of the addends is zero, or the pair is the whole sum);
+// the three-or-more pixels are re-added in tile order by pf_fuse_multicover_patch.
+__global__ void __launch_bounds__(kBlock) k_rows_add(float* __restrict__ dst,
+                                                     const float* __restrict__ src, long long n)
+{
+    const long long i = ((long long)blockIdx.x * kBlock + threadIdx.x) * 4;
+    if (i + 3 < n) {
+        float4 a = *reinterpret_cast<const float4*>(dst + i);
+        const float4 b = *reinterpret_cast<const float4*>(src + i);
+        a.x += b.x; a.y += b.y; a.z += b.z; a.w += b.w;
+        *reinterpret_cast<float4*>(dst + i) = a;
+    } else {
+        for (long long j = i; j < n; j++) dst[j] += src[j];
+    }
 }
 
 // Parity probe: linear tile index of each tap of the first covering tile.
@@ -768,14 +774,18 @@ void launch_targets(hipStream_t s, const TileGeom* geom, const TileBox* box, int
                        tstride, coeffs, ntiles_total, L, lnorm, lstride);
 }
 
-void launch_targets_partial(hipStream_t s, const TileGeom* geom, const TileBox* box, int t0,
-                            int t1, const GridCol* cols, const GridRow* rows,
-                            const float* tiles, const float* coeffs, LevelDims L, float* lsum,
-                            float* cnt)
+void launch_coverage_rows(hipStream_t s, const TileBox* box, int ntiles, LevelDims L, float* cnt,
+                          int r0, int r1)
 {
-    dim3 grid(nblocks((long long)L.w * (L.h1 - L.h0 + 1)));
-    hipLaunchKernelGGL(k_targets_partial, grid, dim3(kBlock), 0, s, geom, box, t0, t1, cols,
-                       rows, tiles, coeffs, L, lsum, cnt);
+    if (r1 <= r0) return;
+    hipLaunchKernelGGL(k_coverage_rows, dim3(nblocks((long long)L.w * (r1 - r0))), dim3(kBlock),
+                       0, s, box, ntiles, L, cnt, r0, r1);
+}
+
+void launch_rows_add(hipStream_t s, float* dst, const float* src, long long n)
+{
+    if (n <= 0) return;
+    hipLaunchKernelGGL(k_rows_add, dim3(nblocks((n + 3) / 4)), dim3(kBlock), 0, s, dst, src, n);
 }
 
 void launch_multicover(hipStream_t s, const TileGeom* geom, const int2* pairs, int npairs,
@@ -795,10 +805,12 @@ void launch_multicover_patch(hipStream_t s, const int2* pairs, int npairs, const
 }
 
 void launch_normalize(hipStream_t s, const float* lsum, const float* cnt, LevelDims L,
-                      float* lnorm)
+                      float* lnorm, int r0, int r1)
 {
-    dim3 grid(nblocks((long long)L.w * (L.h1 - L.h0 + 1)));
-    hipLaunchKernelGGL(k_normalize, grid, dim3(kBlock), 0, s, lsum, cnt, L, lnorm);
+    if (r0 < 0) { r0 = L.h0; r1 = L.h1 + 1; }
+    if (r1 <= r0) return;
+    dim3 grid(nblocks((long long)L.w * (r1 - r0)));
+    hipLaunchKernelGGL(k_normalize, grid, dim3(kBlock), 0, s, lsum, cnt, L, lnorm, r0, r1);
 }
 
 void launch_probe_taps(hipStream_t s, const TileGeom* geom, const TileBox* box, int ntiles,

@@ -372,6 +372,71 @@ void launch_tapmap(hipStream_t s, const TileGeom* geom, const TapBox* tb, int nt
     hipLaunchKernelGGL(k_tapmap, grid, dim3(256), 0, s, geom, tb, ntiles, cols, rows, map);
 }
 
+// Partial sums of tiles [t0, t1) for one panorama on rows [r0, r1) of the band (pf_fuse_partial,
+// pf_fuse_partial_rows: the sharded fusion).  k_targets_map's gather from the cached tap-index maps
+// without the normalisation: lsum = the tiles' Laplacians added in tile order, cnt = how many.
+template <bool XFORM>
+__global__ void __launch_bounds__(256) k_targets_map_partial(const TileGeom* __restrict__ geom,
+                                                             const TileBox* __restrict__ box,
+                                                             const TapBox* __restrict__ tb,
+                                                             int t0, int t1,
+                                                             const int32_t* __restrict__ map,
+                                                             const float* __restrict__ tiles,
+                                                             const float* __restrict__ coeffs,
+                                                             LevelDims L, float* __restrict__ lsum,
+                                                             float* __restrict__ cnt, int r0,
+                                                             int r1)
+{
+    const unsigned lb = xcd_remap(blockIdx.x, gridDim.x);
+    const long long i = (long long)lb * 256 + threadIdx.x;
+    const long long n_ = (long long)L.w * (r1 - r0);
+    if (i >= n_) return;
+    const int Y = (int)(i / L.w) + r0, X = (int)(i - (long long)(Y - r0) * L.w);
+    float acc = 0.0f, n = 0.0f;
+    if (Y > L.h0 && Y < L.h1) {
+        for (int p = t0; p < t1; p++) {
+            if (!in_box2(box[p], X, Y)) continue;
+            const TapBox B = tb[p];
+            const long long base = B.off + (long long)(Y - B.ymin) * B.nx + (X - B.xmin);
+            const float* t = tiles + geom[p].off;
+            float v[5] = {t[map[base - 1]], t[map[base - B.nx]], t[map[base]], t[map[base + B.nx]],
+                          t[map[base + 1]]};
+            if constexpr (XFORM) {
+                const float4 k = *reinterpret_cast<const float4*>(coeffs + (long long)p * 4);
+#pragma unroll
+                for (int m = 0; m < 5; m++) v[m] = cubic_map(v[m], k.x, k.y, k.z, k.w);
+            }
+            float Lp = 0;  // std::map key order, as k_targets_map
+            Lp += v[0] * -0.25f;
+            Lp += v[1] * -0.25f;
+            Lp += v[2] * 1.0f;
+            Lp += v[3] * -0.25f;
+            Lp += v[4] * -0.25f;
+            acc += Lp;
+            n += 1.0f;
+        }
+    }
+    const long long o = (long long)Y * L.w + X;
+    lsum[o] = acc;
+    cnt[o] = n;
+}
+
+void launch_targets_map_partial(hipStream_t s, const TileGeom* geom, const TileBox* box,
+                                const TapBox* tb, int t0, int t1, const int32_t* map,
+                                const float* tiles, const float* coeffs, LevelDims L, float* lsum,
+                                float* cnt, int r0, int r1)
+{
+    const long long n = (long long)L.w * (r1 - r0);
+    if (n <= 0) return;
+    const unsigned g = (unsigned)((n + 255) / 256);
+    if (coeffs)
+        hipLaunchKernelGGL(k_targets_map_partial<true>, dim3(g), dim3(256), 0, s, geom, box, tb, t0,
+                           t1, map, tiles, coeffs, L, lsum, cnt, r0, r1);
+    else
+        hipLaunchKernelGGL(k_targets_map_partial<false>, dim3(g), dim3(256), 0, s, geom, box, tb, t0,
+                           t1, map, tiles, coeffs, L, lsum, cnt, r0, r1);
+}
+
 void launch_targets_map(hipStream_t s, const TileGeom* geom, const TileBox* box,
                         const TapBox* tb, int ntiles, const int32_t* map, const float* tiles,
                         long long tstride, const float* coeffs, LevelDims L, float* lnorm,

@@ -876,4 +876,310 @@ void launch_warp_depth(hipStream_t s, const TileGeom* geom, int ntiles, const Wa
 #endif
 }
 
+
+// =============================================================================================
+// E->P RGB warp (a18: SaveCubeMap, Main.cpp:242-326, the GL camera and GL_LINEAR + GL_REPEAT
+// sampling of SphereMesh.cpp:74-77), LDS-staged like k_warp_depth.
+//
+// Per layout and panorama size the host cuts every tile into 64x16-pixel patches and, from the
+// taps (rgb_taps_host), gives each patch the byte box of its corners' footprint: rows gy0.. and
+// bytes bx0.. of the u8 RGB panorama, the origin rounded down to 16 B and the width up to 16 B,
+// so the box is staged with whole 16-B loads (both wrap: GL_REPEAT in u and v).  One block =
+// one patch x kNBR panoramas.  Per panorama each thread loads one 16-B unit of the box,
+// converts its bytes to floats and writes them to LDS (double-buffered: the loads for panorama
+// q+2 are in flight while q is blended); a thread then blends its 4 consecutive pixels of one
+// tile row (per channel top = t00*(1-ax) + t01*ax, bottom likewise, v = top*(1-ay) + bot*ay:
+// the oracle's fp32 operations in its order), rounds them to u8 and writes the 12 bytes with
+// one 12-B store, so a wave writes four 192-B runs of tile rows.  Patches whose box exceeds
+// the LDS slot (near the poles) blend from direct byte gathers of the taps.
+// =============================================================================================
+static constexpr int kNBR = 16;  // panoramas per block
+
+static inline int wrap_signed(int d, int n)
+{
+    if (d > n / 2) d -= n;
+    if (d < -(n / 2)) d += n;
+    return d;
+}
+
+// Footprint of a patch of nrow rows: per panorama row v (unwrapped from the patch's first
+// corner) the x-range [xlo, xhi] of the corners that read it (pixels whose y0 is v or v-1, with
+// their x0 and x0 + 1), rounded out to 16-B units of the u8 RGB row.  Returns the unit count.
+static inline long long floor_div16(long long x) { return x >= 0 ? x / 16 : -((15 - x) / 16); }
+
+struct RgbFoot {
+    int vmin = 0, nv = 0;
+    std::vector<int> xlo, xhi, u0, nu, off;  // per row: pixel range, first unit, units, LDS unit
+    int units = 0;
+};
+static int rgb_footprint(const RgbTap* taps, int w, int X0, int X1, int Y0, int Y1, int pw,
+                         int ph, int rx, int ry, RgbFoot& F)
+{
+    int vmin = INT32_MAX, vmax = INT32_MIN;
+    for (int Y = Y0; Y < Y1; Y++)
+        for (int X = X0; X < X1; X++) {
+            const int dv = wrap_signed((int)(taps[(long long)Y * w + X].x0y0 >> 16) - ry, ph);
+            vmin = std::min(vmin, dv);
+            vmax = std::max(vmax, dv);
+        }
+    F.vmin = vmin;
+    F.nv = vmax - vmin + 2;
+    if (F.nv > ph / 2) return INT32_MAX;
+    F.xlo.assign(F.nv, INT32_MAX);
+    F.xhi.assign(F.nv, INT32_MIN);
+    for (int Y = Y0; Y < Y1; Y++)
+        for (int X = X0; X < X1; X++) {
+            const RgbTap& t = taps[(long long)Y * w + X];
+            const int du = wrap_signed((int)(t.x0y0 & 0xFFFFu) - rx, pw);
+            const int dv = wrap_signed((int)(t.x0y0 >> 16) - ry, ph) - vmin;
+            for (int r = dv; r <= dv + 1; r++) {
+                F.xlo[r] = std::min(F.xlo[r], du);
+                F.xhi[r] = std::max(F.xhi[r], du + 1);
+            }
+        }
+    F.u0.resize(F.nv);
+    F.nu.resize(F.nv);
+    F.off.resize(F.nv);
+    F.units = 0;
+    for (int r = 0; r < F.nv; r++) {
+        if (F.xhi[r] - F.xlo[r] + 1 > pw / 2) return INT32_MAX;
+        const long long b0 = 3LL * (rx + F.xlo[r]), b1 = 3LL * (rx + F.xhi[r]) + 3;  // unwrapped
+        const long long q0 = floor_div16(b0), q1 = floor_div16(b1 + 15);
+        F.u0[r] = (int)q0;
+        F.nu[r] = (int)(q1 - q0);
+        F.off[r] = F.units;
+        F.units += F.nu[r];
+    }
+    return F.units;
+}
+
+void rgb_patches_host(const TileGeom& g, int tile, const RgbTap* taps, int pw, int ph,
+                      std::vector<RgbPatch>& patches, std::vector<uint32_t>& units,
+                      uint32_t* loc, float* wts)
+{
+    const int rowu = 3 * pw / 16;  // units per panorama row
+    for (int Y0 = 0; Y0 < g.h;) {
+        // one band of patches of a common height: the tallest (16, 8, .., 1 rows) whose every
+        // patch's footprint fits kRgbUnits units; rows that do not fit even alone go "wide"
+        int hp = std::min(kRgbPH, g.h - Y0);
+        std::vector<RgbFoot> feet;
+        for (;; hp = std::max(1, hp / 2)) {
+            feet.assign((g.w + kRgbPW - 1) / kRgbPW, RgbFoot{});
+            bool fit = true;
+            for (int X0 = 0, k = 0; X0 < g.w; X0 += kRgbPW, k++) {
+                const RgbTap& t0 = taps[(long long)Y0 * g.w + X0];
+                const int n = rgb_footprint(taps, g.w, X0, std::min(g.w, X0 + kRgbPW), Y0, Y0 + hp,
+                                            pw, ph, (int)(t0.x0y0 & 0xFFFFu), (int)(t0.x0y0 >> 16),
+                                            feet[k]);
+                fit = fit && n <= kRgbUnits;
+            }
+            if (fit || hp == 1) break;
+        }
+        for (int X0 = 0, k = 0; X0 < g.w; X0 += kRgbPW, k++) {
+            const RgbFoot& F = feet[k];
+            RgbPatch P{};
+            P.tile = tile; P.X0 = X0; P.Y0 = Y0; P.nrow = hp;
+            P.wide = F.units > kRgbUnits ? 1 : 0;
+            P.units = P.wide ? 1 : F.units;
+            const RgbTap& t0 = taps[(long long)Y0 * g.w + X0];
+            const int rx = (int)(t0.x0y0 & 0xFFFFu), ry = (int)(t0.x0y0 >> 16);
+            const size_t base = units.size();
+            units.resize(base + kRgbUnits, 0u);
+            if (!P.wide)
+                for (int r = 0; r < F.nv; r++) {
+                    const int prow = ((ry + F.vmin + r) % ph + ph) % ph;
+                    for (int u = 0; u < F.nu[r]; u++) {
+                        const int cu = ((F.u0[r] + u) % rowu + rowu) % rowu;
+                        units[base + F.off[r] + u] = (uint32_t)prow * (uint32_t)(3 * pw) +
+                                                     (uint32_t)(16 * cu);
+                    }
+                }
+            for (int Y = Y0; Y < Y0 + hp; Y++)
+                for (int X = X0; X < std::min(g.w, X0 + kRgbPW); X++) {
+                    const long long i = (long long)Y * g.w + X;
+                    const RgbTap& t = taps[i];
+                    uint32_t l = 0;
+                    if (!P.wide) {
+                        const int du = wrap_signed((int)(t.x0y0 & 0xFFFFu) - rx, pw);
+                        const int dv = wrap_signed((int)(t.x0y0 >> 16) - ry, ph) - F.vmin;
+                        const long long bx = 3LL * (rx + du);  // unwrapped byte of corner x0
+                        const uint32_t lt = (uint32_t)(16 * (F.off[dv] - F.u0[dv]) + bx);
+                        const uint32_t lb = (uint32_t)(16 * (F.off[dv + 1] - F.u0[dv + 1]) + bx);
+                        l = lt | lb << 16;
+                    }
+                    loc[i] = l;
+                    wts[2 * i] = t.ax;
+                    wts[2 * i + 1] = t.ay;
+                }
+            patches.push_back(P);
+        }
+        Y0 += hp;
+    }
+}
+
+__device__ __forceinline__ uint32_t rgb_u8(float v)
+{  // (int)floorf(v + 0.5f) clamped to [0, 255]: v >= 0 (a blend of u8 values with weights in
+   // [0, 1]), so the floor is the truncating conversion
+    const uint32_t q = (uint32_t)(v + 0.5f);
+    return q < 255u ? q : 255u;
+}
+
+__device__ __forceinline__ float lerp_ref(float a, float b, float w)
+{  // a * (1 - w) + b * w with separate roundings (the oracle's / GL-restatement order)
+    return a * (1.0f - w) + b * w;
+}
+
+__global__ void __launch_bounds__(256) k_warp_rgb_box(const TileGeom* __restrict__ geom,
+                                                      const RgbPatch* __restrict__ patches,
+                                                      int npatch,
+                                                      const uint32_t* __restrict__ unit_tbl,
+                                                      const uint32_t* __restrict__ loc,
+                                                      const float2* __restrict__ wts,
+                                                      const RgbTap* __restrict__ taps,
+                                                      const long long* __restrict__ rgb_off,
+                                                      const uint8_t* __restrict__ pano, int pw,
+                                                      int ph, long long pstride,
+                                                      uint8_t* __restrict__ tiles,
+                                                      long long tstride, int batch)
+{
+    __shared__ float box[2 * kRgbCap];
+    const unsigned lb = xcd_remap(blockIdx.x, gridDim.x);
+    const int pid = (int)(lb % (unsigned)npatch);
+    const int chunk = (int)(lb / (unsigned)npatch);
+    const RgbPatch P = patches[pid];
+    const TileGeom& g = geom[P.tile];
+    const int t = threadIdx.x;
+    const int X = P.X0 + 4 * (t & 15), Y = P.Y0 + (t >> 4);
+    const int bbeg = chunk * kNBR, nb = min(kNBR, batch - bbeg);
+    const bool rowok = (t >> 4) < P.nrow && Y < g.h;
+    bool ok[4];
+    uint32_t la[4];
+    float ax[4], ay[4];
+    long long pix[4];
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+        ok[k] = rowok && X + k < g.w;
+        pix[k] = (long long)Y * g.w + X + k;
+        la[k] = 0; ax[k] = 0.0f; ay[k] = 0.0f;
+        if (ok[k]) {
+            la[k] = loc[g.pix_off + pix[k]];
+            const float2 w = wts[g.pix_off + pix[k]];
+            ax[k] = w.x;
+            ay[k] = w.y;
+        }
+    }
+    const long long toff = rgb_off[P.tile];
+    // byte offset of the lane's first pixel inside one panorama's tile block (past the block for
+    // lanes outside the tile: the buffer store is then dropped)
+    const uint32_t ob = ok[0] ? (uint32_t)(toff + 3 * pix[0]) : 0xFFFFFFF0u;
+    const uint32_t tbytes = (uint32_t)tstride;
+    const uint32_t pbytes = (uint32_t)pstride;
+
+    auto blend_store = [&](const auto& corner, uint8_t* tb) {
+        // corner(k, c) -> the 12 floats c00 RGB, c01 RGB, c10 RGB, c11 RGB of pixel k
+        uint32_t q[12];
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+            float c[12];
+            corner(k, c);
+#pragma unroll
+            for (int ch = 0; ch < 3; ch++) {
+                const float top = lerp_ref(c[ch], c[3 + ch], ax[k]);
+                const float bot = lerp_ref(c[6 + ch], c[9 + ch], ax[k]);
+                q[3 * k + ch] = rgb_u8(lerp_ref(top, bot, ay[k]));
+            }
+        }
+        const auto orr = rsrc(tb, tbytes);
+        if (ok[3]) {
+            typedef uint32_t u3v __attribute__((ext_vector_type(3)));
+            const u3v o = {q[0] | q[1] << 8 | q[2] << 16 | q[3] << 24,
+                           q[4] | q[5] << 8 | q[6] << 16 | q[7] << 24,
+                           q[8] | q[9] << 8 | q[10] << 16 | q[11] << 24};
+            __builtin_amdgcn_raw_buffer_store_b96(o, orr, (int)ob, 0, 2);
+        } else {
+#pragma unroll
+            for (int k = 0; k < 4; k++)
+                if (ok[k])
+#pragma unroll
+                    for (int ch = 0; ch < 3; ch++)
+                        __builtin_amdgcn_raw_buffer_store_b8((uint8_t)q[3 * k + ch], orr,
+                                                             (int)(ob + 3 * k + ch), 0, 2);
+        }
+    };
+
+    if (P.wide) {  // even one row's footprint exceeds the LDS slot: direct byte gathers
+        for (int q = 0; q < nb; q++) {
+            const uint8_t* pp = pano + (long long)(bbeg + q) * pstride;
+            blend_store([&](int k, float* c) {
+                const RgbTap tp = ok[k] ? taps[g.pix_off + pix[k]] : RgbTap{0, 0, 0.0f, 0.0f};
+                const long long x0 = tp.x0y0 & 0xFFFFu, y0 = tp.x0y0 >> 16;
+                const long long x1 = tp.x1y1 & 0xFFFFu, y1 = tp.x1y1 >> 16;
+                const long long a[4] = {(y0 * pw + x0) * 3, (y0 * pw + x1) * 3,
+                                        (y1 * pw + x0) * 3, (y1 * pw + x1) * 3};
+#pragma unroll
+                for (int m = 0; m < 4; m++)
+#pragma unroll
+                    for (int ch = 0; ch < 3; ch++) c[3 * m + ch] = (float)pp[a[m] + ch];
+            }, tiles + (long long)(bbeg + q) * tstride);
+        }
+        return;
+    }
+
+    // staging: thread t owns unit t of the patch's footprint (units past it reload its first
+    // unit, so every load is issued unconditionally)
+    const uint32_t goff = unit_tbl[(long long)pid * kRgbUnits + (t < P.units ? t : 0)];
+    u4v stg[2];
+    auto fetch = [&](int sl, int q) {
+        const auto pr = rsrc(pano + (long long)(bbeg + (q < nb ? q : nb - 1)) * pstride, pbytes);
+        stg[sl] = __builtin_amdgcn_raw_buffer_load_b128(pr, (int)goff, 0, 0);
+    };
+    auto put = [&](int pa, const u4v v) {
+        float4* d = reinterpret_cast<float4*>(box + pa * kRgbCap + 16 * t);
+#pragma unroll
+        for (int m = 0; m < 4; m++) {
+            const uint32_t w = v[m];
+            d[m] = make_float4((float)(w & 0xFFu), (float)((w >> 8) & 0xFFu),
+                               (float)((w >> 16) & 0xFFu), (float)(w >> 24));
+        }
+    };
+    auto iter = [&](auto parity, int q) {
+        constexpr int PA = decltype(parity)::value;
+        fetch(PA, q + 2);  // stg[PA] held panorama q, put into parity PA last iteration
+        const float* L = box + PA * kRgbCap;
+        blend_store([&](int k, float* c) {
+            const float* st = L + (la[k] & 0xFFFFu);
+            const float* sb = L + (la[k] >> 16);
+#pragma unroll
+            for (int j = 0; j < 6; j++) {
+                c[j] = st[j];
+                c[6 + j] = sb[j];
+            }
+        }, tiles + (long long)(bbeg + q) * tstride);
+        put(1 - PA, stg[1 - PA]);  // panorama q+1 (a duplicate past the chunk: unread)
+        __syncthreads();
+    };
+    fetch(0, 0);
+    fetch(1, 1);
+    put(0, stg[0]);
+    __syncthreads();
+    using I0 = std::integral_constant<int, 0>;
+    using I1 = std::integral_constant<int, 1>;
+    for (int q = 0; q < nb; q += 2) {
+        iter(I0{}, q);
+        if (q + 1 < nb) iter(I1{}, q + 1);
+    }
+}
+
+void launch_warp_rgb_box(hipStream_t s, const TileGeom* geom, const RgbPatch* patches,
+                         int npatch, const uint32_t* units, const uint32_t* loc, const float* wts,
+                         const RgbTap* taps, const long long* rgb_off, const uint8_t* pano,
+                         int pw, int ph, long long pstride, uint8_t* tiles, long long tstride,
+                         int batch)
+{
+    const unsigned nblk = (unsigned)npatch * (unsigned)((batch + kNBR - 1) / kNBR);
+    hipLaunchKernelGGL(k_warp_rgb_box, dim3(nblk), dim3(256), 0, s, geom, patches, npatch, units,
+                       loc, (const float2*)wts, taps, rgb_off, pano, pw, ph, pstride, tiles,
+                       tstride, batch);
+}
+
 }  // namespace pf

@@ -30,9 +30,12 @@ EXPORTS = [
     "pf_fuse_multicover_patch", "pf_solve_smoothing", "pf_set_metrics_order",
     "pf_jres_errors", "pf_set_jacobi_engine", "pf_stream_wait_level", "pf_debug_jres_fault",
     "pf_probe_warp_coords", "pf_probe_rgb_taps", "pf_debug_smooth_fault",
+    "pf_fuse_partial_rows", "pf_fuse_coverage_rows", "pf_fuse_normalize_rows",
+    "pf_fuse_tile_rows", "pf_rows_add",
 ]
 NEW_R4 = {"pf_debug_jres_fault", "pf_probe_warp_coords", "pf_probe_rgb_taps",
-          "pf_debug_smooth_fault"}
+          "pf_debug_smooth_fault", "pf_fuse_partial_rows", "pf_fuse_coverage_rows",
+          "pf_fuse_normalize_rows", "pf_fuse_tile_rows", "pf_rows_add"}
 METRICS_ORDERS = {"tree": 0, "sequential": 1}  # PF_METRICS_*; "sequential" = the reference's
 SOLVERS = {"normal": 0, "lm": 1}  # PF_SOLVER_*; "lm" = the reference's Ceres LM (default)
 
@@ -107,6 +110,13 @@ def load():
     L.pf_jres_errors.argtypes = [vp]
     # (entry points added after round 3: an A/B variant built from older sources may lack them)
     for name, at in (("pf_debug_jres_fault", [vp, ip]), ("pf_debug_smooth_fault", [vp, ip]),
+                     ("pf_fuse_partial_rows", [vp, vp, vp, ip, ip, ip, ip, fp, fp, ip, ip, ip,
+                                               vp, vp]),
+                     ("pf_fuse_coverage_rows", [vp, ip, ip, fp, fp, ip, ip, ip, vp]),
+                     ("pf_fuse_normalize_rows", [vp, vp, vp, ip, ip, fp, fp, ip, ip, ip, vp]),
+                     ("pf_fuse_tile_rows", [vp, ip, ip, fp, fp, ip, ip, ip,
+                                            C.POINTER(C.c_int), C.POINTER(C.c_int)]),
+                     ("pf_rows_add", [vp, vp, vp, C.c_longlong]),
                      ("pf_probe_warp_coords", [C.POINTER(Window), ip, ip, ip, ip, vp, vp]),
                      ("pf_probe_rgb_taps", [C.POINTER(Window), ip, ip, ip, ip, vp])):
         if hasattr(L, name):
@@ -310,6 +320,36 @@ class Fuser:
         self._check(self.L.pf_fuse_partial(self.h, _ptr(tiles), _ptr(coeffs), t0, t1, out_w,
                                            out_w // 2, float(zr[0]), float(zr[1]), level,
                                            _ptr(lsum), _ptr(cnt)))
+
+    def fuse_partial_rows(self, tiles, coeffs, t0, t1, out_w, zr, level, row0, row1, lsum, cnt):
+        """pf_fuse_partial on rows [row0, row1) only (no zeroing elsewhere)."""
+        self._check(self.L.pf_fuse_partial_rows(self.h, _ptr(tiles), _ptr(coeffs), t0, t1, out_w,
+                                                out_w // 2, float(zr[0]), float(zr[1]), level,
+                                                int(row0), int(row1), _ptr(lsum), _ptr(cnt)))
+
+    def fuse_coverage_rows(self, out_w, zr, level, row0, row1, cnt):
+        """Coverage count of every tile on rows [row0, row1) (layout-only)."""
+        self._check(self.L.pf_fuse_coverage_rows(self.h, out_w, out_w // 2, float(zr[0]),
+                                                 float(zr[1]), level, int(row0), int(row1),
+                                                 _ptr(cnt)))
+
+    def fuse_normalize_rows(self, lsum, cnt, out_w, zr, level, row0, row1, lnorm):
+        self._check(self.L.pf_fuse_normalize_rows(self.h, _ptr(lsum), _ptr(cnt), out_w,
+                                                  out_w // 2, float(zr[0]), float(zr[1]), level,
+                                                  int(row0), int(row1), _ptr(lnorm)))
+
+    def fuse_tile_rows(self, out_w, zr, level, t0, t1):
+        """(ymin, ymax): rows where tiles [t0, t1) have non-zero partial sums (ymin > ymax: none)."""
+        lo, hi = C.c_int(), C.c_int()
+        self._check(self.L.pf_fuse_tile_rows(self.h, out_w, out_w // 2, float(zr[0]),
+                                             float(zr[1]), level, int(t0), int(t1), C.byref(lo),
+                                             C.byref(hi)))
+        return lo.value, hi.value
+
+    def rows_add(self, dst, src):
+        """dst += src (same-size fp32 device tensors), on the context's stream."""
+        assert dst.numel() == src.numel()
+        self._check(self.L.pf_rows_add(self.h, _ptr(dst), _ptr(src), dst.numel()))
 
     def fuse_seed(self, emap, prev, out_w, zr, level, buf):
         ew, eh, ec = _emap_dims(emap) if emap is not None else (0, 0, 0)

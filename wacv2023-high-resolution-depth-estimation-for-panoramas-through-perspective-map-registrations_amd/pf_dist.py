@@ -113,13 +113,28 @@ def fuse_tile_sharded(backend, nlevels, ntiles, rank, world, comm=None):
 
 # ---------------------------------------------------------------------------------------------
 # Row-band sharding of the sweeps: removes the Amdahl ceiling of
-# fuse_tile_sharded, whose Jacobi runs on rank 0 alone.  Every rank scatters its tiles' targets,
-# the grids are all-reduced, and each rank sweeps its own contiguous band of rows; before every
-# pass but a level's first, the T+1 rows nearest each band edge are exchanged with the
-# neighbouring ranks (a pass of depth T reads rows row0-T-1 .. row1+T).  Each band row is
-# computed exactly as in the one-GPU fusion (the kernels are the same; the band is just the row
-# range of the chunks), so the result is bit-identical.  After a level its bands are broadcast
-# so every rank holds the full buffer the next level upsamples; the u16 bands likewise.
+# fuse_tile_sharded, whose Jacobi runs on rank 0 alone.  Every rank sweeps its own contiguous band
+# of rows; before every pass but a level's first, the T+1 rows nearest each band edge are
+# exchanged with the neighbouring ranks (a pass of depth T reads rows row0-T-1 .. row1+T).  Each
+# band row is computed exactly as in the one-GPU fusion (the kernels are the same; the band is just
+# the row range of the chunks), so the result is bit-identical.
+#
+# Round 5: every exchange carries only the rows its receiver reads.
+#  * Targets: a sparse reduce-scatter by band rows.  The tiles are dealt to the ranks in layout
+#    order, which for the band layouts is zenith band by zenith band, and the row bands start at
+#    the first row of each rank's tiles (band_bounds), so a rank's tiles feed its own rows plus the
+#    one boundary row its neighbour shares.  A rank computes its tiles' partial sums only on the
+#    rows it needs (its band + halo) and the rows it sends (pf_fuse_partial_rows); it sends each
+#    other rank the rows of that rank's band + halo where its tiles are non-zero -- in practice the
+#    K = T+1 halo rows to each neighbour -- and adds what it receives (pf_rows_add).  The coverage
+#    count is layout-only, so every rank counts its own rows (pf_fuse_coverage_rows): only fp32
+#    sums travel, never counts.
+#  * Between levels: no broadcast of the bands.  The next level's first pass reads the 2x
+#    upsample of the previous level on its band + halo, i.e. about T/2 + 2 rows of the
+#    neighbouring ranks' previous bands, which they send (prev_exchange).
+#  * The u16 result is gathered to rank 0 only.
+#  * Rank 0 and the last rank own the rows above / below the band (k_border).
+# DESIGN.md section 6 tabulates the bytes per rank per panorama at C5.
 
 class TorchComm:
     """The collectives fuse_row_sharded / fuse_tile_sharded need, over torch.distributed (RCCL
@@ -182,78 +197,242 @@ class TorchComm:
 
 
 def band_rows(h0, h1, rank, world):
-    """[row0, row1) of rank's band of the level rows h0..h1."""
+    """[row0, row1) of rank's band of the level rows h0..h1 (even split)."""
     lo, hi = shard_range(h1 - h0 + 1, rank, world)
     return h0 + lo, h0 + hi
 
 
-def fuse_row_sharded(backend, nlevels, ntiles, rank, world, comm=None):
+def band_bounds(h0, h1, world, extents=None, halo=0):
+    """Boundaries [b_0 = h0, b_1, .., b_world = h1 + 1] of the row bands: rank r sweeps
+    [b_r, b_r+1).  extents[r] = (ymin, ymax), the rows where rank r's tiles have non-zero partial
+    sums; when every rank has tiles and their first rows ascend with the rank (a band layout dealt
+    in layout order), b_r = rank r's first row, so the partial sums stay local except for the
+    boundary row and the halo.  Otherwise, or if a band would be thinner than `halo` + 1 rows, an
+    even split.  A function of the layout only: identical on every rank."""
+    even = [band_rows(h0, h1, r, world)[0] for r in range(world)] + [h1 + 1]
+    if not extents or world == 1:
+        return even
+    b = [h0] + [extents[r][0] for r in range(1, world)] + [h1 + 1]
+    if any(lo > hi for lo, hi in extents) or \
+            any(b[r + 1] - b[r] < halo + 1 for r in range(world)):
+        return even
+    return b
+
+
+def _span(a, b):
+    """Intersection of two half-open row ranges, or None."""
+    lo, hi = max(a[0], b[0]), min(a[1], b[1])
+    return (lo, hi) if lo < hi else None
+
+
+def owned_rows(bounds, h, rank):
+    """Rows a rank owns at a level: its band, plus all rows above it (rank 0) or below it (the
+    last rank) -- the border rows of k_border."""
+    world = len(bounds) - 1
+    lo = 0 if rank == 0 else bounds[rank]
+    hi = h if rank == world - 1 else bounds[rank + 1]
+    return lo, hi
+
+
+def prev_rows_needed(bounds, h0, h1, K, hp, rank):
+    """Rows of the previous level (hp rows) a rank's first pass and border read at this level: the
+    2x upsample of its band + halo [b_r - K, b_r+1 + K) (a virtual column past a row end reaches
+    one row more), all rows above for rank 0 and below for the last rank."""
+    world = len(bounds) - 1
+    lo = 0 if rank == 0 else max(0, ((max(h0, bounds[rank] - K - 1) - 1) >> 1) - 1)
+    hi = hp if rank == world - 1 else min(hp, ((min(h1, bounds[rank + 1] + K) + 1) >> 1) + 2)
+    return lo, hi
+
+
+class ExchangeLog:
+    """Bytes each rank moves, per kind of exchange (DESIGN.md section 6's model is checked
+    against it in tests/test_dist.py)."""
+
+    def __init__(self):
+        self.sent = {}
+
+    def add(self, kind, nbytes):
+        self.sent[kind] = self.sent.get(kind, 0) + int(nbytes)
+
+
+def fuse_row_sharded(backend, nlevels, ntiles, rank, world, comm=None, log=None):
     """One panorama's fusion with tiles AND rows sharded over `world` ranks.
 
     backend (one rank's device):
-      partial(level, t0, t1) -> (lsum, cnt)   the targets of tiles [t0, t1), full-level grids
-      multicover_count / multicover / multicover_patch   as fuse_tile_sharded
       dims(level) -> (w, h, h0, h1)
-      plane(level) -> a new full-level fp32 buffer (flat)
-      normalize(level, lsum, cnt) -> lnorm
+      plane(level) -> a new full-level fp32 buffer (flat); scratch(n) -> n fp32
+      tile_rows(level, t0, t1) -> (ymin, ymax)   rows with non-zero sums of tiles [t0, t1)
+      partial_rows(level, t0, t1, row0, row1, lsum, cnt)   the sums of tiles [t0, t1) on rows
+                                               [row0, row1) (cnt: their coverage count)
+      coverage_rows(level, row0, row1, cnt)    the count of ALL tiles on rows [row0, row1)
+      rows_add(dst, src)                       dst += src (device views)
+      multicover_count / multicover / multicover_patch   as fuse_tile_sharded
+      normalize_rows(level, lsum, cnt, row0, row1, lnorm)
       plan(level, nbands) -> [T, ...]          identical on every rank
       border(level, prev, a, b)               rows outside [h0, h1] (u16 `out` on the last level)
       band_pass(level, lnorm, src_mode, src, dst, T, row0, row1, last, prev)
                                                src_mode 0: src, 1: upsample prev, 2: emap seed
-      out                                      the u16 result plane (flat), filled on every rank
-    comm: TorchComm (or a stand-in with the same methods); None for world == 1.
-    Returns the final level's band-assembled buffer (None for the last level, whose result is
-    backend.out)."""
+      out                                      the u16 result plane (flat); complete on rank 0
+    comm: TorchComm (or a stand-in with exchange / all_reduce_sum / agree); None for world 1.
+    log: an ExchangeLog, or None.
+    Returns the bounds of the last level's bands."""
     t0, t1 = shard_range(ntiles, rank, world)
-    prev = None
+    prev, pbounds, bounds = None, None, None
     for level in range(nlevels):
         last = level == nlevels - 1
-        lsum, cnt = backend.partial(level, t0, t1)
-        if world > 1:
-            comm.all_reduce_sum(lsum)
-            comm.all_reduce_sum(cnt)
-            if backend.multicover_count(level):  # exact sums where 3+ tiles meet
-                contrib = backend.multicover(level, t0, t1)
-                comm.all_reduce_sum(contrib)
-                backend.multicover_patch(level, contrib, lsum)
-        lnorm = backend.normalize(level, lsum, cnt)
         w, h, h0, h1 = backend.dims(level)
-        r0, r1 = band_rows(h0, h1, rank, world)
         plan = backend.plan(level, world)
         if world > 1 and hasattr(comm, "agree"):
             # one plan for all ranks: rank 0's (the plan depends on per-process state -- CU
             # count, occupancy, PF_J* overrides -- and mismatched passes would hang the exchanges)
             plan = comm.agree(plan, 0, getattr(backend, "device", None))
-        if world > 1 and (h1 - h0 + 1) // world < max(plan) + 1:
+        K = max(plan) + 1
+        ext = [backend.tile_rows(level, *shard_range(ntiles, r, world)) for r in range(world)]
+        bounds = band_bounds(h0, h1, world, ext, K)
+        if world > 1 and min(bounds[r + 1] - bounds[r] for r in range(world)) < K:
             raise ValueError(f"level {level}: {h1 - h0 + 1} band rows over {world} ranks leave "
-                             f"bands thinner than the {max(plan) + 1}-row halo")
+                             f"bands thinner than the {K}-row halo")
+        r0, r1 = bounds[rank], bounds[rank + 1]
+        need = [(max(h0, bounds[d] - K), min(h1 + 1, bounds[d + 1] + K)) for d in range(world)]
+        e0, e1 = need[rank]
+        # the previous level's rows this rank's first pass / border read, from their owners
+        if level > 0 and world > 1:
+            hp = backend.dims(level - 1)[1]
+            wp = backend.dims(level - 1)[0]
+            sends, recvs = [], []
+            mine = owned_rows(pbounds, hp, rank)
+            for d in range(world):
+                if d == rank:
+                    continue
+                sp = _span(prev_rows_needed(bounds, h0, h1, K, hp, d), mine)
+                if sp:
+                    sends.append((d, prev[sp[0] * wp:sp[1] * wp]))
+                rp = _span(prev_rows_needed(bounds, h0, h1, K, hp, rank),
+                           owned_rows(pbounds, hp, d))
+                if rp:
+                    recvs.append((d, prev[rp[0] * wp:rp[1] * wp]))
+            comm.exchange(sends, recvs)
+            if log:
+                log.add("prev_halo", sum(4 * t.numel() for _, t in sends))
+        # targets: this rank's tiles on the rows it needs and the rows it sends
+        lsum, cnt, lnorm = backend.plane(level), backend.plane(level), backend.plane(level)
+        mlo, mhi = ext[rank][0], ext[rank][1] + 1
+        lo, hi = (min(e0, mlo), max(e1, mhi)) if mlo < mhi else (e0, e1)
+        backend.partial_rows(level, t0, t1, lo, hi, lsum, cnt)
+        if world > 1:
+            backend.coverage_rows(level, e0, e1, cnt)  # every tile's count: layout-only
+            sends, recvs, bufs = [], [], []
+            for d in range(world):
+                if d == rank:
+                    continue
+                sp = _span(need[d], (mlo, mhi))
+                if sp:
+                    sends.append((d, lsum[sp[0] * w:sp[1] * w]))
+                s_lo, s_hi = ext[d][0], ext[d][1] + 1
+                rp = _span(need[rank], (s_lo, s_hi)) if s_lo < s_hi else None
+                if rp:
+                    buf = backend.scratch((rp[1] - rp[0]) * w)
+                    recvs.append((d, buf))
+                    bufs.append((rp, buf))
+            comm.exchange(sends, recvs)
+            if log:
+                log.add("targets", sum(4 * t.numel() for _, t in sends))
+            for (a, b), buf in bufs:  # one addend per covering tile: exact up to 2 (below: 3+)
+                backend.rows_add(lsum[a * w:b * w], buf)
+            if backend.multicover_count(level):  # exact sums where 3+ tiles meet
+                contrib = backend.multicover(level, t0, t1)
+                comm.all_reduce_sum(contrib)
+                if log:
+                    log.add("multicover", 4 * contrib.numel())
+                backend.multicover_patch(level, contrib, lsum)
+        backend.normalize_rows(level, lsum, cnt, e0, e1, lnorm)
         a, b = backend.plane(level), backend.plane(level)
-        backend.border(level, prev, a, b)
+        if rank == 0 or rank == world - 1:  # the rows above / below the band
+            backend.border(level, prev, a, b)
         src, dst = None, a
         for i, T in enumerate(plan):
             if i > 0 and world > 1:
                 k = T + 1
                 sends, recvs = [], []
                 if rank > 0:
-                    lo = max(r0 - k, h0)
+                    lo_ = max(r0 - k, h0)
                     sends.append((rank - 1, src[r0 * w:min(r0 + k, r1) * w]))
-                    recvs.append((rank - 1, src[lo * w:r0 * w]))
+                    recvs.append((rank - 1, src[lo_ * w:r0 * w]))
                 if rank < world - 1:
-                    hi = min(r1 + k, h1 + 1)
+                    hi_ = min(r1 + k, h1 + 1)
                     sends.append((rank + 1, src[max(r1 - k, r0) * w:r1 * w]))
-                    recvs.append((rank + 1, src[r1 * w:hi * w]))
+                    recvs.append((rank + 1, src[r1 * w:hi_ * w]))
                 comm.exchange(sends, recvs)
+                if log:
+                    log.add("pass_halo", sum(4 * t.numel() for _, t in sends))
             mode = (2 if level == 0 else 1) if i == 0 else 0
             fin = last and i == len(plan) - 1
             backend.band_pass(level, lnorm, mode, src, dst, T, r0, r1, fin, prev)
             src, dst = dst, (b if dst is a else a)
-        res = backend.out if last else src
-        if world > 1:
-            for r in range(world):
-                q0, q1 = band_rows(h0, h1, r, world)
-                comm.broadcast(res[q0 * w:q1 * w], r)
-        prev = None if last else res
-    return prev
+        prev, pbounds = (None if last else src), bounds
+    # the u16 result: every rank's owned rows to rank 0
+    if world > 1:
+        import torch
+        w, h = backend.dims(nlevels - 1)[:2]
+
+        def out8(a_, b_):  # as bytes: gloo has no 16-bit integers
+            return backend.out[a_ * w:b_ * w].view(torch.uint8)
+        if rank == 0:
+            recvs = [(s, out8(*owned_rows(bounds, h, s))) for s in range(1, world)]
+            comm.exchange([], recvs)
+        else:
+            snd = out8(*owned_rows(bounds, h, rank))
+            comm.exchange([(0, snd)], [])
+            if log:
+                log.add("gather_u16", snd.numel())
+    return bounds
+
+
+def exchange_model(dims, plans, ext, world, multicover=None):
+    """Bytes each rank SENDS per panorama in fuse_row_sharded, by kind -- the same row arithmetic
+    as the flow, from the layout alone (tests/test_dist.py checks it against
+    the bytes a gloo run logs).  dims[l] = (w, h, h0, h1); plans[l] = the pass depths of level l;
+    ext[l][r] = (ymin, ymax) of rank r's tiles at level l; multicover[l] = that level's count of
+    (pixel, tile) pairs covered three or more times (one fp32 each, all-reduced)."""
+    res = [dict() for _ in range(world)]
+
+    def add(r, kind, n):
+        if n:
+            res[r][kind] = res[r].get(kind, 0) + n
+    if world == 1:
+        return res
+    pb = None
+    for lv, (w, h, h0, h1) in enumerate(dims):
+        K = max(plans[lv]) + 1
+        b = band_bounds(h0, h1, world, ext[lv], K)
+        need = [(max(h0, b[d] - K), min(h1 + 1, b[d + 1] + K)) for d in range(world)]
+        for r in range(world):
+            if lv > 0:
+                wp, hp = dims[lv - 1][:2]
+                for d in range(world):
+                    if d != r:
+                        sp = _span(prev_rows_needed(b, h0, h1, K, hp, d), owned_rows(pb, hp, r))
+                        add(r, "prev_halo", 4 * wp * (sp[1] - sp[0]) if sp else 0)
+            lo, hi = ext[lv][r][0], ext[lv][r][1] + 1
+            for d in range(world):
+                if d != r and lo < hi:
+                    sp = _span(need[d], (lo, hi))
+                    add(r, "targets", 4 * w * (sp[1] - sp[0]) if sp else 0)
+            if multicover and multicover[lv]:
+                add(r, "multicover", 4 * multicover[lv])
+            r0, r1 = b[r], b[r + 1]
+            for T in plans[lv][1:]:
+                k = T + 1
+                if r > 0:
+                    add(r, "pass_halo", 4 * w * (min(r0 + k, r1) - r0))
+                if r < world - 1:
+                    add(r, "pass_halo", 4 * w * (r1 - max(r1 - k, r0)))
+        pb = b
+    w, h = dims[-1][:2]
+    for r in range(1, world):
+        lo, hi = owned_rows(pb, h, r)
+        add(r, "gather_u16", 2 * w * (hi - lo))
+    return res
 
 
 class HipRowShardBackend:
@@ -282,20 +461,29 @@ class HipRowShardBackend:
         w, h = self.levels[level][:2]
         return torch.empty(h * w, dtype=torch.float32, device=self.tiles.device)
 
-    def partial(self, level, t0, t1):
-        lsum, cnt = self.plane(level), self.plane(level)
-        self.fz.fuse_partial(self.tiles, self.coeffs, t0, t1, self.out_w, self.zr, level,
-                             lsum, cnt)
-        return lsum, cnt
+    def scratch(self, n):
+        import torch
+        return torch.empty(n, dtype=torch.float32, device=self.tiles.device)
+
+    def tile_rows(self, level, t0, t1):
+        return self.fz.fuse_tile_rows(self.out_w, self.zr, level, t0, t1)
+
+    def partial_rows(self, level, t0, t1, row0, row1, lsum, cnt):
+        self.fz.fuse_partial_rows(self.tiles, self.coeffs, t0, t1, self.out_w, self.zr, level,
+                                  row0, row1, lsum, cnt)
+
+    def coverage_rows(self, level, row0, row1, cnt):
+        self.fz.fuse_coverage_rows(self.out_w, self.zr, level, row0, row1, cnt)
+
+    def rows_add(self, dst, src):
+        self.fz.rows_add(dst, src)
 
     multicover_count = HipTileShardBackend.multicover_count
     multicover = HipTileShardBackend.multicover
     multicover_patch = HipTileShardBackend.multicover_patch
 
-    def normalize(self, level, lsum, cnt):
-        lnorm = self.plane(level)
-        self.fz.fuse_normalize(lsum, cnt, self.out_w, self.zr, level, lnorm)
-        return lnorm
+    def normalize_rows(self, level, lsum, cnt, row0, row1, lnorm):
+        self.fz.fuse_normalize_rows(lsum, cnt, self.out_w, self.zr, level, row0, row1, lnorm)
 
     def plan(self, level, nbands):
         return self.fz.fuse_band_plan(self.out_w, self.zr, level, nbands)
