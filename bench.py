@@ -426,7 +426,7 @@ def rank_seeds(batch, rank):
 # pipelined steps: the next batch's warp waits for this level of the current fusion (-1: only for
 # the fusion that last read its buffer).  Level 0 (default): the memory-bound warp runs beside
 # the finer levels' streaming passes instead of contending with the resident level-0 kernel,
-# which fills every CU -- measured on MI355X (tools/warp_after_ab.sh, three alternating rounds):
+# which fills every CU -- measured on MI355X (recipe: tools/gpu_round.sh ab with PF_WARP_AFTER, three alternating rounds):
 # 14.12-14.28k panoramas/s against 13.51-14.02k (-1) and 13.94-14.32k (1).
 WARP_AFTER_LEVEL = int(os.environ.get("PF_WARP_AFTER", "0"))
 

@@ -1,7 +1,21 @@
 #!/bin/bash
-# GPU-box session: parity tests, smoke, bench, rocprofv3 kernel trace.  Every GPU step has its own
-# time limit; a crash/abort/timeout (exit >= 2 other than pytest's test-failure code 1) ends the
-# script before any further GPU step.
+# GPU-box session recipes, one step per word of $STEPS (default: tests smoke bench prof).  Every
+# GPU step has its own time limit; a crash / abort / timeout (exit >= 2 other than pytest's
+# test-failure code 1) ends the script before any further GPU step.  Outputs under gpurun_out/.
+#
+#   tests    the -m gpu suite                        -> pytest_gpu.log
+#   smoke    __graft_entry__.smoke()                  -> smoke.log
+#   bench    the default bench line (C3, two lanes)   -> bench.log
+#   prof     kernel trace + stats of a short bench    -> prof/
+#   serial   kernel trace of serial steps (--pipeline 0) and the per-level Jacobi times
+#            (tools/ktrace_levels.py): the basis of the Jacobi roofline -> serial/
+#   pmc      HBM-traffic PMC passes (tools/pmc_round.sh) -> pmc_traffic.txt
+#   c5       the C5 line at world 1 (+ the 8-rank byte model)  -> bench_c5.log
+#   c4       bench.py --gpus 8 on the one GPU (gloo, --same-device): C4's 8-rank shape
+#   rgb      the RGB warp probe (tools/rgb_probe.py)   -> rgb.log
+#   ab       A/B of environment knobs: $VARIANTS = "NAME:ENV=VAL,ENV=VAL NAME2:" run in $ROUNDS
+#            alternating rounds on the default bench line (-> ab/NAME.R.log, one summary line
+#            each); BENCH_ARGS adds bench.py flags
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 OUT=gpurun_out
@@ -9,26 +23,63 @@ mkdir -p $OUT
 export TMPDIR=/tmp
 STEPS="${STEPS:-tests smoke bench prof}"
 ok() { local rc=$1; [ "$rc" -eq 0 ] || [ "$rc" -eq 1 ]; }
+summ() {  # one line of a bench JSON: value and stage times
+  python3 - "$1" "$2" <<'PY'
+import json, sys
+d = json.loads([l for l in open(sys.argv[1]) if l.startswith("{")][-1])
+st = d.get("stages", {})
+print(f"{sys.argv[2]:>10}  value {d['value']:.0f}  ms/step {d['ms_per_step']:.3f}  " +
+      "  ".join(f"{k} {v['ms_per_step']:.3f}" for k, v in st.items()
+                if v["ms_per_step"] and k != "metrics"))
+PY
+}
 for s in $STEPS; do
   case $s in
     tests)
-      timeout -k 10 600 python -u -m pytest tests -x -v -m gpu --timeout 120 --timeout-method thread > $OUT/pytest_gpu.log 2>&1; rc=$?
+      timeout -k 10 900 python -u -m pytest tests -x -v -m gpu --timeout 200 --timeout-method thread > $OUT/pytest_gpu.log 2>&1; rc=$?
       echo "pytest rc=$rc"; tail -5 $OUT/pytest_gpu.log; ok $rc || exit $rc ;;
     smoke)
       timeout -k 10 300 python -c 'import __graft_entry__ as g; g.smoke()' > $OUT/smoke.log 2>&1; rc=$?
       echo "smoke rc=$rc"; tail -3 $OUT/smoke.log; [ $rc -eq 0 ] || exit $rc ;;
     bench)
       timeout -k 10 600 python bench.py > $OUT/bench.log 2>&1; rc=$?
-      echo "bench rc=$rc"; tail -2 $OUT/bench.log; [ $rc -eq 0 ] || exit $rc ;;
-    c5)
-      timeout -k 10 300 python bench.py --mode c5 --steps 3 --warmup 1 > $OUT/bench_c5.log 2>&1; rc=$?
-      echo "c5 rc=$rc"; tail -2 $OUT/bench_c5.log; [ $rc -eq 0 ] || exit $rc ;;
-    pmc)
-      bash tools/pmc_round.sh; rc=$?; [ $rc -eq 0 ] || exit $rc ;;
+      echo "bench rc=$rc"; [ $rc -eq 0 ] || { tail -5 $OUT/bench.log; exit $rc; }; summ $OUT/bench.log bench ;;
     prof)
       timeout -k 10 600 rocprofv3 --kernel-trace --stats -d $OUT/prof -o run --output-format csv -- \
         python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline > $OUT/prof.log 2>&1; rc=$?
-      echo "prof rc=$rc"; tail -2 $OUT/prof.log; [ $rc -eq 0 ] || exit $rc ;;
+      echo "prof rc=$rc"; tail -2 $OUT/prof.log | cut -c1-300; [ $rc -eq 0 ] || exit $rc ;;
+    serial)
+      rm -rf $OUT/serial; mkdir -p $OUT/serial
+      timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/serial/prof -o run --output-format csv -- \
+        python3 bench.py --steps 5 --warmup 2 --no-cpu-baseline --no-extra-configs --pipeline 0 > $OUT/serial/bench.log 2>&1; rc=$?
+      echo "serial rc=$rc"; [ $rc -eq 0 ] || exit $rc
+      python3 tools/ktrace_levels.py $(find $OUT/serial/prof -name "run_kernel_trace.csv" | head -1) > $OUT/serial/levels.txt
+      tail -12 $OUT/serial/levels.txt ;;
+    pmc)
+      bash tools/pmc_round.sh; rc=$?; [ $rc -eq 0 ] || exit $rc ;;
+    c5)
+      timeout -k 10 300 python bench.py --mode c5 --steps 5 --warmup 2 --no-cpu-baseline > $OUT/bench_c5.log 2>&1; rc=$?
+      echo "c5 rc=$rc"; tail -c 800 $OUT/bench_c5.log; [ $rc -eq 0 ] || exit $rc ;;
+    c4)
+      timeout -k 10 600 python3 bench.py --gpus 8 --same-device --backend gloo --steps 3 --warmup 1 \
+        --no-cpu-baseline --no-extra-configs --prof-steps 1 > $OUT/c4_8rank.log 2>&1; rc=$?
+      echo "c4 rc=$rc"; tail -c 1200 $OUT/c4_8rank.log; [ $rc -eq 0 ] || exit $rc ;;
+    rgb)
+      timeout -k 10 120 python3 tools/rgb_probe.py > $OUT/rgb.log 2>&1; rc=$?
+      echo "rgb rc=$rc"; cat $OUT/rgb.log | tail -2; [ $rc -eq 0 ] || exit $rc ;;
+    ab)
+      mkdir -p $OUT/ab
+      for r in $(seq 1 ${ROUNDS:-2}); do
+        for v in ${VARIANTS:-base:}; do
+          name=${v%%:*}; envs=${v#*:}
+          ( for kv in ${envs//,/ }; do [ -n "$kv" ] && export "$kv"; done
+            timeout -k 10 300 python bench.py --no-cpu-baseline --no-extra-configs ${BENCH_ARGS:-} \
+              > $OUT/ab/$name.$r.log 2>&1 ); rc=$?
+          [ $rc -eq 0 ] || { echo "$name rc=$rc"; tail -5 $OUT/ab/$name.$r.log; exit $rc; }
+          summ $OUT/ab/$name.$r.log $name
+        done
+      done ;;
+    *) echo "unknown step $s"; exit 2 ;;
   esac
 done
 echo "all done"

@@ -1,4 +1,4 @@
-"""Per-launch SQ counters of k_warp_depth from tools/warp_sq.sh (new vs old library)."""
+"""Per-launch SQ counters of k_warp_depth from profiles/r03/warp/warp_sq_summary.txt; recipe: tools/gpu_round.sh pmc-style passes (new vs old library)."""
 import collections
 import csv
 import glob

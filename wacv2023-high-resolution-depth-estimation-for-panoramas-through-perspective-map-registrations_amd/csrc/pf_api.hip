@@ -87,7 +87,8 @@ struct pf_ctx {
     // boxes, per tile pixel the corner index in its box and the (fx, fy) weights; built on
     // first use
     int wmap_pw = 0, wmap_ph = 0, npatch = 0;
-    DevBuf wmap, wfxy, wpatch;
+    DevBuf wmap, wfxy, wpatch, wunits;  // wunits: the ragged footprints' unit table
+    std::vector<WarpPatch> wpatch_grid_h;  // the layout's plain 32x32 patch grid
     // workspace
     DevBuf buf[3], lnorm, coeffs, lsum_ws, metrics_ws, reg_sums, reg_active;
     // SolveDepthBySmoothing (pf_smooth.hip): boxes, grid tables, per-pixel source and mask
@@ -353,7 +354,7 @@ void pf_destroy(pf_ctx* c)
     (void)hipStreamSynchronize(c->stream);
     DevBuf* all[] = {&c->geom, &c->reg, &c->reg_sidx, &c->rcols, &c->rrows, &c->rgbtap, &c->rgb_off, &c->rgbpatch, &c->rgbunits, &c->rgbloc, &c->rgbw,
                      &c->buf[0], &c->buf[1], &c->buf[2], &c->lnorm, &c->coeffs, &c->lsum_ws,
-                     &c->wmap, &c->wfxy, &c->wpatch, &c->metrics_ws, &c->reg_sums,
+                     &c->wmap, &c->wfxy, &c->wpatch, &c->wunits, &c->metrics_ws, &c->reg_sums,
                      &c->reg_active, &c->sm_box, &c->sm_cols, &c->sm_rows, &c->sm_src,
                      &c->sm_mask, &c->seed_ecol, &c->seed_erow, &c->jres_x, &c->jres_sync,
                      &c->sm_sync, &c->sm_list, &c->sm_off};
@@ -621,8 +622,9 @@ int pf_set_tiles(pf_ctx* c, const pf_window* fovs, const pf_window* ranges, int 
     const int pe = warp_patch_edge(), peh = warp_patch_height();
     for (int i = 0; i < ntiles; i++)
         for (int y = 0; y < tile_h[i]; y += peh)
-            for (int x = 0; x < tile_w[i]; x += pe) patches.push_back(WarpPatch{i, x, y, 0, 0, 0, 0, 0});
+            for (int x = 0; x < tile_w[i]; x += pe) patches.push_back(WarpPatch{i, x, y, 0, 0, 0, 0, 0, 0, 0});
     c->npatch = (int)patches.size();
+    c->wpatch_grid_h = patches;
     int rc;
     if ((rc = upload(c, c->wpatch, patches))) return rc;
     if ((rc = upload(c, c->geom, c->geom_h))) return rc;
@@ -894,7 +896,7 @@ static int check_emap(pf_ctx* c, const float* emap, int ew, int eh, int ec)
 // overhead in update units), PF_JC=4 (4 columns per lane, builds with PF_JACOBI_C4 only).
 struct JacobiTuning {
     int C = 2, Tmax = 10;  // PF_JC=0: per level, the cheaper of 2 and 4 by the cost model
-    double step_overhead = 3.0, lone_cycles = 4.0;  // swept on MI355X (tools/jsweep.sh)
+    double step_overhead = 3.0, lone_cycles = 4.0;  // swept on MI355X (profiles/r02/jacobi; recipe: tools/gpu_round.sh ab)
     double c4_eff = 23.0 / 26.0;  // packed C=4 issue per pixel-update relative to C=2
     double pipe_overhead = 1.0;   // pipelined engine: barrier + exchange per step, update units
     // per pass, in the cost units of best_chunks (~10 ns each at C3): a launch's fixed cost
@@ -1775,8 +1777,15 @@ int pf_warp_depth(pf_ctx* c, const float* pano, int pw, int ph, int batch,
         // call per panorama size blocks the host (the staging memory is reused).
         const size_t kStagePix = (size_t)1 << 24;
         const size_t cap = std::max((size_t)c->npix_max, std::min((size_t)npix, kStagePix));
-        std::vector<uint32_t> wxy(cap);
+        std::vector<uint32_t> wxy(cap), loc;
         std::vector<float> wf(2 * cap);
+        // ragged footprints (host, warp_patches_host) unless PF_WARP_RAGGED=0 or pw % 4 != 0;
+        // else the bounding boxes of k_patch_box / k_warp_local
+        const char* rg = getenv("PF_WARP_RAGGED");
+        const bool ragged = (pw % 4) == 0 && !(rg && atoi(rg) == 0);
+        std::vector<WarpPatch> patches;
+        std::vector<uint32_t> units;
+        if (ragged) loc.resize(cap);
         for (int p0 = 0; p0 < c->ntiles;) {
             const size_t off0 = (size_t)c->geom_h[p0].pix_off;
             size_t n = 0;
@@ -1786,25 +1795,62 @@ int pf_warp_depth(pf_ctx* c, const float* pano, int pw, int ph, int batch,
                 const size_t m = (size_t)g.w * g.h;
                 if (p1 > p0 && n + m > cap) break;
                 warp_coords_host(g, pw, ph, wxy.data() + n, wf.data() + 2 * n);
+                if (ragged)
+                    warp_patches_host(g, p1, wxy.data() + n, pw, ph, patches, units,
+                                      loc.data() + n);
                 n += m;
             }
-            HIPCHK(c, hipMemcpyAsync((uint32_t*)c->wmap.p + off0, wxy.data(), 4 * n,
-                                     hipMemcpyHostToDevice, c->stream));
+            HIPCHK(c, hipMemcpyAsync((uint32_t*)c->wmap.p + off0, ragged ? loc.data() : wxy.data(),
+                                     4 * n, hipMemcpyHostToDevice, c->stream));
             HIPCHK(c, hipMemcpyAsync((float*)c->wfxy.p + 2 * off0, wf.data(), 8 * n,
                                      hipMemcpyHostToDevice, c->stream));
             HIPCHK(c, hipStreamSynchronize(c->stream));  // the staging run is reused
             p0 = p1;
         }
-        launch_warp_boxes(c->stream, (const TileGeom*)c->geom.p, (WarpPatch*)c->wpatch.p,
-                          c->npatch, pw, ph, (uint32_t*)c->wmap.p);
-        HIPCHK(c, hipGetLastError());
-        if ((rc = sort_warp_patches(c, pw))) return rc;
+        if (ragged) {
+            // footprint order, as sort_warp_patches: 32-row bands of the first staged unit, then
+            // its column (a wide patch: its first corner)
+            std::vector<long long> keys(patches.size());
+            for (size_t q = 0; q < patches.size(); q++) {
+                const WarpPatch& P = patches[q];
+                long long row, col;
+                if (P.units > 0) {
+                    const uint32_t e = units[P.uoff] / 4u;
+                    row = e / (uint32_t)pw;
+                    col = e % (uint32_t)pw;
+                } else {
+                    const TileGeom& g = c->geom_h[P.tile];
+                    row = 0;
+                    col = P.X0 + (long long)g.w * P.Y0;  // keep tile order among wide patches
+                }
+                keys[q] = (row / 32) * (1LL << 40) + col;
+            }
+            std::vector<size_t> ord(patches.size());
+            for (size_t q = 0; q < ord.size(); q++) ord[q] = q;
+            std::stable_sort(ord.begin(), ord.end(),
+                             [&](size_t a, size_t b) { return keys[a] < keys[b]; });
+            std::vector<WarpPatch> sp(patches.size());
+            for (size_t q = 0; q < ord.size(); q++) sp[q] = patches[ord[q]];
+            if (units.empty()) units.push_back(0u);
+            if ((rc = upload(c, c->wpatch, sp))) return rc;
+            if ((rc = upload(c, c->wunits, units))) return rc;
+            c->npatch = (int)sp.size();
+        } else {
+            // the plain patch grid (a ragged build for another size replaced it)
+            if ((rc = upload(c, c->wpatch, c->wpatch_grid_h))) return rc;
+            c->npatch = (int)c->wpatch_grid_h.size();
+            launch_warp_boxes(c->stream, (const TileGeom*)c->geom.p, (WarpPatch*)c->wpatch.p,
+                              c->npatch, pw, ph, (uint32_t*)c->wmap.p);
+            HIPCHK(c, hipGetLastError());
+            if ((rc = sort_warp_patches(c, pw))) return rc;
+        }
         c->wmap_pw = pw;
         c->wmap_ph = ph;
     }
     StageTimer t(c, PF_STAGE_WARP, batch * (4.0 * pw * ph + 4.0 * (double)npix), 1);
     launch_warp_depth(c->stream, (const TileGeom*)c->geom.p, c->ntiles,
-                      (const WarpPatch*)c->wpatch.p, c->npatch, (const uint32_t*)c->wmap.p,
+                      (const WarpPatch*)c->wpatch.p, (const uint32_t*)c->wunits.p, c->npatch,
+                      (const uint32_t*)c->wmap.p,
                       (const float*)c->wfxy.p, pano, pw, ph, (long long)pw * ph,
                       (const Resp*)resp, tiles, c->tile_elems, batch);
     HIPCHK(c, hipGetLastError());

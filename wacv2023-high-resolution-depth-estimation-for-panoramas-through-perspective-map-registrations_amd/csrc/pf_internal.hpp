@@ -92,8 +92,8 @@ struct RgbPatch {
     int pad[2];
 };
 static constexpr int kRgbPW = 64, kRgbPH = 16;  // RGB warp patch (4 pixels per thread)
-static constexpr int kRgbUnits = 256;            // 16-B units per patch: 4 KB of u8 = 4096 floats
-static constexpr int kRgbCap = 16 * kRgbUnits;   // LDS floats per parity (bytes widened to fp32)
+static constexpr int kRgbUnits = 512;            // 16-B units per patch (two per thread)
+static constexpr int kRgbCap = 16 * kRgbUnits;   // LDS bytes per parity: the u8 RGB rows as is
 
 // Synthetic depth-net response (same layout as pf_response in panofuse.h).
 struct Resp {
@@ -107,6 +107,10 @@ struct WarpPatch {
     int tile, X0, Y0;
     int gx0, gy0, bw, bh;  // box origin (column mod pw, row) and size, +1 row/column
     int wide;              // box larger than the LDS staging capacity: direct gathers
+    // ragged footprint (round 5, the default when pw % 4 == 0): the 16-B units of the panorama
+    // rows the patch's corners read, each row only over its corners' columns, listed as byte
+    // offsets at unit_tbl[uoff .. uoff + units) (warp_patches_host); 0 units = the box above
+    int uoff, units;
 };
 
 struct LevelDims {
@@ -327,6 +331,13 @@ int warp_patch_height();
 // host tables (pf_warp.hip): wxy/wfxy of one tile's pixels; the RGB taps of one tile
 void warp_coords_host(const TileGeom& g, int pw, int ph, uint32_t* wxy, float* wfxy);
 void rgb_taps_host(const RgbCam& cam, int W, int H, int pw, int ph, RgbTap* taps);
+// The depth warp's patches of one tile with ragged footprints (from its corner map wxy, as
+// warp_coords_host writes it): appended to `patches`, their units' byte offsets to `units`, and
+// per pixel loc = LDS float index of the top corner pair | of the bottom pair << 16 (for a "wide"
+// patch the global corner index with the x1/y1 flags of k_warp_local).  Needs pw % 4 == 0.
+void warp_patches_host(const TileGeom& g, int tile, const uint32_t* wxy, int pw, int ph,
+                       std::vector<WarpPatch>& patches, std::vector<uint32_t>& units,
+                       uint32_t* loc);
 // The RGB warp's patches of one tile (its taps at `taps`), appended to `patches`; their staged
 // units' byte offsets to `units` (kRgbUnits per patch); per pixel the LDS float indices of its
 // top and bottom corner pairs (loc: top | bottom << 16) and the GL_LINEAR weights (wts: ax, ay).
@@ -343,6 +354,7 @@ void launch_warp_rgb_box(hipStream_t s, const TileGeom* geom, const RgbPatch* pa
 void launch_warp_boxes(hipStream_t s, const TileGeom* geom, WarpPatch* patches, int npatch,
                        int pw, int ph, uint32_t* wloc);
 void launch_warp_depth(hipStream_t s, const TileGeom* geom, int ntiles, const WarpPatch* patches,
+                       const uint32_t* unit_tbl,
                        int npatch, const uint32_t* wloc, const float* wfxy, const float* pano,
                        int pw, int ph, long long pstride, const Resp* resp, float* tiles,
                        long long tstride, int batch);

@@ -29,7 +29,7 @@
 
 #ifndef PF_JNT
 // nt stores of the streamed passes' finished rows: 3.03 / 3.10 ms against 3.16 / 3.08 for the
-// plain stores in two alternating rounds (tools/r3_tgt.sh, profiles/r03/jnt/): within the noise
+// plain stores in two alternating rounds (profiles/r03/tgt and profiles/r03/jnt; recipe: tools/gpu_round.sh ab, profiles/r03/jnt/): within the noise
 #define PF_JNT 0
 #endif
 
@@ -59,7 +59,7 @@
 // register ring takes the packed pass from 132 VGPRs + 48 KB of LDS per 4-wave workgroup to
 // 166-167 VGPRs and no LDS -- the same 3 waves per SIMD -- and drops the T LDS reads per step:
 // C3 Jacobi stage 3.37-3.38 -> 3.19-3.24 ms, 14.10-14.35k -> 14.75-14.81k panoramas/s (three
-// alternating rounds on one MI355X, tools/r4_ab.sh)
+// alternating rounds on one MI355X, profiles/r04/ab_lreg; recipe: tools/gpu_round.sh ab)
 #define PF_JLREG_T 10
 #endif
 

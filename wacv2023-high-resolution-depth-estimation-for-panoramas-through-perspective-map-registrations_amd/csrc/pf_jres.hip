@@ -623,7 +623,7 @@ static void launch_cr(hipStream_t s, const JresArgs& A, int grid, int src_mode, 
 // Workgroup shape: PF_JRES_WAVES waves over a 64-row region -- 16 waves of 4 rows (default: one
 // workgroup per CU at <= 128 VGPRs) or 8 waves of 8 rows (two waves per SIMD at <= 256 VGPRs,
 // leaving a sixth of the register file to co-resident kernels).  Measured in the pipelined C3
-// step on MI355X (tools/jres_ab.sh, three alternating rounds): 13.64-13.97k panoramas/s for 16
+// step on MI355X (profiles/r03 logs; recipe: tools/gpu_round.sh ab, three alternating rounds): 13.64-13.97k panoramas/s for 16
 // waves, 13.66-13.76k for 8, 12.89-13.02k for the streaming passes.
 #ifndef PF_JRES_WAVES
 #define PF_JRES_WAVES 16

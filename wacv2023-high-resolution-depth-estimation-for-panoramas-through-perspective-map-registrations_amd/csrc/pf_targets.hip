@@ -135,7 +135,7 @@ __global__ void __launch_bounds__(256) k_targets_map(const TileGeom* __restrict_
 // (Depth2DepthTransform), staged in LDS, and the five-point stencils read LDS.  The per-pixel
 // arithmetic and the tile-order accumulation are exactly those of k_targets_map.
 // patch height: 8 rows (2 pixels per thread) stages 1.29 grid points per pixel instead of 1.55
-// at 4 rows; measured at C3 (tools/lib_ab.sh): 4 rows 0.687 ms, 8 rows 0.635, 16 rows 0.670
+// at 4 rows; measured at C3 (profiles/r02 logs; recipe: tools/gpu_round.sh ab): 4 rows 0.687 ms, 8 rows 0.635, 16 rows 0.670
 #ifndef PF_TGT_PH
 #define PF_TGT_PH 8
 #endif
@@ -151,7 +151,7 @@ static constexpr int kTNB = PF_TGT_NB;                           // panoramas pe
 #endif
 #ifndef PF_TGT_NT
 // nt stores of the target planes keep the tiles' lines in L2 for the neighbouring patches: the
-// stage went 0.629-0.633 -> 0.618-0.623 ms per C3 step (tools/r3_tgt.sh, profiles/r03/tgt/);
+// stage went 0.629-0.633 -> 0.618-0.623 ms per C3 step (profiles/r03/tgt and profiles/r03/jnt; recipe: tools/gpu_round.sh ab, profiles/r03/tgt/);
 // 4 / 16 panoramas per block measured 0.639-0.651 / 0.730
 #define PF_TGT_NT 1
 #endif

@@ -44,7 +44,7 @@ namespace pf {
 // one 32x8 patch per WAVE with its own LDS box and no workgroup barrier (waves drift and overlap
 // each other's latencies) instead of one 32x32 patch per 256-thread block with a barrier per
 // panorama (SQ counters: ~20% of the block form's wave-cycles wait at barriers).  Measured
-// slower on MI355X at C3 (tools/r3_wb.sh): 0.69 ms with 1024-float wave boxes, 0.83 with 512,
+// slower on MI355X at C3 (profiles/r03/warp/wb*.log; recipe: tools/gpu_round.sh ab): 0.69 ms with 1024-float wave boxes, 0.83 with 512,
 // against 0.53 for the block form (bit-identical tiles) -- the small boxes re-read more and send
 // more patches to the direct-gather path.  Off.
 #define PF_WARP_WAVEBOX 0
@@ -67,7 +67,7 @@ static_assert(PF_WARP_WAVEBOX || kCap % (4 * kWB) == 0, "whole 16-B staging slot
 #endif
 static constexpr int kNB = PF_WARP_BATCH;               // panoramas per block
 // Memory operation widths and cache policy, measured on MI355X at C3 (tools/warp_probe.py,
-// tools/r3_warp2.sh).  Round 2: 16-B staging loads 0.596 ms, 16-B row stores 0.600, both 0.637,
+// profiles/r03/warp; recipe: tools/gpu_round.sh ab).  Round 2: 16-B staging loads 0.596 ms, 16-B row stores 0.600, both 0.637,
 // against 0.586 for 4-B loads and stores.  Round 3, with the split LDS parities: nt tile stores
 // 0.545-0.551 ms against 0.560-0.569 (written tiles no longer evict the staged boxes' lines from
 // L2), and 16-B staging loads on top 0.527-0.531 (kept: the defaults below); 16-B stores through
@@ -80,7 +80,7 @@ static constexpr int kNB = PF_WARP_BATCH;               // panoramas per block
 #ifndef PF_WARP_SPLIT
 // the two staging parities in separate LDS halves (consecutive lanes read/write consecutive
 // dwords: conflict-free) instead of interleaved (stride-2 dwords: 2-way bank conflicts, 64% of
-// the kernel's LDS-active cycles on MI355X, tools/warp_sq.sh)
+// the kernel's LDS-active cycles on MI355X, profiles/r03/warp/warp_sq_summary.txt; recipe: tools/gpu_round.sh pmc-style passes)
 #define PF_WARP_SPLIT 1
 #endif
 #ifndef PF_WARP_STPOL
@@ -158,6 +158,97 @@ void warp_coords_host(const TileGeom& g, int pw, int ph, uint32_t* wxy, float* w
                 wfxy[2 * i + 1] = fy;
             }
     });
+}
+
+static inline long long floor_div(long long x, long long d) { return x >= 0 ? x / d : -((d - 1 - x) / d); }
+static inline int wrap_du_h(int d, int pw)
+{  // the column offset d in (-pw/2, pw/2] (k_patch_box's wrap_du, host side)
+    if (d > pw / 2) d -= pw;
+    if (d < -(pw / 2)) d += pw;
+    return d;
+}
+
+// Ragged footprints of the depth warp's 32x32 patches (round 5).  The bounding box of a patch's
+// corners (k_patch_box) holds the empty corners of a rotated footprint and whole rows of
+// columns no corner of that row reads; here each panorama row v of the footprint is staged only
+// over the columns [xlo(v), xhi(v)] its corners use (pixels with y0 == v read their (x0, x0+1) on
+// row v, pixels with y0 == v-1 on row v as y1), in whole 16-B units, the rows packed one after
+// another in LDS.  Columns unwrap around the patch's first corner (the azimuth seam: staging
+// wraps mod pw); rows past ph-1 (y1 clamped: fy == 0 there) stage row ph-1.
+void warp_patches_host(const TileGeom& g, int tile, const uint32_t* wxy, int pw, int ph,
+                       std::vector<WarpPatch>& patches, std::vector<uint32_t>& units,
+                       uint32_t* loc)
+{
+    const int cap = kCap / 4;  // 16-B units per staged footprint
+    std::vector<int> xlo, xhi, q0, off;
+    for (int Y0 = 0; Y0 < g.h; Y0 += kPatchH)
+        for (int X0 = 0; X0 < g.w; X0 += kPatch) {
+            const int X1 = std::min(g.w, X0 + kPatch), Y1 = std::min(g.h, Y0 + kPatchH);
+            const uint32_t m0 = wxy[(long long)Y0 * g.w + X0];
+            const int rx = (int)(m0 & 0xFFFFu);
+            int vmin = INT32_MAX, vmax = INT32_MIN;
+            for (int Y = Y0; Y < Y1; Y++)
+                for (int X = X0; X < X1; X++) {
+                    const int y0 = (int)(wxy[(long long)Y * g.w + X] >> 16);
+                    vmin = std::min(vmin, y0);
+                    vmax = std::max(vmax, y0);
+                }
+            const int nv = vmax - vmin + 2;
+            xlo.assign(nv, INT32_MAX);
+            xhi.assign(nv, INT32_MIN);
+            for (int Y = Y0; Y < Y1; Y++)
+                for (int X = X0; X < X1; X++) {
+                    const uint32_t m = wxy[(long long)Y * g.w + X];
+                    const int du = wrap_du_h((int)(m & 0xFFFFu) - rx, pw);
+                    const int r = (int)(m >> 16) - vmin;
+                    for (int k = r; k <= r + 1; k++) {
+                        xlo[k] = std::min(xlo[k], du);
+                        xhi[k] = std::max(xhi[k], du + 1);
+                    }
+                }
+            q0.resize(nv);
+            off.resize(nv);
+            long long nu = 0;
+            bool fits = nv <= ph;
+            for (int r = 0; r < nv && fits; r++) {
+                fits = xhi[r] - xlo[r] + 1 <= pw / 2;
+                const long long a = floor_div(rx + xlo[r], 4), b = floor_div(rx + xhi[r] + 4, 4);
+                q0[r] = (int)a;
+                off[r] = (int)nu;
+                nu += b - a;
+            }
+            WarpPatch P{};
+            P.tile = tile; P.X0 = X0; P.Y0 = Y0;
+            P.wide = (!fits || nu > cap) ? 1 : 0;
+            P.uoff = (int)units.size();
+            P.units = P.wide ? 0 : (int)nu;
+            if (!P.wide)
+                for (int r = 0; r < nv; r++) {
+                    const int row = std::min(vmin + r, ph - 1);
+                    const int n = (r + 1 < nv ? off[r + 1] : (int)nu) - off[r];
+                    for (int u = 0; u < n; u++) {
+                        const int col = (int)((((4LL * (q0[r] + u)) % pw) + pw) % pw);
+                        units.push_back(((uint32_t)row * (uint32_t)pw + (uint32_t)col) * 4u);
+                    }
+                }
+            for (int Y = Y0; Y < Y1; Y++)
+                for (int X = X0; X < X1; X++) {
+                    const long long i = (long long)Y * g.w + X;
+                    const uint32_t m = wxy[i];
+                    const int x0 = (int)(m & 0xFFFFu), y0 = (int)(m >> 16);
+                    if (P.wide) {  // k_warp_local's global form: index | x1 != x0 | y1 != y0
+                        loc[i] = (uint32_t)(y0 * pw + x0) | (x0 < pw - 1 ? 1u << 31 : 0u) |
+                                 (y0 < ph - 1 ? 1u << 30 : 0u);
+                    } else {
+                        const int r = y0 - vmin;
+                        const long long xf = rx + wrap_du_h(x0 - rx, pw);  // unwrapped column
+                        const uint32_t lt = (uint32_t)(4LL * (off[r] - q0[r]) + xf);
+                        const uint32_t lb = (uint32_t)(4LL * (off[r + 1] - q0[r + 1]) + xf);
+                        loc[i] = lt | lb << 16;
+                    }
+                }
+            patches.push_back(P);
+        }
 }
 
 // The RGB warp's texel taps (row f4 / a18): the GL camera ray of pixel centre (i, r)
@@ -372,27 +463,33 @@ struct WarpLanes {  // one thread's kLPx pixels, all panorama-invariant
 // are consecutive in one tile row: one 16-B store per panorama when they are all inside.
 typedef uint32_t u4v __attribute__((ext_vector_type(4)));
 #if !PF_WARP_WAVEBOX  // the block form (default)
-template <int NS, bool RESP, bool V4>
+template <int NS, bool RESP, bool V4, bool RAG = false>
 __device__ __forceinline__ void warp_staged(float* box, float* xbuf, const RespK* rk,
                                             const WarpPatch& P,
                                             int t, const WarpLanes& W,
                                             const float* __restrict__ pano, int pw, int ph,
                                             long long pstride, float* __restrict__ tiles,
-                                            long long tstride, int bbeg, int nb)
+                                            long long tstride, int bbeg, int nb,
+                                            const uint32_t* __restrict__ unit_tbl = nullptr)
 {
+    static_assert(!RAG || (V4 && PF_WARP_SPLIT), "ragged footprints: 16-B units, split parities");
     constexpr int U = V4 ? 4 : 1;  // floats per staging unit
-    const int bw2 = 2 * P.bw, bwu = P.bw / U, units = bwu * P.bh;
+    const int bw2 = 2 * P.bw, bwu = RAG ? 1 : P.bw / U, units = RAG ? P.units : bwu * P.bh;
     uint32_t goff[NS];  // unit e = t + 256*s of the box -> panorama byte offset
 #pragma unroll
     for (int s = 0; s < NS; s++) {
         int e = t + s * kWB;
         e = e < units ? e : units - 1;
-        const int r = e / bwu, c = (e - r * bwu) * U;
-        int row = P.gy0 + r;
-        row = row < ph ? row : ph - 1;
-        int col = P.gx0 + c;
-        col = col < pw ? col : col - pw;
-        goff[s] = (uint32_t)(row * pw + col) * 4u;
+        if constexpr (RAG) {
+            goff[s] = unit_tbl[P.uoff + e];
+        } else {
+            const int r = e / bwu, c = (e - r * bwu) * U;
+            int row = P.gy0 + r;
+            row = row < ph ? row : ph - 1;
+            int col = P.gx0 + c;
+            col = col < pw ? col : col - pw;
+            goff[s] = (uint32_t)(row * pw + col) * 4u;
+        }
     }
     constexpr int D = PF_WARP_PFD;  // prefetch depth: panorama j is staged in stg[j % D]
     float stg[D][NS][U];
@@ -441,8 +538,11 @@ __device__ __forceinline__ void warp_staged(float* box, float* xbuf, const RespK
             f2 v;
 #pragma unroll
             for (int j = 0; j < 2; j++) {
-                const float* c = L + W.la[k + j];
-                if constexpr (PF_WARP_SPLIT)
+                const float* c = L + (RAG ? (W.la[k + j] & 0xFFFFu) : W.la[k + j]);
+                if constexpr (RAG) {  // the bottom pair sits on its own packed row
+                    const float* c2 = L + (W.la[k + j] >> 16);
+                    v[j] = bilinear(f2{c[0], c[1]}, f2{c2[0], c2[1]}, W.wx[k + j], W.wy[k + j]);
+                } else if constexpr (PF_WARP_SPLIT)
                     v[j] = bilinear(f2{c[0], c[1]}, f2{c[P.bw], c[P.bw + 1]}, W.wx[k + j],
                                     W.wy[k + j]);
                 else
@@ -509,18 +609,19 @@ __device__ __forceinline__ void warp_staged(float* box, float* xbuf, const RespK
     }
 }
 
-template <int NS, bool V4>
+template <int NS, bool V4, bool RAG = false>
 __device__ __forceinline__ void warp_staged_sel(bool resp, float* box, float* xbuf,
                                                 const RespK* rk,
                                                 const WarpPatch& P, int t, const WarpLanes& W,
                                                 const float* pano, int pw, int ph,
                                                 long long pstride, float* tiles,
-                                                long long tstride, int bbeg, int nb)
+                                                long long tstride, int bbeg, int nb,
+                                                const uint32_t* unit_tbl = nullptr)
 {
-    if (resp) warp_staged<NS, true, V4>(box, xbuf, rk, P, t, W, pano, pw, ph, pstride, tiles, tstride,
-                                        bbeg, nb);
-    else warp_staged<NS, false, V4>(box, xbuf, rk, P, t, W, pano, pw, ph, pstride, tiles, tstride,
-                                    bbeg, nb);
+    if (resp) warp_staged<NS, true, V4, RAG>(box, xbuf, rk, P, t, W, pano, pw, ph, pstride, tiles,
+                                             tstride, bbeg, nb, unit_tbl);
+    else warp_staged<NS, false, V4, RAG>(box, xbuf, rk, P, t, W, pano, pw, ph, pstride, tiles,
+                                         tstride, bbeg, nb, unit_tbl);
 }
 
 #ifndef PF_WARP_WPE
@@ -530,6 +631,7 @@ __global__ void __launch_bounds__(kWB) __attribute__((amdgpu_waves_per_eu(PF_WAR
 k_warp_depth(const TileGeom* __restrict__ geom,
                                                     int ntiles,
                                                     const WarpPatch* __restrict__ patches,
+                                                    const uint32_t* __restrict__ unit_tbl,
                                                     int npatch, const uint32_t* __restrict__ wloc,
                                                     const float2* __restrict__ wfxy,
                                                     const float* __restrict__ pano, int pw,
@@ -617,7 +719,15 @@ k_warp_depth(const TileGeom* __restrict__ geom,
     __shared__ RespK rk[kNB];  // published by the first barrier inside warp_staged
     if (t < nb) rk[t] = resp_key(resp, bbeg + t, ntiles, P.tile);
     const bool rs = resp != nullptr;
-    if (PF_WARP_V4 && (pw & 3) == 0) {  // quad-aligned boxes (k_patch_box): 16-B staging loads
+    if (PF_WARP_V4 && PF_WARP_SPLIT && P.units > 0) {  // ragged footprint (warp_patches_host)
+        const int nq = (P.units + kWB - 1) / kWB;  // uniform: 16-B loads per thread
+        if (nq <= 1) warp_staged_sel<1, true, true>(rs, box, xbuf, rk, P, t, W, pano, pw, ph, pstride,
+                                                    tiles, tstride, bbeg, nb, unit_tbl);
+        else if (nq <= 2) warp_staged_sel<2, true, true>(rs, box, xbuf, rk, P, t, W, pano, pw, ph,
+                                                         pstride, tiles, tstride, bbeg, nb, unit_tbl);
+        else warp_staged_sel<kSlots / 4, true, true>(rs, box, xbuf, rk, P, t, W, pano, pw, ph,
+                                                     pstride, tiles, tstride, bbeg, nb, unit_tbl);
+    } else if (PF_WARP_V4 && (pw & 3) == 0) {  // quad-aligned boxes (k_patch_box): 16-B staging loads
         const int nq = (P.bw * P.bh / 4 + kWB - 1) / kWB;  // uniform: loads per thread
         if (nq <= 1) warp_staged_sel<1, true>(rs, box, xbuf, rk, P, t, W, pano, pw, ph, pstride, tiles,
                                               tstride, bbeg, nb);
@@ -859,6 +969,7 @@ int warp_patch_edge() { return kPatch; }
 int warp_patch_height() { return kPatchH; }
 
 void launch_warp_depth(hipStream_t s, const TileGeom* geom, int ntiles, const WarpPatch* patches,
+                       const uint32_t* unit_tbl,
                        int npatch, const uint32_t* wloc, const float* wfxy, const float* pano,
                        int pw, int ph, long long pstride, const Resp* resp, float* tiles,
                        long long tstride, int batch)
@@ -871,8 +982,8 @@ void launch_warp_depth(hipStream_t s, const TileGeom* geom, int ntiles, const Wa
 #else
     const long long n = (long long)npatch * ((batch + kNB - 1) / kNB);
     hipLaunchKernelGGL(k_warp_depth, dim3((unsigned)n), dim3(kWB), 0, s, geom, ntiles, patches,
-                       npatch, wloc, (const float2*)wfxy, pano, pw, ph, pstride, resp, tiles,
-                       tstride, batch);
+                       unit_tbl, npatch, wloc, (const float2*)wfxy, pano, pw, ph, pstride, resp,
+                       tiles, tstride, batch);
 #endif
 }
 
@@ -1042,7 +1153,8 @@ __global__ void __launch_bounds__(256) k_warp_rgb_box(const TileGeom* __restrict
                                                       uint8_t* __restrict__ tiles,
                                                       long long tstride, int batch)
 {
-    __shared__ float box[2 * kRgbCap];
+    // two parities of kRgbCap bytes (+ one dword: a pixel's last 3-dword read may pass the end)
+    __shared__ uint32_t boxw[2 * (kRgbCap / 4) + 4];
     const unsigned lb = xcd_remap(blockIdx.x, gridDim.x);
     const int pid = (int)(lb % (unsigned)npatch);
     const int chunk = (int)(lb / (unsigned)npatch);
@@ -1125,35 +1237,51 @@ __global__ void __launch_bounds__(256) k_warp_rgb_box(const TileGeom* __restrict
         return;
     }
 
-    // staging: thread t owns unit t of the patch's footprint (units past it reload its first
-    // unit, so every load is issued unconditionally)
-    const uint32_t goff = unit_tbl[(long long)pid * kRgbUnits + (t < P.units ? t : 0)];
-    u4v stg[2];
+    // staging: thread t owns units t and t + 256 of the patch's footprint (units past it reload
+    // its first unit, so every load is issued unconditionally).  LDS holds the u8 rows as they
+    // are (one 16-B store per unit, consecutive lanes on consecutive 16 B: no bank conflicts);
+    // a pixel's corner pair is the 6 bytes at its byte offset a, read as the 3 dwords from
+    // a & ~3 and aligned with v_alignbyte (round 5: the fp32-widened box of the first version
+    // spent 70 % of its LDS cycles in bank conflicts, SQ_LDS_BANK_CONFLICT, profiles/r05/rgb)
+    constexpr int NU = kRgbUnits / 256;
+    uint32_t goff[NU];
+#pragma unroll
+    for (int u = 0; u < NU; u++) {
+        const int e = t + 256 * u;
+        goff[u] = unit_tbl[(long long)pid * kRgbUnits + (e < P.units ? e : 0)];
+    }
+    u4v stg[2][NU];
     auto fetch = [&](int sl, int q) {
         const auto pr = rsrc(pano + (long long)(bbeg + (q < nb ? q : nb - 1)) * pstride, pbytes);
-        stg[sl] = __builtin_amdgcn_raw_buffer_load_b128(pr, (int)goff, 0, 0);
-    };
-    auto put = [&](int pa, const u4v v) {
-        float4* d = reinterpret_cast<float4*>(box + pa * kRgbCap + 16 * t);
 #pragma unroll
-        for (int m = 0; m < 4; m++) {
-            const uint32_t w = v[m];
-            d[m] = make_float4((float)(w & 0xFFu), (float)((w >> 8) & 0xFFu),
-                               (float)((w >> 16) & 0xFFu), (float)(w >> 24));
-        }
+        for (int u = 0; u < NU; u++)
+            stg[sl][u] = __builtin_amdgcn_raw_buffer_load_b128(pr, (int)goff[u], 0, 0);
+    };
+    auto put = [&](int pa, const u4v* v) {
+#pragma unroll
+        for (int u = 0; u < NU; u++)
+            *reinterpret_cast<u4v*>(boxw + pa * (kRgbCap / 4) + 4 * (t + 256 * u)) = v[u];
+    };
+    // the 6 bytes R0 G0 B0 R1 G1 B1 at byte offset a of parity L, as floats into c[0..5]
+    auto pair6 = [&](const uint32_t* L, uint32_t a, float* c) {
+        const uint32_t* w = L + (a >> 2);
+        const uint32_t w0 = w[0], w1 = w[1], w2 = w[2], sh = a & 3u;
+        const uint32_t lo = __builtin_amdgcn_alignbyte(w1, w0, sh);  // bytes a .. a+3
+        const uint32_t hi = __builtin_amdgcn_alignbyte(w2, w1, sh);  // bytes a+4 .. a+7
+        c[0] = (float)(lo & 0xFFu);
+        c[1] = (float)((lo >> 8) & 0xFFu);
+        c[2] = (float)((lo >> 16) & 0xFFu);
+        c[3] = (float)(lo >> 24);
+        c[4] = (float)(hi & 0xFFu);
+        c[5] = (float)((hi >> 8) & 0xFFu);
     };
     auto iter = [&](auto parity, int q) {
         constexpr int PA = decltype(parity)::value;
         fetch(PA, q + 2);  // stg[PA] held panorama q, put into parity PA last iteration
-        const float* L = box + PA * kRgbCap;
+        const uint32_t* L = boxw + PA * (kRgbCap / 4);
         blend_store([&](int k, float* c) {
-            const float* st = L + (la[k] & 0xFFFFu);
-            const float* sb = L + (la[k] >> 16);
-#pragma unroll
-            for (int j = 0; j < 6; j++) {
-                c[j] = st[j];
-                c[6 + j] = sb[j];
-            }
+            pair6(L, la[k] & 0xFFFFu, c);
+            pair6(L, la[k] >> 16, c + 6);
         }, tiles + (long long)(bbeg + q) * tstride);
         put(1 - PA, stg[1 - PA]);  // panorama q+1 (a duplicate past the chunk: unread)
         __syncthreads();

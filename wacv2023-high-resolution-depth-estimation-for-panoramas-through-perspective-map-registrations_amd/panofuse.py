@@ -13,7 +13,7 @@ import os
 import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-# PANOFUSE_LIB selects another build of the same library (A/B tuning runs, tools/variants.sh)
+# PANOFUSE_LIB selects another build of the same library (A/B tuning runs, tools/gpu_round.sh (ab step))
 LIB_PATH = os.environ.get("PANOFUSE_LIB") or os.path.join(HERE, "lib", "libpanofuse.so")
 
 PF_OK, PF_EINVAL, PF_ENOMEM, PF_EHIP, PF_ESTATE, PF_EDEGENERATE = 0, -1, -2, -3, -4, -5
