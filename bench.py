@@ -47,6 +47,10 @@ def parse():
                     help="c5 mode: rows = tiles AND sweep row bands sharded over the ranks "
                          "(pf_dist.fuse_row_sharded, halo exchange per pass); tiles = tiles "
                          "sharded, every sweep on rank 0 (pf_dist.fuse_tile_sharded)")
+    ap.add_argument("--c5-rep", type=int, default=-1,
+                    help="c5 rows mode: the coarsest levels replicated on every rank instead of "
+                         "row-sharded (pf_dist.fuse_row_sharded rep_levels); -1 = auto "
+                         "(pf_dist.auto_rep_levels)")
     ap.add_argument("--mode", choices=("batch", "c5"), default="batch",
                     help="batch: configs C3/C4 (the headline metric); c5: one 8192x4096 "
                          "panorama, tiles sharded over the ranks")
@@ -215,6 +219,8 @@ def c5_measure(args, rank, world, local, dev, steps, warmup):
     nlevels = panofuse.level_info(out_w, out_w // 2, zr, 0)[5]
 
     logs = []
+    be0 = pf_dist.HipRowShardBackend(fz, emap, tiles, coeffs, out_w, zr, out.view(-1))
+    rep = args.c5_rep if args.c5_rep >= 0 else pf_dist.auto_rep_levels(be0, nlevels, world)
 
     def step():
         if fs is not None:
@@ -222,10 +228,10 @@ def c5_measure(args, rank, world, local, dev, steps, warmup):
             fs.warp_depth(gt, mine, resp)
             fs.register(emap, mine, zr, degree=3, apply=False, coeffs=coeffs[t0:t1][None])
         comm = pf_dist.TorchComm(dist, stage_host=args.backend == "gloo") if world > 1 else None
-        if args.c5_shard == "rows":
-            be = pf_dist.HipRowShardBackend(fz, emap, tiles, coeffs, out_w, zr, out.view(-1))
+        if args.c5_shard == "rows":  # be0 keeps the per-level geometry across panoramas
             logs.append(pf_dist.ExchangeLog())
-            pf_dist.fuse_row_sharded(be, nlevels, lay.ntiles, rank, world, comm, logs[-1])
+            pf_dist.fuse_row_sharded(be0, nlevels, lay.ntiles, rank, world, comm, logs[-1],
+                                     rep_levels=rep)
         else:
             be = pf_dist.HipTileShardBackend(fz, emap, tiles, coeffs, out_w, zr, out)
             pf_dist.fuse_tile_sharded(be, nlevels, lay.ntiles, rank, world, comm)
@@ -281,20 +287,8 @@ def c5_measure(args, rank, world, local, dev, steps, warmup):
         one_call = sorted(ts_)[len(ts_) // 2]
     model8 = None
     if world == 1 and args.c5_shard == "rows":
-        # the bytes each of 8 ranks would send per panorama, from the same
-        # row arithmetic as the flow (pf_dist.exchange_model) with this GPU's band plans
-        be = pf_dist.HipRowShardBackend(fz, emap, tiles, coeffs, out_w, zr, out.view(-1))
-        dims = [be.dims(lv) for lv in range(nlevels)]
-        plans = [be.plan(lv, 8) for lv in range(nlevels)]
-        ext = [[be.tile_rows(lv, *pf_dist.shard_range(lay.ntiles, r, 8)) for r in range(8)]
-               for lv in range(nlevels)]
-        mc = [be.multicover_count(lv) for lv in range(nlevels)]
-        per = pf_dist.exchange_model(dims, plans, ext, 8, mc)
-        tot = [sum(d.values()) for d in per]
-        model8 = {"plans": plans, "per_rank": per, "max_rank_bytes": max(tot),
-                  "total_bytes": sum(tot),
-                  "bounds": [pf_dist.band_bounds(d[2], d[3], 8, e, max(p) + 1)
-                             for d, e, p in zip(dims, ext, plans)]}
+        model8 = c5_rehearsal(fz, lay, gt, emap, resp_all, coeffs, tiles, out, out_w, zr,
+                              nlevels, dev, local)
     nz = int((out != 0).sum().item())
     sent = logs[-1].sent if logs else None  # this rank's bytes of the last step, by kind
     if world > 1 and sent is not None:
@@ -303,7 +297,87 @@ def c5_measure(args, rank, world, local, dev, steps, warmup):
         sent = per
     return {"value": steps / elapsed, "elapsed": elapsed, "mine_s": mine_s,
             "bit_exact": bit_exact, "nonzero_px": nz, "one_call_ms": one_call,
-            "bytes_sent_per_rank": sent, "model_8_ranks": model8}
+            "bytes_sent_per_rank": sent, "model_8_ranks": model8, "rep_levels": rep}
+
+
+# C5 over 8 GPUs, predicted from one GPU.  The exchanges themselves
+# cannot run here (one GPU: RCCL refuses two ranks on a device), so they enter as a stated model:
+# an exchange round costs XCHG_LAT_US of latency on the critical path (RCCL point-to-point over
+# xGMI, small messages) plus its bytes at XCHG_GBS (one xGMI link, ~153 GB/s peak, taken at a
+# third).  Each rank's compute is measured: the sharded flow of rank r of 8 run alone on this GPU
+# with a communicator that moves nothing (pf_dist.NullComm), its own tiles warped and registered
+# first (hipEvents).  Predicted = max over ranks (compute) + rounds x latency + max bytes / rate.
+XCHG_LAT_US = 20.0
+XCHG_GBS = 50.0
+
+
+def c5_rehearsal(fz, lay, gt, emap, resp_all, coeffs, tiles, out, out_w, zr, nlevels, dev,
+                 local, world=8):
+    import torch
+
+    import panofuse
+    import pf_dist
+    import pf_layouts as PL
+    be = pf_dist.HipRowShardBackend(fz, emap, tiles, coeffs, out_w, zr, out.view(-1))
+    dims = [be.dims(lv) for lv in range(nlevels)]
+    ext = [[be.tile_rows(lv, *pf_dist.shard_range(lay.ntiles, r, world)) for r in range(world)]
+           for lv in range(nlevels)]
+    mc = [be.multicover_count(lv) for lv in range(nlevels)]
+    subs = []
+    for r in range(world):  # each rank's tile context, maps built before the timing
+        a, b = pf_dist.shard_range(lay.ntiles, r, world)
+        f = panofuse.Fuser(local)
+        f.set_tiles(PL.Layout(f"C5[{a}:{b}]", lay.fovs[a:b], lay.ranges[a:b], lay.tile_w[a:b],
+                              lay.tile_h[a:b]))
+        off = int(sum(int(lay.tile_w[i]) * int(lay.tile_h[i]) for i in range(a)))
+        subs.append((f, a, b, off, panofuse.make_responses(resp_all[a:b], dev)))
+    res = {}
+    for rep in range(nlevels):
+        plans = [be.plan(lv, 1 if lv < rep else world) for lv in range(nlevels)]
+        try:
+            per = pf_dist.exchange_model(dims, plans, ext, world, mc, rep_levels=rep)
+        except ValueError:
+            continue
+        times, rounds = [], 0
+        for r, (f, a, b, off, resp) in enumerate(subs):
+            mine = tiles[:, off:off + f.tile_elems]
+            log = pf_dist.ExchangeLog()
+            ts = []
+            for it in range(3):
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record()
+                f.warp_depth(gt, mine, resp)
+                f.register(emap, mine, zr, degree=3, apply=False, coeffs=coeffs[a:b][None])
+                log = pf_dist.ExchangeLog()
+                try:
+                    pf_dist.fuse_row_sharded(be, nlevels, lay.ntiles, r, world,
+                                             pf_dist.NullComm(), log, rep_levels=rep)
+                except ValueError:
+                    ts = None
+                    break
+                e1.record()
+                torch.cuda.synchronize()
+                if it:
+                    ts.append(e0.elapsed_time(e1))
+            if ts is None:
+                times = None
+                break
+            times.append(min(ts))
+            rounds = max(rounds, log.rounds)
+        if times is None:
+            continue
+        tot = [sum(d.values()) for d in per]
+        pred = max(times) + rounds * XCHG_LAT_US * 1e-3 + max(tot) / (XCHG_GBS * 1e9) * 1e3
+        res[f"rep{rep}"] = {"rep_levels": rep, "plans": plans, "compute_ms_per_rank": times,
+                            "rounds": rounds, "bytes_per_rank": per, "max_rank_bytes": max(tot),
+                            "total_bytes": sum(tot), "predicted_ms": pred}
+    for f, *_ in subs:
+        f.close()
+    best = min(res.values(), key=lambda d: d["predicted_ms"]) if res else None
+    return {"world": world, "assumed_round_latency_us": XCHG_LAT_US,
+            "assumed_link_GBps": XCHG_GBS, "by_rep_levels": res,
+            "best": best and {k: best[k] for k in ("rep_levels", "predicted_ms",
+                                                   "max_rank_bytes", "total_bytes", "rounds")}}
 
 
 def run_c5(args, rank, world, local, dev):
@@ -332,6 +406,7 @@ def run_c5(args, rank, world, local, dev):
             "bytes_sent_per_rank": r["bytes_sent_per_rank"],
             "model_8_ranks": r["model_8_ranks"],
             "one_call_ms": r["one_call_ms"],
+            "rep_levels": r["rep_levels"],
             "backend": args.backend if world > 1 else None,
             "elapsed_rank0_s": mine_s}), flush=True)
     if world > 1:

@@ -152,6 +152,24 @@ class OracleRowBackend(OracleBackend):
     def scratch(self, n):
         return torch.zeros(n, dtype=torch.float32)
 
+    def seed(self, level, prev):  # a replicated level (flat torch planes, as the GPU backend)
+        lv = self._lv(level)
+        if level == 0:
+            base = self.O.seed_level0(self.emap, lv)
+        else:
+            plv = self._lv(level - 1)
+            base = self.O.upsample(prev.numpy().reshape(plv.h, plv.w), lv)
+        return torch.from_numpy(np.ascontiguousarray(base).ravel().copy())
+
+    def finish(self, level, lsum, cnt, buf, last):
+        lv = self._lv(level)
+        Ln = self.O.normalize(lsum.numpy().reshape(lv.h, lv.w),
+                              cnt.numpy().astype(np.int32).reshape(lv.h, lv.w), lv)
+        res = self.O.jacobi(buf.numpy().reshape(lv.h, lv.w), Ln, lv, lv.iters)
+        if last:
+            self.out.copy_(torch.from_numpy(self.O.quantize(res).view(np.int16).ravel()))
+        return torch.from_numpy(np.ascontiguousarray(res).ravel().copy())
+
     def _subset(self, level, t0, t1):
         key = (level, t0, t1)
         if not hasattr(self, "_sub"):
@@ -227,7 +245,7 @@ class OracleRowBackend(OracleBackend):
             dst[sl] = torch.from_numpy(res[sl].copy())
 
 
-def _row_worker(rank, world, port, q):
+def _row_worker(rank, world, port, q, rep=0):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
@@ -242,13 +260,14 @@ def _row_worker(rank, world, port, q):
         data = np.random.RandomState(9).rand(total).astype(np.float32)
         be = OracleRowBackend(O, PL, 512, emap, tiles, data)
         log = pf_dist.ExchangeLog()
-        pf_dist.fuse_row_sharded(be, 3, lay.ntiles, rank, world, pf_dist.TorchComm(dist), log)
+        pf_dist.fuse_row_sharded(be, 3, lay.ntiles, rank, world, pf_dist.TorchComm(dist), log,
+                                 rep_levels=rep)
         # the bytes this rank sent are those of the exchange model
         dims = [be.dims(lv) for lv in range(3)]
-        plans = [be.plan(lv, world) for lv in range(3)]
+        plans = [be.plan(lv, 1 if lv < rep else world) for lv in range(3)]
         ext = [[be.tile_rows(lv, *pf_dist.shard_range(lay.ntiles, r, world))
                 for r in range(world)] for lv in range(3)]
-        model = pf_dist.exchange_model(dims, plans, ext, world)[rank]
+        model = pf_dist.exchange_model(dims, plans, ext, world, rep_levels=rep)[rank]
         same = all(model.get(k, 0) == v for k, v in log.sent.items()) and \
             all(log.sent.get(k, 0) == v for k, v in model.items())
         ok = True
@@ -260,14 +279,17 @@ def _row_worker(rank, world, port, q):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world", [2, 3])
-def test_row_sharded_fusion_gloo(world):
-    """tiles and rows sharded, halo rows exchanged between passes -- every
-    rank ends with the u16 panorama of the unsharded oracle fusion, bit for bit."""
+@pytest.mark.parametrize("world,rep", [(2, 0), (3, 1), (2, 3)])
+def test_row_sharded_fusion_gloo(world, rep):
+    """tiles and rows sharded, halo rows exchanged between passes; rank 0 ends
+    with the u16 panorama of the unsharded oracle fusion, bit for bit.  rep = the coarse levels
+    replicated on every rank instead (an all-gather of the partial target rows, no pass halos):
+    none, the first, all three."""
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_row_worker, args=(r, world, port, q)) for r in range(world)]
+    procs = [ctx.Process(target=_row_worker, args=(r, world, port, q, rep))
+             for r in range(world)]
     for p in procs:
         p.start()
     for p in procs:
@@ -280,6 +302,6 @@ def test_row_sharded_fusion_gloo(world):
     # plus the shared boundary row (K + 1 <= 12 rows of <= 512 floats, 3 levels), far below a
     # full plane.  (World 3 deals 2 tiles per rank across the bands: the bands fall back to an
     # even split and more rows travel -- still exactly the model's bytes.)
-    if world == 2:
+    if world == 2 and rep == 0:
         for _, _, sent, _ in res:
             assert 0 < sent.get("targets", 0) <= 3 * 12 * 512 * 4, sent

@@ -73,7 +73,7 @@ class ThreadComm:
         return RankComm()
 
 
-def _run(cfg, world, seed, flow="rows"):
+def _run(cfg, world, seed, flow="rows", rep=0):
     lay = PL.config_layout(cfg)
     out_w, ew = PL.CONFIGS["C5" if cfg == "C5" else "C2"]
     seeds = pf_synth.seeds_for(1, seed)
@@ -99,7 +99,8 @@ def _run(cfg, world, seed, flow="rows"):
             out = torch.zeros(out_w * (out_w // 2), dtype=torch.int16, device=DEV)
             if flow == "rows":
                 be = pf_dist.HipRowShardBackend(f, emap, tiles, coeffs[0], out_w, ZR, out)
-                pf_dist.fuse_row_sharded(be, be.nlevels, lay.ntiles, r, world, comm.rank(r))
+                pf_dist.fuse_row_sharded(be, be.nlevels, lay.ntiles, r, world, comm.rank(r),
+                                         rep_levels=rep)
             else:  # tiles only: rank 0 sweeps
                 be = pf_dist.HipTileShardBackend(f, emap, tiles, coeffs[0], out_w, ZR,
                                                  out.view(out_w // 2, out_w))
@@ -132,6 +133,13 @@ def test_row_sharded_c2_equals_fuse(world):
 
 def test_row_sharded_c5_equals_fuse():
     _run("C5", 4, 20261015 + 12)
+
+
+def test_row_sharded_c5_eight_ranks_coarse_levels_replicated():
+    """C5's 8-rank shape with the 1024- and 2048-wide levels replicated on every rank (the
+    all-gather of partial target rows) and the two finer levels row-sharded: rank 0's u16 ==
+    the one-GPU fusion (8 threads on one GPU)."""
+    _run("C5", 8, 20261015 + 14, rep=2)
 
 
 def test_tile_sharded_c5_threads_equals_fuse():

@@ -245,18 +245,42 @@ def prev_rows_needed(bounds, h0, h1, K, hp, rank):
 
 
 class ExchangeLog:
-    """Bytes each rank moves, per kind of exchange (DESIGN.md section 6's model is checked
-    against it in tests/test_dist.py)."""
+    """Bytes each rank sends per kind of exchange (DESIGN.md section 6's model is checked
+    against it in tests/test_dist.py), and the number of exchange rounds (each a latency on the
+    critical path)."""
 
     def __init__(self):
         self.sent = {}
+        self.rounds = 0
 
     def add(self, kind, nbytes):
         self.sent[kind] = self.sent.get(kind, 0) + int(nbytes)
+        self.rounds += 1
 
 
-def fuse_row_sharded(backend, nlevels, ntiles, rank, world, comm=None, log=None):
+class NullComm:
+    """A communicator that moves nothing: every rank's COMPUTE of the sharded flow can be run
+    alone on one GPU (bench.py's 8-rank rehearsal times each rank's kernels this way; the values
+    are not the sharded result)."""
+
+    def exchange(self, sends, recvs):
+        pass
+
+    def all_reduce_sum(self, t):
+        pass
+
+    def agree(self, values, src=0, device=None):
+        return list(values)
+
+
+def fuse_row_sharded(backend, nlevels, ntiles, rank, world, comm=None, log=None, rep_levels=0):
     """One panorama's fusion with tiles AND rows sharded over `world` ranks.
+
+    rep_levels: the first (coarsest) rep_levels levels are REPLICATED instead of row-sharded:
+    every rank receives every other rank's partial target rows (an all-gather of the tile rows)
+    and sweeps the whole level itself, with no halo exchange per pass; the next level then has
+    every previous row locally.  Worth it where a rank's band is thin against the halo (many
+    short passes, each an exchange on the critical path): C5's 1024-wide level at 8 ranks.
 
     backend (one rank's device):
       dims(level) -> (w, h, h0, h1)
@@ -278,25 +302,46 @@ def fuse_row_sharded(backend, nlevels, ntiles, rank, world, comm=None, log=None)
     Returns the bounds of the last level's bands."""
     t0, t1 = shard_range(ntiles, rank, world)
     prev, pbounds, bounds = None, None, None
+    # the per-level geometry is a function of the layout and the plans only: computed (and the
+    # plan agreed) once per backend, then reused by every panorama
+    geo = getattr(backend, "_row_geo", None)
+    if geo is None:
+        geo = {}
+        try:
+            backend._row_geo = geo
+        except AttributeError:
+            pass
     for level in range(nlevels):
         last = level == nlevels - 1
+        rep = world > 1 and level < rep_levels
         w, h, h0, h1 = backend.dims(level)
-        plan = backend.plan(level, world)
-        if world > 1 and hasattr(comm, "agree"):
-            # one plan for all ranks: rank 0's (the plan depends on per-process state -- CU
-            # count, occupancy, PF_J* overrides -- and mismatched passes would hang the exchanges)
-            plan = comm.agree(plan, 0, getattr(backend, "device", None))
-        K = max(plan) + 1
-        ext = [backend.tile_rows(level, *shard_range(ntiles, r, world)) for r in range(world)]
-        bounds = band_bounds(h0, h1, world, ext, K)
-        if world > 1 and min(bounds[r + 1] - bounds[r] for r in range(world)) < K:
-            raise ValueError(f"level {level}: {h1 - h0 + 1} band rows over {world} ranks leave "
-                             f"bands thinner than the {K}-row halo")
-        r0, r1 = bounds[rank], bounds[rank + 1]
-        need = [(max(h0, bounds[d] - K), min(h1 + 1, bounds[d + 1] + K)) for d in range(world)]
+        key = (level, world, rep, ntiles)
+        if key not in geo:
+            plan = backend.plan(level, 1 if rep else world)
+            if world > 1 and hasattr(comm, "agree"):
+                # one plan for all ranks: rank 0's (the plan depends on per-process state -- CU
+                # count, occupancy, PF_J* overrides -- and mismatched passes would hang the
+                # exchanges)
+                plan = comm.agree(plan, 0, getattr(backend, "device", None))
+            K = max(plan) + 1
+            ext = [backend.tile_rows(level, *shard_range(ntiles, r, world)) for r in range(world)]
+            if rep:
+                bnd = [h0] + [h1 + 1] * world  # rank 0's band is the level; all sweep it
+                need = [(h0, h1 + 1)] * world
+            else:
+                bnd = band_bounds(h0, h1, world, ext, K)
+                if world > 1 and min(bnd[r + 1] - bnd[r] for r in range(world)) < K:
+                    raise ValueError(f"level {level}: {h1 - h0 + 1} band rows over {world} ranks "
+                                     f"leave bands thinner than the {K}-row halo")
+                need = [(max(h0, bnd[d] - K), min(h1 + 1, bnd[d + 1] + K))
+                        for d in range(world)]
+            geo[key] = (plan, K, ext, bnd, need)
+        plan, K, ext, bounds, need = geo[key]
+        r0, r1 = (h0, h1 + 1) if rep else (bounds[rank], bounds[rank + 1])
         e0, e1 = need[rank]
         # the previous level's rows this rank's first pass / border read, from their owners
-        if level > 0 and world > 1:
+        # (after a replicated level every rank holds all of them)
+        if level > 0 and world > 1 and pbounds is not None:
             hp = backend.dims(level - 1)[1]
             wp = backend.dims(level - 1)[0]
             sends, recvs = [], []
@@ -318,7 +363,7 @@ def fuse_row_sharded(backend, nlevels, ntiles, rank, world, comm=None, log=None)
         lsum, cnt, lnorm = backend.plane(level), backend.plane(level), backend.plane(level)
         mlo, mhi = ext[rank][0], ext[rank][1] + 1
         lo, hi = (min(e0, mlo), max(e1, mhi)) if mlo < mhi else (e0, e1)
-        backend.partial_rows(level, t0, t1, lo, hi, lsum, cnt)
+        backend.partial_rows(level, t0, t1, lo, hi, lsum, cnt)  # rep: lo, hi = the whole band
         if world > 1:
             backend.coverage_rows(level, e0, e1, cnt)  # every tile's count: layout-only
             sends, recvs, bufs = [], [], []
@@ -345,6 +390,11 @@ def fuse_row_sharded(backend, nlevels, ntiles, rank, world, comm=None, log=None)
                 if log:
                     log.add("multicover", 4 * contrib.numel())
                 backend.multicover_patch(level, contrib, lsum)
+        if rep:  # the whole level on this rank: the one-GPU level (seed, normalise, sweeps)
+            buf = backend.seed(level, prev)
+            prev = backend.finish(level, lsum, cnt, buf, last)
+            pbounds = None
+            continue
         backend.normalize_rows(level, lsum, cnt, e0, e1, lnorm)
         a, b = backend.plane(level), backend.plane(level)
         if rank == 0 or rank == world - 1:  # the rows above / below the band
@@ -370,8 +420,8 @@ def fuse_row_sharded(backend, nlevels, ntiles, rank, world, comm=None, log=None)
             backend.band_pass(level, lnorm, mode, src, dst, T, r0, r1, fin, prev)
             src, dst = dst, (b if dst is a else a)
         prev, pbounds = (None if last else src), bounds
-    # the u16 result: every rank's owned rows to rank 0
-    if world > 1:
+    # the u16 result: every rank's owned rows to rank 0 (a replicated last level: all local)
+    if world > 1 and pbounds is not None:
         import torch
         w, h = backend.dims(nlevels - 1)[:2]
 
@@ -388,7 +438,7 @@ def fuse_row_sharded(backend, nlevels, ntiles, rank, world, comm=None, log=None)
     return bounds
 
 
-def exchange_model(dims, plans, ext, world, multicover=None):
+def exchange_model(dims, plans, ext, world, multicover=None, rep_levels=0):
     """Bytes each rank SENDS per panorama in fuse_row_sharded, by kind -- the same row arithmetic
     as the flow, from the layout alone (tests/test_dist.py checks it against
     the bytes a gloo run logs).  dims[l] = (w, h, h0, h1); plans[l] = the pass depths of level l;
@@ -404,10 +454,19 @@ def exchange_model(dims, plans, ext, world, multicover=None):
     pb = None
     for lv, (w, h, h0, h1) in enumerate(dims):
         K = max(plans[lv]) + 1
+        if lv < rep_levels:  # replicated: every rank's tile rows to every other rank
+            for r in range(world):
+                lo, hi = ext[lv][r][0], ext[lv][r][1] + 1
+                if lo < hi:
+                    add(r, "targets", 4 * w * (hi - lo) * (world - 1))
+                if multicover and multicover[lv]:
+                    add(r, "multicover", 4 * multicover[lv])
+            pb = None
+            continue
         b = band_bounds(h0, h1, world, ext[lv], K)
         need = [(max(h0, b[d] - K), min(h1 + 1, b[d + 1] + K)) for d in range(world)]
         for r in range(world):
-            if lv > 0:
+            if lv > 0 and pb is not None:
                 wp, hp = dims[lv - 1][:2]
                 for d in range(world):
                     if d != r:
@@ -428,11 +487,29 @@ def exchange_model(dims, plans, ext, world, multicover=None):
                 if r < world - 1:
                     add(r, "pass_halo", 4 * w * (r1 - max(r1 - k, r0)))
         pb = b
+    if pb is None:  # a replicated last level: no gather
+        return res
     w, h = dims[-1][:2]
     for r in range(1, world):
         lo, hi = owned_rows(pb, h, r)
         add(r, "gather_u16", 2 * w * (hi - lo))
     return res
+
+
+def auto_rep_levels(backend, nlevels, world, ratio=10):
+    """The coarse levels worth replicating at `world` ranks: the leading levels whose band per
+    rank is under `ratio` halos deep (each of their many short passes would wait for an exchange)."""
+    if world <= 1:
+        return 0
+    n = 0
+    for lv in range(nlevels - 1):  # the finest level stays sharded
+        w, h, h0, h1 = backend.dims(lv)
+        K = max(backend.plan(lv, world)) + 1
+        if (h1 - h0 + 1) / world < ratio * K:
+            n = lv + 1
+        else:
+            break
+    return n
 
 
 class HipRowShardBackend:
@@ -484,6 +561,17 @@ class HipRowShardBackend:
 
     def normalize_rows(self, level, lsum, cnt, row0, row1, lnorm):
         self.fz.fuse_normalize_rows(lsum, cnt, self.out_w, self.zr, level, row0, row1, lnorm)
+
+    def seed(self, level, prev):  # a replicated level: the one-GPU path (fuse_tile_sharded's)
+        buf = self.plane(level)
+        self.fz.fuse_seed(self.emap if level == 0 else None, prev, self.out_w, self.zr, level,
+                          buf)
+        return buf
+
+    def finish(self, level, lsum, cnt, buf, last):
+        self.fz.fuse_finish_level(lsum, cnt, self.out_w, self.zr, level, buf,
+                                  self.out.view(self.levels[level][1], -1) if last else None)
+        return buf
 
     def plan(self, level, nbands):
         return self.fz.fuse_band_plan(self.out_w, self.zr, level, nbands)
