@@ -199,10 +199,9 @@ class OracleRowBackend(OracleBackend):
         lsum[sl] = torch.from_numpy(Ls[sl].copy())
         cnt[sl] = torch.from_numpy(n[sl].astype(np.float32))
 
-    def coverage_rows(self, level, row0, row1, cnt):
+    def coverage_plane(self, level):
         _, n = self._subset(level, 0, len(self.tiles))
-        sl = self._rows(level, row0, row1)
-        cnt[sl] = torch.from_numpy(n[sl].astype(np.float32))
+        return torch.from_numpy(n.astype(np.float32))
 
     def rows_add(self, dst, src):
         dst += src

@@ -2053,7 +2053,7 @@ int pf_fuse_tile_rows(pf_ctx* c, int out_w, int out_h, float zr0, float zr1, int
         return fail(c, PF_EINVAL, "tile range [%d,%d) outside [0,%d)", t0, t1, c->ntiles);
     const LevelDims& L = c->lc.dims[level];
     int lo = INT32_MAX, hi = INT32_MIN;
-    for (int p = t0; p < t1; p++) {  // rows where k_targets_map_partial can write a non-zero sum
+    for (int p = t0; p < t1; p++) {  // rows where k_targets_patch_partial can write a non-zero sum
         const TileBox& b = c->lc.box_h[level][p];
         const int a = std::max(std::min(b.y0, b.y1), L.h0 + 1);
         const int z = std::min(std::max(b.y0, b.y1), L.h1 - 1);
@@ -2113,7 +2113,15 @@ int pf_fuse_finish_level(pf_ctx* c, const float* lsum, const float* cnt, int out
     if ((rc = ensure(c, c->lsum_ws, sizeof(float) * st))) return rc;
     launch_normalize(c->stream, lsum, cnt, L, (float*)c->lnorm.p);
     float* other = (float*)c->lsum_ws.p;
-    HIPCHK(c, hipMemcpyAsync(other, buf, sizeof(float) * st, hipMemcpyDeviceToDevice, c->stream));
+    // every pass stores every band row [h0, h1] of the plane it writes (pf_jacobi.hip): the second
+    // plane takes the rows outside the band's interior (h0, h1), and the band comes back at the end
+    const size_t rowb = sizeof(float) * (size_t)L.w;
+    const int ia = std::max(L.h0 + 1, 0), ib = std::min(L.h1, L.h);  // interior rows [ia, ib)
+    const int ba = std::max(L.h0, 0), bb = std::min(L.h1 + 1, L.h);  // band rows [ba, bb)
+    HIPCHK(c, hipMemcpyAsync(other, buf, rowb * ia, hipMemcpyDeviceToDevice, c->stream));
+    if (ib < L.h)
+        HIPCHK(c, hipMemcpyAsync(other + (size_t)ib * L.w, buf + (size_t)ib * L.w,
+                                 rowb * (L.h - ib), hipMemcpyDeviceToDevice, c->stream));
     float* res = nullptr;
     if (jacobi_tcap(L) >= 1)
         res = run_jacobi(c, L, 0, nullptr, 0, 0, 0, 0, nullptr, nullptr, nullptr, 0,
@@ -2121,8 +2129,9 @@ int pf_fuse_finish_level(pf_ctx* c, const float* lsum, const float* cnt, int out
                          lc.full[level] ? (const float*)lc.hcol[level].p : nullptr);
     else
         launch_jacobi(c->stream, buf, other, (const float*)c->lnorm.p, st, L, L.iters, 1, &res);
-    if (res != buf)
-        HIPCHK(c, hipMemcpyAsync(buf, res, sizeof(float) * st, hipMemcpyDeviceToDevice, c->stream));
+    if (res != buf && bb > ba)
+        HIPCHK(c, hipMemcpyAsync(buf + (size_t)ba * L.w, res + (size_t)ba * L.w,
+                                 rowb * (bb - ba), hipMemcpyDeviceToDevice, c->stream));
     if (level == lc.nlevels - 1 && out) launch_quantize(c->stream, buf, st, (int)st, out, st, 1);
     HIPCHK(c, hipGetLastError());
     return PF_OK;

@@ -156,8 +156,8 @@ static constexpr int kTNB = PF_TGT_NB;                           // panoramas pe
 #define PF_TGT_NT 1
 #endif
 
-// One block's work: patch `pid` of level L for panoramas [bgrp*kTNB, +kTNB).
-template <bool XFORM>
+// One block's work: patch `pid` of level L for panoramas [bgrp*NB, +NB).
+template <bool XFORM, int NB>
 __device__ __forceinline__ void targets_patch(const TileGeom* __restrict__ geom,
                                               const TileBox* __restrict__ box,
                                               const TapBox* __restrict__ tb, int ntiles,
@@ -173,14 +173,14 @@ __device__ __forceinline__ void targets_patch(const TileGeom* __restrict__ geom,
     const int X0 = (pid % npx) * kTPW, Y0 = L.h0 + (pid / npx) * kTPH;
     const int t = threadIdx.x;
     const int X = X0 + (t & (kTPW - 1));
-    const int bbeg = bgrp * kTNB;
-    float acc[kTPP][kTNB];
+    const int bbeg = bgrp * NB;
+    float acc[kTPP][NB];
     int n[kTPP];
 #pragma unroll
     for (int j = 0; j < kTPP; j++) {
         n[j] = 0;
 #pragma unroll
-        for (int q = 0; q < kTNB; q++) acc[j][q] = 0.0f;
+        for (int q = 0; q < NB; q++) acc[j][q] = 0.0f;
     }
     const int X1 = min(X0 + kTPW - 1, L.w - 1), Y1 = min(Y0 + kTPH - 1, L.h1);
     // one tile's contribution to the patch (tiles come in index order: the reference's
@@ -189,10 +189,10 @@ __device__ __forceinline__ void targets_patch(const TileGeom* __restrict__ geom,
         const TileBox bx = box[p];
         const TapBox B = tb[p];
         const long long toff = geom[p].off;
-        float4 k[kTNB];
+        float4 k[NB];
         if constexpr (XFORM) {
 #pragma unroll
-            for (int q = 0; q < kTNB; q++) {
+            for (int q = 0; q < NB; q++) {
                 const int b = bbeg + q < batch ? bbeg + q : batch - 1;
                 k[q] = *reinterpret_cast<const float4*>(coeffs + ((long long)b * ntiles + p) * 4);
             }
@@ -202,15 +202,15 @@ __device__ __forceinline__ void targets_patch(const TileGeom* __restrict__ geom,
             const int gx = X0 - 1 + g % kTGW - B.xmin, gy = Y0 - 1 + g / kTGW - B.ymin;
             if (gx < 0 || gx >= B.nx || gy < 0 || gy >= B.ny) continue;
             const int32_t m = map[B.off + (long long)gy * B.nx + gx];
-            float v[kTNB];
+            float v[NB];
 #pragma unroll
-            for (int q = 0; q < kTNB; q++) {
+            for (int q = 0; q < NB; q++) {
                 const int b = bbeg + q < batch ? bbeg + q : batch - 1;
                 if constexpr ((PF_TGT_DIAG & 1) != 0) v[q] = (float)(m & 1023) * 1e-3f + (float)b;
                 else v[q] = tiles[b * tstride + toff + m];
             }
 #pragma unroll
-            for (int q = 0; q < kTNB; q++) {
+            for (int q = 0; q < NB; q++) {
                 float x = v[q];
                 if constexpr (XFORM) x = cubic_map(x, k[q].x, k[q].y, k[q].z, k[q].w);
                 sv[q][g] = x;
@@ -224,7 +224,7 @@ __device__ __forceinline__ void targets_patch(const TileGeom* __restrict__ geom,
             if (X < L.w && Y <= L.h1 && Y > L.h0 && Y < L.h1 && in_box2(bx, X, Y)) {
                 const int c = (r + 1) * kTGW + (t & (kTPW - 1)) + 1;  // (X, Y) in the grid
 #pragma unroll
-                for (int q = 0; q < kTNB; q++) {
+                for (int q = 0; q < NB; q++) {
                     // taps in std::map key order: (X-1,Y), (X,Y-1), (X,Y), (X,Y+1), (X+1,Y)
                     float Lp = 0;
                     Lp += sv[q][c - 1] * -0.25f;
@@ -263,7 +263,7 @@ __device__ __forceinline__ void targets_patch(const TileGeom* __restrict__ geom,
         }
         const long long o = (long long)Y * L.w + X;
 #pragma unroll
-        for (int q = 0; q < kTNB; q++) {
+        for (int q = 0; q < NB; q++) {
             const int b = bbeg + q;
             if (b >= batch) break;
             float out;
@@ -281,7 +281,7 @@ __device__ __forceinline__ void targets_patch(const TileGeom* __restrict__ geom,
     }
 }
 
-template <bool XFORM>
+template <bool XFORM, int NB>
 __global__ void __launch_bounds__(256) k_targets_patch(const TileGeom* __restrict__ geom,
                                                        const TileBox* __restrict__ box,
                                                        const TapBox* __restrict__ tb, int ntiles,
@@ -293,11 +293,11 @@ __global__ void __launch_bounds__(256) k_targets_patch(const TileGeom* __restric
                                                        float* __restrict__ lnorm,
                                                        long long lstride, int batch)
 {
-    __shared__ float sv[kTNB][kTG];
+    __shared__ float sv[NB][kTG];
     // XCD-contiguous runs of patches (neighbouring patches read the same tile lines)
     const unsigned lb = xcd_remap(blockIdx.x, gridDim.x);
     const int pid = (int)(lb % (unsigned)npatch), bgrp = (int)(lb / (unsigned)npatch);
-    targets_patch<XFORM>(geom, box, tb, ntiles, map, tiles, tstride, coeffs, L, npx, pid, bgrp,
+    targets_patch<XFORM, NB>(geom, box, tb, ntiles, map, tiles, tstride, coeffs, L, npx, pid, bgrp,
                          lnorm, lstride, batch, sv);
 }
 
@@ -309,7 +309,7 @@ __global__ void __launch_bounds__(256) k_targets_patch(const TileGeom* __restric
 // finest level's patches come first, then each coarser level's patches of the same band (a host
 // table of (level, patch) entries).  The XCD-contiguous mapping gives every XCD a contiguous run
 // of the table, so a band's lines are re-read from its L2 / the MALL instead of HBM.
-template <bool XFORM>
+template <bool XFORM, int NB>
 __global__ void __launch_bounds__(256) k_targets_multi(const TileGeom* __restrict__ geom,
                                                        int ntiles, const float* __restrict__ tiles,
                                                        long long tstride,
@@ -317,12 +317,12 @@ __global__ void __launch_bounds__(256) k_targets_multi(const TileGeom* __restric
                                                        TgtMulti M, const int2* __restrict__ order,
                                                        int batch)
 {
-    __shared__ float sv[kTNB][kTG];
+    __shared__ float sv[NB][kTG];
     const unsigned lb = xcd_remap(blockIdx.x, gridDim.x);
     const int e = (int)(lb % (unsigned)M.nentries), bgrp = (int)(lb / (unsigned)M.nentries);
     const int2 ent = order[e];  // (level, patch)
     const TgtLevel& T = M.lv[ent.x];
-    targets_patch<XFORM>(geom, T.box, T.tb, ntiles, T.map, tiles, tstride, coeffs, T.L, T.npx,
+    targets_patch<XFORM, NB>(geom, T.box, T.tb, ntiles, T.map, tiles, tstride, coeffs, T.L, T.npx,
                          ent.y, bgrp, T.lnorm, T.lstride, batch, sv, T.tmask, T.nmw);
 }
 
@@ -334,13 +334,21 @@ void launch_targets_multi(hipStream_t s, const TileGeom* geom, int ntiles, const
                           long long tstride, const float* coeffs, const TgtMulti& M,
                           const int2* order, int batch)
 {
-    const long long nblk = (long long)M.nentries * ((batch + kTNB - 1) / kTNB);
-    if (coeffs)
-        hipLaunchKernelGGL(k_targets_multi<true>, dim3((unsigned)nblk), dim3(256), 0, s, geom,
-                           ntiles, tiles, tstride, coeffs, M, order, batch);
+    // one panorama (pf_merge, C2 / C5): blocks of one panorama, not kTNB copies of it
+    const int nb = batch == 1 ? 1 : kTNB;
+    const dim3 g((unsigned)((long long)M.nentries * ((batch + nb - 1) / nb)));
+    if (nb == 1 && coeffs)
+        hipLaunchKernelGGL((k_targets_multi<true, 1>), g, dim3(256), 0, s, geom, ntiles, tiles,
+                           tstride, coeffs, M, order, batch);
+    else if (nb == 1)
+        hipLaunchKernelGGL((k_targets_multi<false, 1>), g, dim3(256), 0, s, geom, ntiles, tiles,
+                           tstride, coeffs, M, order, batch);
+    else if (coeffs)
+        hipLaunchKernelGGL((k_targets_multi<true, kTNB>), g, dim3(256), 0, s, geom, ntiles, tiles,
+                           tstride, coeffs, M, order, batch);
     else
-        hipLaunchKernelGGL(k_targets_multi<false>, dim3((unsigned)nblk), dim3(256), 0, s, geom,
-                           ntiles, tiles, tstride, coeffs, M, order, batch);
+        hipLaunchKernelGGL((k_targets_multi<false, kTNB>), g, dim3(256), 0, s, geom, ntiles,
+                           tiles, tstride, coeffs, M, order, batch);
 }
 
 void launch_targets_patch(hipStream_t s, const TileGeom* geom, const TileBox* box,
@@ -351,15 +359,22 @@ void launch_targets_patch(hipStream_t s, const TileGeom* geom, const TileBox* bo
     const int npx = (L.w + kTPW - 1) / kTPW;
     const int npy = (L.h1 - L.h0 + 1 + kTPH - 1) / kTPH;
     const int npatch = npx * npy;
-    const long long nblk = (long long)npatch * ((batch + kTNB - 1) / kTNB);
-    if (coeffs)
-        hipLaunchKernelGGL(k_targets_patch<true>, dim3((unsigned)nblk), dim3(256), 0, s, geom, box,
-                           tb, ntiles, map, tiles, tstride, coeffs, L, npx, npatch, lnorm, lstride,
+    const int nb = batch == 1 ? 1 : kTNB;
+    const dim3 g((unsigned)((long long)npatch * ((batch + nb - 1) / nb)));
+    if (nb == 1 && coeffs)
+        hipLaunchKernelGGL((k_targets_patch<true, 1>), g, dim3(256), 0, s, geom, box, tb, ntiles,
+                           map, tiles, tstride, coeffs, L, npx, npatch, lnorm, lstride, batch);
+    else if (nb == 1)
+        hipLaunchKernelGGL((k_targets_patch<false, 1>), g, dim3(256), 0, s, geom, box, tb, ntiles,
+                           map, tiles, tstride, coeffs, L, npx, npatch, lnorm, lstride, batch);
+    else if (coeffs)
+        hipLaunchKernelGGL((k_targets_patch<true, kTNB>), g, dim3(256), 0, s, geom, box, tb,
+                           ntiles, map, tiles, tstride, coeffs, L, npx, npatch, lnorm, lstride,
                            batch);
     else
-        hipLaunchKernelGGL(k_targets_patch<false>, dim3((unsigned)nblk), dim3(256), 0, s, geom,
-                           box, tb, ntiles, map, tiles, tstride, coeffs, L, npx, npatch, lnorm,
-                           lstride, batch);
+        hipLaunchKernelGGL((k_targets_patch<false, kTNB>), g, dim3(256), 0, s, geom, box, tb,
+                           ntiles, map, tiles, tstride, coeffs, L, npx, npatch, lnorm, lstride,
+                           batch);
 }
 
 void launch_tapmap(hipStream_t s, const TileGeom* geom, const TapBox* tb, int ntiles,
@@ -373,52 +388,81 @@ void launch_tapmap(hipStream_t s, const TileGeom* geom, const TapBox* tb, int nt
 }
 
 // Partial sums of tiles [t0, t1) for one panorama on rows [r0, r1) of the band (pf_fuse_partial,
-// pf_fuse_partial_rows: the sharded fusion).  k_targets_map's gather from the cached tap-index maps
-// without the normalisation: lsum = the tiles' Laplacians added in tile order, cnt = how many.
+// pf_fuse_partial_rows: the sharded fusion): lsum = the tiles' Laplacians added in tile order,
+// cnt = how many, with k_targets_map's per-pixel arithmetic.  Patch-staged like targets_patch,
+// for one panorama: a block owns a kPPW x kPPH patch of rows [r0, r1); for every tile of the range
+// whose box meets the patch (index order) the tap values of the patch plus a one-pixel ring are
+// gathered once from the tap-index map, transformed once (Depth2DepthTransform) and staged in
+// LDS, and the five-point stencils read LDS.  The per-pixel gather form re-read every tile value
+// five times and tested all t1-t0 boxes per pixel: C5 at world 1 spent 1.17 ms per panorama in it
+// against 0.55 ms for the one-call path's k_targets_multi (profiles/r05/c5).
+static constexpr int kPPW = 64, kPPH = 16, kPPP = kPPW * kPPH / 256;
+static constexpr int kPGW = kPPW + 2, kPG = kPGW * (kPPH + 2);
 template <bool XFORM>
-__global__ void __launch_bounds__(256) k_targets_map_partial(const TileGeom* __restrict__ geom,
-                                                             const TileBox* __restrict__ box,
-                                                             const TapBox* __restrict__ tb,
-                                                             int t0, int t1,
-                                                             const int32_t* __restrict__ map,
-                                                             const float* __restrict__ tiles,
-                                                             const float* __restrict__ coeffs,
-                                                             LevelDims L, float* __restrict__ lsum,
-                                                             float* __restrict__ cnt, int r0,
-                                                             int r1)
+__global__ void __launch_bounds__(256) k_targets_patch_partial(const TileGeom* __restrict__ geom,
+                                                               const TileBox* __restrict__ box,
+                                                               const TapBox* __restrict__ tb,
+                                                               int t0, int t1,
+                                                               const int32_t* __restrict__ map,
+                                                               const float* __restrict__ tiles,
+                                                               const float* __restrict__ coeffs,
+                                                               LevelDims L, float* __restrict__ lsum,
+                                                               float* __restrict__ cnt, int r0,
+                                                               int r1, int npx)
 {
+    __shared__ float sv[kPG];
     const unsigned lb = xcd_remap(blockIdx.x, gridDim.x);
-    const long long i = (long long)lb * 256 + threadIdx.x;
-    const long long n_ = (long long)L.w * (r1 - r0);
-    if (i >= n_) return;
-    const int Y = (int)(i / L.w) + r0, X = (int)(i - (long long)(Y - r0) * L.w);
-    float acc = 0.0f, n = 0.0f;
-    if (Y > L.h0 && Y < L.h1) {
-        for (int p = t0; p < t1; p++) {
-            if (!in_box2(box[p], X, Y)) continue;
-            const TapBox B = tb[p];
-            const long long base = B.off + (long long)(Y - B.ymin) * B.nx + (X - B.xmin);
-            const float* t = tiles + geom[p].off;
-            float v[5] = {t[map[base - 1]], t[map[base - B.nx]], t[map[base]], t[map[base + B.nx]],
-                          t[map[base + 1]]};
-            if constexpr (XFORM) {
-                const float4 k = *reinterpret_cast<const float4*>(coeffs + (long long)p * 4);
+    const int X0 = (int)(lb % (unsigned)npx) * kPPW, Y0 = r0 + (int)(lb / (unsigned)npx) * kPPH;
+    const int t = threadIdx.x;
+    const int X = X0 + (t & (kPPW - 1));
+    const int X1 = min(X0 + kPPW - 1, L.w - 1);
+    // band rows of the patch: Depth.cpp's targets exist on h0 < Y < h1 only
+    const int ya = max(Y0, L.h0 + 1), yb = min(min(Y0 + kPPH - 1, r1 - 1), L.h1 - 1);
+    float acc[kPPP], n[kPPP];
 #pragma unroll
-                for (int m = 0; m < 5; m++) v[m] = cubic_map(v[m], k.x, k.y, k.z, k.w);
-            }
-            float Lp = 0;  // std::map key order, as k_targets_map
-            Lp += v[0] * -0.25f;
-            Lp += v[1] * -0.25f;
-            Lp += v[2] * 1.0f;
-            Lp += v[3] * -0.25f;
-            Lp += v[4] * -0.25f;
-            acc += Lp;
-            n += 1.0f;
+    for (int j = 0; j < kPPP; j++) acc[j] = n[j] = 0.0f;
+    for (int p = t0; ya <= yb && p < t1; p++) {
+        const TileBox bx = box[p];
+        if (!box_meets(bx, X0, X1, ya, yb)) continue;  // block-uniform
+        const TapBox B = tb[p];
+        const float* tv = tiles + geom[p].off;
+        float4 k = make_float4(0.f, 0.f, 0.f, 0.f);
+        if constexpr (XFORM) k = *reinterpret_cast<const float4*>(coeffs + (long long)p * 4);
+        for (int g = t; g < kPG; g += 256) {
+            const int gx = X0 - 1 + g % kPGW - B.xmin, gy = Y0 - 1 + g / kPGW - B.ymin;
+            if (gx < 0 || gx >= B.nx || gy < 0 || gy >= B.ny) continue;
+            float x = tv[map[B.off + (long long)gy * B.nx + gx]];
+            if constexpr (XFORM) x = cubic_map(x, k.x, k.y, k.z, k.w);
+            sv[g] = x;
         }
+        __syncthreads();
+#pragma unroll
+        for (int j = 0; j < kPPP; j++) {
+            const int r = t / kPPW + j * (256 / kPPW);
+            const int Y = Y0 + r;
+            if (X <= X1 && Y >= ya && Y <= yb && in_box2(bx, X, Y)) {
+                const int c = (r + 1) * kPGW + (t & (kPPW - 1)) + 1;
+                // taps in std::map key order: (X-1,Y), (X,Y-1), (X,Y), (X,Y+1), (X+1,Y)
+                float Lp = 0;
+                Lp += sv[c - 1] * -0.25f;
+                Lp += sv[c - kPGW] * -0.25f;
+                Lp += sv[c] * 1.0f;
+                Lp += sv[c + kPGW] * -0.25f;
+                Lp += sv[c + 1] * -0.25f;
+                acc[j] += Lp;
+                n[j] += 1.0f;
+            }
+        }
+        __syncthreads();
     }
-    const long long o = (long long)Y * L.w + X;
-    lsum[o] = acc;
-    cnt[o] = n;
+#pragma unroll
+    for (int j = 0; j < kPPP; j++) {
+        const int Y = Y0 + t / kPPW + j * (256 / kPPW);
+        if (X > X1 || Y >= r1) continue;
+        const long long o = (long long)Y * L.w + X;
+        lsum[o] = acc[j];
+        cnt[o] = n[j];
+    }
 }
 
 void launch_targets_map_partial(hipStream_t s, const TileGeom* geom, const TileBox* box,
@@ -426,15 +470,15 @@ void launch_targets_map_partial(hipStream_t s, const TileGeom* geom, const TileB
                                 const float* tiles, const float* coeffs, LevelDims L, float* lsum,
                                 float* cnt, int r0, int r1)
 {
-    const long long n = (long long)L.w * (r1 - r0);
-    if (n <= 0) return;
-    const unsigned g = (unsigned)((n + 255) / 256);
+    if (r1 <= r0 || L.w <= 0) return;
+    const int npx = (L.w + kPPW - 1) / kPPW, npy = (r1 - r0 + kPPH - 1) / kPPH;
+    const unsigned g = (unsigned)npx * (unsigned)npy;
     if (coeffs)
-        hipLaunchKernelGGL(k_targets_map_partial<true>, dim3(g), dim3(256), 0, s, geom, box, tb, t0,
-                           t1, map, tiles, coeffs, L, lsum, cnt, r0, r1);
+        hipLaunchKernelGGL(k_targets_patch_partial<true>, dim3(g), dim3(256), 0, s, geom, box, tb,
+                           t0, t1, map, tiles, coeffs, L, lsum, cnt, r0, r1, npx);
     else
-        hipLaunchKernelGGL(k_targets_map_partial<false>, dim3(g), dim3(256), 0, s, geom, box, tb, t0,
-                           t1, map, tiles, coeffs, L, lsum, cnt, r0, r1);
+        hipLaunchKernelGGL(k_targets_patch_partial<false>, dim3(g), dim3(256), 0, s, geom, box, tb,
+                           t0, t1, map, tiles, coeffs, L, lsum, cnt, r0, r1, npx);
 }
 
 void launch_targets_map(hipStream_t s, const TileGeom* geom, const TileBox* box,

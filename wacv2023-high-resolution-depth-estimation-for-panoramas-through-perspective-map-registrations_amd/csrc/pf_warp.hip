@@ -1266,12 +1266,8 @@ __global__ void __launch_bounds__(256) k_warp_rgb_box(const TileGeom* __restrict
     // 16 bytes from a & ~7 as two 8-B reads (ds_read_b64 banks over 64 dwords: the 16 lanes of a
     // tile row span ~42), then the 8 bytes from a picked and aligned in registers
     auto pair6 = [&](const uint32_t* L, uint32_t a, float* c) {
-        typedef uint32_t u2v __attribute__((ext_vector_type(2)));
-        const u2v* w = reinterpret_cast<const u2v*>(L + ((a >> 3) << 1));
-        const u2v x = w[0], y = w[1];
-        const bool up = (a & 4u) != 0;  // bytes a.. start in the second dword
-        const uint32_t s0 = up ? x[1] : x[0], s1 = up ? y[0] : x[1], s2 = up ? y[1] : y[0];
-        const uint32_t sh = a & 3u;
+        const uint32_t* w = L + (a >> 2);
+        const uint32_t s0 = w[0], s1 = w[1], s2 = w[2], sh = a & 3u;
         const uint32_t lo = __builtin_amdgcn_alignbyte(s1, s0, sh);  // bytes a .. a+3
         const uint32_t hi = __builtin_amdgcn_alignbyte(s2, s1, sh);  // bytes a+4 .. a+7
         c[0] = (float)(lo & 0xFFu);

@@ -288,7 +288,8 @@ def fuse_row_sharded(backend, nlevels, ntiles, rank, world, comm=None, log=None,
       tile_rows(level, t0, t1) -> (ymin, ymax)   rows with non-zero sums of tiles [t0, t1)
       partial_rows(level, t0, t1, row0, row1, lsum, cnt)   the sums of tiles [t0, t1) on rows
                                                [row0, row1) (cnt: their coverage count)
-      coverage_rows(level, row0, row1, cnt)    the count of ALL tiles on rows [row0, row1)
+      coverage_plane(level) -> the coverage count of ALL tiles on the level's band (layout-only;
+                                               a backend may count it once and keep it)
       rows_add(dst, src)                       dst += src (device views)
       multicover_count / multicover / multicover_patch   as fuse_tile_sharded
       normalize_rows(level, lsum, cnt, row0, row1, lnorm)
@@ -313,7 +314,8 @@ def fuse_row_sharded(backend, nlevels, ntiles, rank, world, comm=None, log=None,
             pass
     for level in range(nlevels):
         last = level == nlevels - 1
-        rep = world > 1 and level < rep_levels
+        # replicated: the whole level on this rank (at world 1, every level: the one-GPU path)
+        rep = world == 1 or level < rep_levels
         w, h, h0, h1 = backend.dims(level)
         key = (level, world, rep, ntiles)
         if key not in geo:
@@ -365,7 +367,8 @@ def fuse_row_sharded(backend, nlevels, ntiles, rank, world, comm=None, log=None,
         lo, hi = (min(e0, mlo), max(e1, mhi)) if mlo < mhi else (e0, e1)
         backend.partial_rows(level, t0, t1, lo, hi, lsum, cnt)  # rep: lo, hi = the whole band
         if world > 1:
-            backend.coverage_rows(level, e0, e1, cnt)  # every tile's count: layout-only
+            # every tile's coverage count (layout-only: counted once per backend and level)
+            cnt = backend.coverage_plane(level)
             sends, recvs, bufs = [], [], []
             for d in range(world):
                 if d == rank:
@@ -549,8 +552,13 @@ class HipRowShardBackend:
         self.fz.fuse_partial_rows(self.tiles, self.coeffs, t0, t1, self.out_w, self.zr, level,
                                   row0, row1, lsum, cnt)
 
-    def coverage_rows(self, level, row0, row1, cnt):
-        self.fz.fuse_coverage_rows(self.out_w, self.zr, level, row0, row1, cnt)
+    def coverage_plane(self, level):
+        cov = self.__dict__.setdefault("_cov", {})
+        if level not in cov:
+            w, h, h0, h1 = self.levels[level][:4]
+            cov[level] = self.plane(level)
+            self.fz.fuse_coverage_rows(self.out_w, self.zr, level, h0, h1 + 1, cov[level])
+        return cov[level]
 
     def rows_add(self, dst, src):
         self.fz.rows_add(dst, src)
