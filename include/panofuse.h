@@ -147,6 +147,14 @@ int pf_fuse_seed(pf_ctx* ctx, const float* emap, int ew, int eh, int ec, const f
 int pf_fuse_finish_level(pf_ctx* ctx, const float* lsum, const float* cnt, int out_w,
                          int out_h, float zr0, float zr1, int level, float* buf,
                          uint16_t* out);
+/* pf_fuse_seed + pf_fuse_finish_level in one: the level is seeded (level 0 from emap, else
+ * the 2x upsample of prev, the previous level's plane) inside its first sweep pass, as
+ * pf_merge does it, with no seeded plane and no full-plane copies.  buf receives the level
+ * (every row), except on the last level with out != NULL, where only out is written.  The
+ * replicated levels of the row-sharded C5 flow (pf_dist.fuse_row_sharded).  Round 5. */
+int pf_fuse_level(pf_ctx* ctx, const float* emap, int ew, int eh, int ec, const float* prev,
+                  const float* lsum, const float* cnt, int out_w, int out_h, float zr0,
+                  float zr1, int level, float* buf, uint16_t* out);
 /* Exactness of the summed grids.  Per pixel the reference adds the covering tiles' Laplacians
  * one at a time (Depth.cpp:1609-1617); summing per-rank partials reproduces that for pixels
  * covered by at most two tiles, not for the few covered by three or more (sector corners on

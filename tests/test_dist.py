@@ -170,6 +170,10 @@ class OracleRowBackend(OracleBackend):
             self.out.copy_(torch.from_numpy(self.O.quantize(res).view(np.int16).ravel()))
         return torch.from_numpy(np.ascontiguousarray(res).ravel().copy())
 
+    def level(self, level, prev, lsum, cnt, last):  # pf_fuse_level's contract
+        res = self.finish(level, lsum, cnt, self.seed(level, prev), last)
+        return None if last else res
+
     def _subset(self, level, t0, t1):
         key = (level, t0, t1)
         if not hasattr(self, "_sub"):

@@ -1128,19 +1128,12 @@ void rgb_patches_host(const TileGeom& g, int tile, const RgbTap* taps, int pw, i
     }
 }
 
-__device__ __forceinline__ uint32_t rgb_u8(float v)
-{  // (int)floorf(v + 0.5f) clamped to [0, 255]: v >= 0 (a blend of u8 values with weights in
-   // [0, 1]), so the floor is the truncating conversion
-    const uint32_t q = (uint32_t)(v + 0.5f);
-    return q < 255u ? q : 255u;
-}
-
 __device__ __forceinline__ float lerp_ref(float a, float b, float w)
 {  // a * (1 - w) + b * w with separate roundings (the oracle's / GL-restatement order)
     return a * (1.0f - w) + b * w;
 }
 
-__global__ void __launch_bounds__(256) k_warp_rgb_box(const TileGeom* __restrict__ geom,
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) k_warp_rgb_box(const TileGeom* __restrict__ geom,
                                                       const RgbPatch* __restrict__ patches,
                                                       int npatch,
                                                       const uint32_t* __restrict__ unit_tbl,
@@ -1189,33 +1182,62 @@ __global__ void __launch_bounds__(256) k_warp_rgb_box(const TileGeom* __restrict
 
     auto blend_store = [&](const auto& corner, uint8_t* tb) {
         // corner(k, c) -> the 12 floats c00 RGB, c01 RGB, c10 RGB, c11 RGB of pixel k
-        uint32_t q[12];
+        typedef float f2 __attribute__((ext_vector_type(2)));
+        float c00[12], c01[12], c10[12], c11[12];
 #pragma unroll
         for (int k = 0; k < 4; k++) {
             float c[12];
             corner(k, c);
 #pragma unroll
             for (int ch = 0; ch < 3; ch++) {
-                const float top = lerp_ref(c[ch], c[3 + ch], ax[k]);
-                const float bot = lerp_ref(c[6 + ch], c[9 + ch], ax[k]);
-                q[3 * k + ch] = rgb_u8(lerp_ref(top, bot, ay[k]));
+                c00[3 * k + ch] = c[ch];
+                c01[3 * k + ch] = c[3 + ch];
+                c10[3 * k + ch] = c[6 + ch];
+                c11[3 * k + ch] = c[9 + ch];
             }
+        }
+        // the 12 values (pixel k, channel ch) at 3k + ch, blended two at a time with packed fp32
+        // (v_pk_mul / v_pk_add: per element the same IEEE operations as lerp_ref)
+        float v[12];
+#pragma unroll
+        for (int i = 0; i < 6; i++) {
+            const int e0 = 2 * i, e1 = 2 * i + 1;
+            const f2 wx = {ax[e0 / 3], ax[e1 / 3]}, wy = {ay[e0 / 3], ay[e1 / 3]};
+            const f2 one = {1.0f, 1.0f}, half = {0.5f, 0.5f};
+            const f2 mx = one - wx, my = one - wy;
+            const f2 top = f2{c00[e0], c00[e1]} * mx + f2{c01[e0], c01[e1]} * wx;
+            const f2 bot = f2{c10[e0], c10[e1]} * mx + f2{c11[e0], c11[e1]} * wx;
+            const f2 r = (top * my + bot * wy) + half;
+            v[e0] = r.x;
+            v[e1] = r.y;
+        }
+        // (int)floorf(v + 0.5f) clamped to [0, 255] (the oracle's u8 rounding), the 12 bytes packed into 3 dwords:
+        // v + 0.5 >= 0.5 and, the blend being of values <= 255 with weights summing to 1 under
+        // five fp32 roundings, below 255 * (1 + 2^-24)^5 + 0.5 < 256, so the truncating
+        // conversion is the clamp and the floor; SDWA writes each result into its byte lane
+        uint32_t o[3];
+#pragma unroll
+        for (int j = 0; j < 3; j++) {
+            asm("v_cvt_u32_f32_sdwa %0, %1 dst_sel:BYTE_0 dst_unused:UNUSED_PAD src0_sel:DWORD"
+                : "=v"(o[j]) : "v"(v[4 * j]));
+            asm("v_cvt_u32_f32_sdwa %0, %1 dst_sel:BYTE_1 dst_unused:UNUSED_PRESERVE "
+                "src0_sel:DWORD" : "+v"(o[j]) : "v"(v[4 * j + 1]));
+            asm("v_cvt_u32_f32_sdwa %0, %1 dst_sel:BYTE_2 dst_unused:UNUSED_PRESERVE "
+                "src0_sel:DWORD" : "+v"(o[j]) : "v"(v[4 * j + 2]));
+            asm("v_cvt_u32_f32_sdwa %0, %1 dst_sel:BYTE_3 dst_unused:UNUSED_PRESERVE "
+                "src0_sel:DWORD" : "+v"(o[j]) : "v"(v[4 * j + 3]));
         }
         const auto orr = rsrc(tb, tbytes);
         if (ok[3]) {
             typedef uint32_t u3v __attribute__((ext_vector_type(3)));
-            const u3v o = {q[0] | q[1] << 8 | q[2] << 16 | q[3] << 24,
-                           q[4] | q[5] << 8 | q[6] << 16 | q[7] << 24,
-                           q[8] | q[9] << 8 | q[10] << 16 | q[11] << 24};
-            __builtin_amdgcn_raw_buffer_store_b96(o, orr, (int)ob, 0, 2);
+            const u3v ov = {o[0], o[1], o[2]};
+            __builtin_amdgcn_raw_buffer_store_b96(ov, orr, (int)ob, 0, 2);
         } else {
 #pragma unroll
-            for (int k = 0; k < 4; k++)
-                if (ok[k])
-#pragma unroll
-                    for (int ch = 0; ch < 3; ch++)
-                        __builtin_amdgcn_raw_buffer_store_b8((uint8_t)q[3 * k + ch], orr,
-                                                             (int)(ob + 3 * k + ch), 0, 2);
+            for (int e = 0; e < 12; e++)
+                if (ok[e / 3])
+                    __builtin_amdgcn_raw_buffer_store_b8((uint8_t)(o[e / 4] >> (8 * (e % 4))), orr,
+                                                         (int)(ob + e), 0, 2);
         }
     };
 
@@ -1263,8 +1285,8 @@ __global__ void __launch_bounds__(256) k_warp_rgb_box(const TileGeom* __restrict
             *reinterpret_cast<u4v*>(boxw + pa * (kRgbCap / 4) + 4 * (t + 256 * u)) = v[u];
     };
     // the 6 bytes R0 G0 B0 R1 G1 B1 at byte offset a of parity L, as floats into c[0..5]: the
-    // 16 bytes from a & ~7 as two 8-B reads (ds_read_b64 banks over 64 dwords: the 16 lanes of a
-    // tile row span ~42), then the 8 bytes from a picked and aligned in registers
+    // three dwords from a & ~3 (the lanes of a tile row 3 dwords apart: an odd stride over the
+    // banks), aligned with v_alignbyte (two 8-B reads from a & ~7 measured slower, 0.71 ms)
     auto pair6 = [&](const uint32_t* L, uint32_t a, float* c) {
         const uint32_t* w = L + (a >> 2);
         const uint32_t s0 = w[0], s1 = w[1], s2 = w[2], sh = a & 3u;

@@ -293,6 +293,8 @@ def fuse_row_sharded(backend, nlevels, ntiles, rank, world, comm=None, log=None,
       rows_add(dst, src)                       dst += src (device views)
       multicover_count / multicover / multicover_patch   as fuse_tile_sharded
       normalize_rows(level, lsum, cnt, row0, row1, lnorm)
+      level(level, prev, lsum, cnt, last) -> the level's plane (None after the last level)
+                                               a replicated level: normalise + seeded sweeps
       plan(level, nbands) -> [T, ...]          identical on every rank
       border(level, prev, a, b)               rows outside [h0, h1] (u16 `out` on the last level)
       band_pass(level, lnorm, src_mode, src, dst, T, row0, row1, last, prev)
@@ -394,8 +396,7 @@ def fuse_row_sharded(backend, nlevels, ntiles, rank, world, comm=None, log=None,
                     log.add("multicover", 4 * contrib.numel())
                 backend.multicover_patch(level, contrib, lsum)
         if rep:  # the whole level on this rank: the one-GPU level (seed, normalise, sweeps)
-            buf = backend.seed(level, prev)
-            prev = backend.finish(level, lsum, cnt, buf, last)
+            prev = backend.level(level, prev, lsum, cnt, last)
             pbounds = None
             continue
         backend.normalize_rows(level, lsum, cnt, e0, e1, lnorm)
@@ -570,16 +571,14 @@ class HipRowShardBackend:
     def normalize_rows(self, level, lsum, cnt, row0, row1, lnorm):
         self.fz.fuse_normalize_rows(lsum, cnt, self.out_w, self.zr, level, row0, row1, lnorm)
 
-    def seed(self, level, prev):  # a replicated level: the one-GPU path (fuse_tile_sharded's)
+    def level(self, level, prev, lsum, cnt, last):
+        """A replicated level: the one-GPU level from the summed targets (pf_fuse_level: seeded
+        inside the first sweep pass).  Returns the level's plane (None after the last)."""
         buf = self.plane(level)
-        self.fz.fuse_seed(self.emap if level == 0 else None, prev, self.out_w, self.zr, level,
-                          buf)
-        return buf
-
-    def finish(self, level, lsum, cnt, buf, last):
-        self.fz.fuse_finish_level(lsum, cnt, self.out_w, self.zr, level, buf,
-                                  self.out.view(self.levels[level][1], -1) if last else None)
-        return buf
+        self.fz.fuse_level(self.emap if level == 0 else None, prev, lsum, cnt, self.out_w,
+                           self.zr, level, buf,
+                           self.out.view(self.levels[level][1], -1) if last else None)
+        return None if last else buf
 
     def plan(self, level, nbands):
         return self.fz.fuse_band_plan(self.out_w, self.zr, level, nbands)
