@@ -91,7 +91,11 @@ struct RgbPatch {
     int wide;   // even one row's footprint exceeds the LDS slot: direct corner gathers
     int pad[2];
 };
-static constexpr int kRgbPW = 64, kRgbPH = 16;  // RGB warp patch (4 pixels per thread)
+#ifndef PF_RGB_PW
+#define PF_RGB_PW 64
+#endif
+// RGB warp patch: 256 threads x 4 consecutive pixels of one row (kRgbPW / 4 lanes per row)
+static constexpr int kRgbPW = PF_RGB_PW, kRgbPH = 1024 / kRgbPW;
 static constexpr int kRgbUnits = 512;            // 16-B units per patch (two per thread)
 static constexpr int kRgbCap = 16 * kRgbUnits;   // LDS bytes per parity: the u8 RGB rows as is
 

@@ -1154,9 +1154,10 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) k
     const RgbPatch P = patches[pid];
     const TileGeom& g = geom[P.tile];
     const int t = threadIdx.x;
-    const int X = P.X0 + 4 * (t & 15), Y = P.Y0 + (t >> 4);
+    constexpr int kRL = kRgbPW / 4;  // lanes per patch row
+    const int X = P.X0 + 4 * (t % kRL), Y = P.Y0 + t / kRL;
     const int bbeg = chunk * kNBR, nb = min(kNBR, batch - bbeg);
-    const bool rowok = (t >> 4) < P.nrow && Y < g.h;
+    const bool rowok = t / kRL < P.nrow && Y < g.h;
     bool ok[4];
     uint32_t la[4];
     float ax[4], ay[4];
