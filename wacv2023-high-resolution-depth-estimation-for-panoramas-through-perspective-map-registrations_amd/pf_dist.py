@@ -127,13 +127,18 @@ def fuse_tile_sharded(backend, nlevels, ntiles, rank, world, comm=None):
 #    rows it needs (its band + halo) and the rows it sends (pf_fuse_partial_rows); it sends each
 #    other rank the rows of that rank's band + halo where its tiles are non-zero -- in practice the
 #    K = T+1 halo rows to each neighbour -- and adds what it receives (pf_rows_add).  The coverage
-#    count is layout-only, so every rank counts its own rows (pf_fuse_coverage_rows): only fp32
-#    sums travel, never counts.
+#    count is layout-only, so every rank counts it itself, once per level and backend
+#    (pf_fuse_coverage_rows, coverage_plane): only fp32 sums travel, never counts.
 #  * Between levels: no broadcast of the bands.  The next level's first pass reads the 2x
 #    upsample of the previous level on its band + halo, i.e. about T/2 + 2 rows of the
 #    neighbouring ranks' previous bands, which they send (prev_exchange).
 #  * The u16 result is gathered to rank 0 only.
 #  * Rank 0 and the last rank own the rows above / below the band (k_border).
+#  * The coarsest levels may be replicated (rep_levels, auto_rep_levels): their bands would be a
+#    few halos deep, so each of their many short passes would wait on an exchange.  Every rank
+#    sends its tile rows to every rank instead and runs the whole level alone (pf_fuse_level);
+#    the next level then reads its previous rows locally.  At world 1 every level is replicated,
+#    which is the one-GPU path.
 # DESIGN.md section 6 tabulates the bytes per rank per panorama at C5.
 
 class TorchComm:
