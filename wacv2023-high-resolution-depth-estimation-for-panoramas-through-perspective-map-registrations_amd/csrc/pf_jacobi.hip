@@ -51,6 +51,11 @@
 #ifndef PF_JGATE
 #define PF_JGATE 0  // skip the sweep levels a step does not need (JLag::sweep_packed)
 #endif
+#ifndef PF_JFILL
+// the first PF_JFILL 6-step groups of a row chunk's lagged fill run as their own unrolled steps
+// with the levels they do not need compiled out (JLag::fill_from); 0 = off, -1 = per depth
+#define PF_JFILL -1
+#endif
 #ifndef PF_JLAG_PF
 #define PF_JLAG_PF 2  // steps of lead for the input and L row loads (1 or 2)
 #endif
@@ -497,27 +502,32 @@ struct JLag {
     // skipped with one wave-uniform branch -- its ring slots then hold stale rows, read only by
     // unneeded updates.  At the default depths this drops 10-30% of the issued updates (the
     // lagged start fills T levels over 3T steps, the drain empties them over T).
-    template <int PH, int GB, int T0, bool ROWS>
+    // NA: levels 1..NA are computed this step (the rest are idle in the chunk's fill, below)
+    template <int PH, int GB, int T0, bool ROWS, int NA>
     __device__ __forceinline__ void sweep_packed(Row<C>* nw, int k) const
     {
         constexpr int T1 = T0 + PF_JPK_GROUP < T ? T0 + PF_JPK_GROUP : T;
         // the groups run from the deepest level down: level t+1 reads the oldest row of level
         // t's ring before level t overwrites it, so the new row can take that row's registers
         // (all reads of a step are rows of earlier steps, so the order is free)
-        if constexpr (T1 < T) sweep_packed<PH, GB, T1, ROWS>(nw, k);
+        if constexpr (T1 < T) sweep_packed<PH, GB, T1, ROWS, NA>(nw, k);
+        constexpr int TB = T1 < NA ? T1 : NA;
+        if constexpr (T0 < TB)
 #if PF_JGATE
         if (k - kr0 >= 3 * (T0 + 1) && k - kr1 < T1)
 #endif
         {
-            Row<C> Lv[T1 - T0];
-            ring_get_range<GB, PH, T0 + 1, T1>(Lv);
-            if constexpr (C == 4) sweep_packed_group4<PH, T0, T1, ROWS>(Lv, nw, k);
-            else sweep_packed_group<PH, T0, T1, ROWS>(Lv, nw, k);
+            Row<C> Lv[TB - T0];
+            ring_get_range<GB, PH, T0 + 1, TB>(Lv);
+            if constexpr (C == 4) sweep_packed_group4<PH, T0, TB, ROWS>(Lv, nw, k);
+            else sweep_packed_group<PH, T0, TB, ROWS>(Lv, nw, k);
         }
     }
 
-    // Step k = (group base) + PH; GB = group base mod R.
-    template <int PH, bool ROWS, int GB>
+    // Step k = (group base) + PH; GB = (group base - k0) mod R: ring slots count from the
+    // chunk's first step, so they are compile-time constants without aligning k0.  NA < T only
+    // in the fill (fill_from).
+    template <int PH, bool ROWS, int GB, int NA = T>
     __device__ __forceinline__ void step(int k)
     {
         // level-0 row k-1 (loaded last step) joins the ring
@@ -535,14 +545,17 @@ struct JLag {
 #endif
         Row<C> nw[T];
         if constexpr (FAST) {
-            sweep_packed<PH, GB, 0, ROWS>(nw, k);
+            sweep_packed<PH, GB, 0, ROWS, NA>(nw, k);
         } else {
+            static_assert(NA == T, "the general form has no fill specialisation");
             Row<C> Lv[T];
             ring_get_range<GB, PH, 1, T>(Lv);
             sweep_general<PH>(Lv, nw);
         }
 #pragma unroll
-        for (int t = 1; t < T; t++) H[t][slot(PH, 2 * t)] = nw[t - 1];
+        for (int t = 1; t < T; t++)
+            if (t <= NA) H[t][slot(PH, 2 * t)] = nw[t - 1];  // an idle level keeps its rows
+        if constexpr (NA < T) return;  // no stored row before every level runs (fill_from)
         const int j = k - 2 * T;  // final-level row finished this step
         // xs0, vlo, vhi and C are even, so a lane's columns are all inside [vlo, vhi) or all
         // outside: one vector store per lane.
@@ -594,16 +607,54 @@ struct JLag {
         if constexpr (G + 1 < NG) return groups_from<ROWS, G + 1>(k, kend);
         else return true;
     }
-    // the step loop: enter the unrolled ring period at group g0 = (k0 mod R) / 6
+    // The chunk's fill.  The stored rows [r0, r1) of level T read level t's rows
+    // [r0 - (T - t), r1 + (T - t)) and nothing else; level t produces row k - 2t at step k, so
+    // its first needed row comes at step r0 - T + 3t = k0 + 1 + 3t.  Before that (s = k - k0 <
+    // 1 + 3t) level t feeds nothing that is stored.  The first NF groups therefore run as their
+    // own unrolled steps with levels na(s) + 1 .. T compiled out; an idle level keeps its
+    // zero-initialised rows, which only idle levels read (level t reads level t - 1 alone, which
+    // is active from three steps earlier).  At T = 10: 175 of the ~2,100 level-steps of a
+    // 183-row chunk.
+    static constexpr int na(int s)
+    {
+        const int a = s >= 1 ? (s - 1) / 3 : 0;
+        return a < T ? a : T;
+    }
+    static constexpr int NF_ALL = (3 * T + 1 + 5) / 6;  // groups with an idle level
+    // hipcc's register allocation of the unrolled loop is erratic in the fill length: at T = 10,
+    // 3 groups keep the step loop at 166-169 VGPRs (3 waves per SIMD) where 1 or 4 take 171-232;
+    // at T = 8, 4 groups keep 140-143 where 3 take 188 (checked in the ISA)
+    static constexpr int NF_AUTO = T == 8 ? 4 : 3;
+    static constexpr int NF_SEL = PF_JFILL < 0 ? NF_AUTO : PF_JFILL;
+    static constexpr int NF = !FAST ? 0 : (NF_SEL < NF_ALL ? NF_SEL : NF_ALL);
+    template <bool ROWS, int F>
+    __device__ __forceinline__ bool fill_from(int& k, int kend)
+    {
+        if constexpr (F < NF) {
+            constexpr int GB = 6 * (F % NG);
+            step<0, ROWS, GB, na(6 * F + 0)>(k);
+            step<1, ROWS, GB, na(6 * F + 1)>(k + 1);
+            step<2, ROWS, GB, na(6 * F + 2)>(k + 2);
+            step<3, ROWS, GB, na(6 * F + 3)>(k + 3);
+            step<4, ROWS, GB, na(6 * F + 4)>(k + 4);
+            step<5, ROWS, GB, na(6 * F + 5)>(k + 5);
+            k += 6;
+            if (k >= kend) return false;
+            return fill_from<ROWS, F + 1>(k, kend);
+        } else {
+            return true;
+        }
+    }
+    // the step loop from the chunk's first step k0 (ring group 0): the fill, the rest of its
+    // ring period, then whole periods
     template <bool ROWS>
-    __device__ __forceinline__ void run(int k0, int kend, int g0)
+    __device__ __forceinline__ void run(int k0, int kend)
     {
         int k = k0;
-        bool more = true;
-        if constexpr (NG > 3) { if (g0 == 3) more = groups_from<ROWS, (NG > 3 ? 3 : 0)>(k, kend); }
-        if constexpr (NG > 2) { if (more && g0 == 2) more = groups_from<ROWS, (NG > 2 ? 2 : 0)>(k, kend); }
-        if constexpr (NG > 1) { if (more && g0 == 1) more = groups_from<ROWS, (NG > 1 ? 1 : 0)>(k, kend); }
-        static_assert(NG <= 4, "entry switch covers up to 4 groups");
+        bool more = fill_from<ROWS, 0>(k, kend);
+        if constexpr (NF % NG != 0) {
+            if (more) more = groups_from<ROWS, NF % NG>(k, kend);
+        }
         while (more) more = groups_from<ROWS, 0>(k, kend);
     }
 };
@@ -676,24 +727,22 @@ __global__ void __launch_bounds__(256, PF_JLAG_WAVES) k_jlag(JacobiPass P)
     }
     S.lane_c = lane * C;
     // steps k0 .. kend: level 0 needs rows from r0 - T, the last output row r1-1 finishes at
-    // step r1 - 1 + 2T; k0 is rounded down to a multiple of 6 so ring slots are static.
-    int kfirst = S.r0 - T - 1;
-    int k0 = kfirst - (((kfirst % 6) + 6) % 6);
-    int kend = S.r1 + 2 * T;
+    // step r1 - 1 + 2T.  Ring slots count from k0 (JLag::step), so k0 needs no alignment.
+    const int k0 = S.r0 - T - 1;
+    const int kend = S.r1 + 2 * T;
     // prime the rows the first steps consume before their in-loop loads land (the rest are
     // loaded PF steps ahead inside step()).  The ring slots of rows before k0 stay unwritten:
-    // they only feed halo/stale cells, like the zero-initialised level rows.  k0 is a multiple
-    // of 6, so row k0 + r sits in buffer r.
+    // they only feed halo/stale cells, like the zero-initialised level rows.  Row k0 + r sits
+    // in buffer r (buffers count from k0, like the ring slots).
 #pragma unroll
     for (int r = 0; r + 1 < S_t::PF; r++) S.In[r] = S.load_input(k0 + r);
 #pragma unroll
     for (int r = 0; r < S_t::PF; r++) S.Lin[r] = S.load_row(S.lnorm, k0 + r);
-    const int g0 = (((k0 % R) + R) % R) / 6;  // k0 is a multiple of 6, so is R
     // rows computed by some level of this pass: k - 2t for k in [k0, kend + 5], t in [1, T]
     const int wlo = k0 - 2 * T, whi = kend + 3;
     const bool rows = (S.h0 >= wlo && S.h0 <= whi) || (S.h1 >= wlo && S.h1 <= whi);
-    if (!FAST || rows) S.template run<true>(k0, kend, g0);
-    else S.template run<false>(k0, kend, g0);
+    if (!FAST || rows) S.template run<true>(k0, kend);
+    else S.template run<false>(k0, kend);
 }
 
 // ---------------------------------------------------------------------------------------------
