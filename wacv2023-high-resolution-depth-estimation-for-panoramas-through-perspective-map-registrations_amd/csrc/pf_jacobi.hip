@@ -56,6 +56,9 @@
 // with the levels they do not need compiled out (JLag::fill_from); 0 = off, -1 = per depth
 #define PF_JFILL -1
 #endif
+#ifndef PF_JPIPE_FILL
+#define PF_JPIPE_FILL 3  // fill groups of the pipelined engine (PF_JFILL = -1)
+#endif
 #ifndef PF_JLAG_PF
 #define PF_JLAG_PF 2  // steps of lead for the input and L row loads (1 or 2)
 #endif
@@ -876,16 +879,19 @@ struct JPipe {
             nw[t - TB].v = pk_add_clamp01(cur[g] * reg_, H[l][md(PH - 2 * t, 3)].v * reg);
         }
     }
-    template <int PH, int T0, bool ROWS>
+    // own levels T0 < t <= min(T1, NA): levels past NA are idle in the fill (JLag::fill_from)
+    template <int PH, int T0, bool ROWS, int NA>
     __device__ __forceinline__ void sweep(const Row<C>* Lv, Row<C>* nw, int k) const
     {
         constexpr int T1 = T0 + G < TE ? T0 + G : TE;
-        sweep_group<PH, T0, T1, ROWS>(Lv, nw, k);
-        if constexpr (T1 < TE) sweep<PH, T1, ROWS>(Lv, nw, k);
+        constexpr int TB_ = T1 < NA ? T1 : NA;
+        if constexpr (T0 < TB_) sweep_group<PH, T0, TB_, ROWS>(Lv, nw, k);
+        if constexpr (T1 < TE) sweep<PH, T1, ROWS, NA>(Lv, nw, k);
     }
 
-    // step k = (group base) + PH, GB = group base mod R
-    template <int PH, bool ROWS, int GB>
+    // step k = (group base) + PH, GB = (group base - k0) mod R (ring slots count from the
+    // chunk's first step, as in JLag); levels past NA idle (the fill)
+    template <int PH, bool ROWS, int GB, int NA = T>
     __device__ __forceinline__ void step(int k)
     {
         // the input level's row k - 2TB + 1 joins ring H[0]
@@ -903,13 +909,15 @@ struct JPipe {
         Lin[md(PH + QO + PF, NB)] = load_row(lnorm, k + QO + PF);
         if constexpr (SI == 0) In[md(PH + PF - 1, NB)] = load_input(k + PF - 1);
         Row<C> nw[TS];
-        sweep<PH, TB - 1, ROWS>(Lv, nw, k);
+        sweep<PH, TB - 1, ROWS, NA>(Lv, nw, k);
 #pragma unroll
-        for (int t = TB; t < TE; t++) H[t - TB + 1][md(PH - 2 * t, 3)] = nw[t - TB];
+        for (int t = TB; t < TE; t++)
+            if (t <= NA) H[t - TB + 1][md(PH - 2 * t, 3)] = nw[t - TB];
         if constexpr (SI < S - 1) {
-            *reinterpret_cast<float2*>(xout + md(PH, 2) * (64 * C) + lane_c) =
-                make_float2(nw[TS - 1].v[0], nw[TS - 1].v[1]);
-        } else {
+            if constexpr (TE <= NA)  // else the next stage's first level is idle too
+                *reinterpret_cast<float2*>(xout + md(PH, 2) * (64 * C) + lane_c) =
+                    make_float2(nw[TS - 1].v[0], nw[TS - 1].v[1]);
+        } else if constexpr (NA == T) {
             const int j = k - 2 * T;  // final-level row finished this step
             if (j >= r0 && j < r1 && xs0 >= vlo && xs0 < vhi) {
                 const long long rowb = (long long)j * w + colbase;
@@ -945,15 +953,42 @@ struct JPipe {
         if constexpr (GI + 1 < NG) return groups_from<ROWS, GI + 1>(k, kend);
         else return true;
     }
+    // the fill as JLag::fill_from: level t idle for steps s = k - k0 < 1 + 3t (every stage runs
+    // the same steps, so the barriers still pair up)
+    static constexpr int na(int s)
+    {
+        const int a = s >= 1 ? (s - 1) / 3 : 0;
+        return a < T ? a : T;
+    }
+    static constexpr int NF_ALL = (3 * T + 1 + 5) / 6;
+    static constexpr int NF_SEL = PF_JFILL < 0 ? PF_JPIPE_FILL : PF_JFILL;
+    static constexpr int NF = NF_SEL < NF_ALL ? NF_SEL : NF_ALL;
+    template <bool ROWS, int F>
+    __device__ __forceinline__ bool fill_from(int& k, int kend)
+    {
+        if constexpr (F < NF) {
+            constexpr int GB = 6 * (F % NG);
+            step<0, ROWS, GB, na(6 * F + 0)>(k);
+            step<1, ROWS, GB, na(6 * F + 1)>(k + 1);
+            step<2, ROWS, GB, na(6 * F + 2)>(k + 2);
+            step<3, ROWS, GB, na(6 * F + 3)>(k + 3);
+            step<4, ROWS, GB, na(6 * F + 4)>(k + 4);
+            step<5, ROWS, GB, na(6 * F + 5)>(k + 5);
+            k += 6;
+            if (k >= kend) return false;
+            return fill_from<ROWS, F + 1>(k, kend);
+        } else {
+            return true;
+        }
+    }
     template <bool ROWS>
-    __device__ __forceinline__ void run(int k0, int kend, int g0)
+    __device__ __forceinline__ void run(int k0, int kend)
     {
         int k = k0;
-        bool more = true;
-        static_assert(NG <= 4, "entry switch covers up to 4 groups");
-        if constexpr (NG > 3) { if (g0 == 3) more = groups_from<ROWS, (NG > 3 ? 3 : 0)>(k, kend); }
-        if constexpr (NG > 2) { if (more && g0 == 2) more = groups_from<ROWS, (NG > 2 ? 2 : 0)>(k, kend); }
-        if constexpr (NG > 1) { if (more && g0 == 1) more = groups_from<ROWS, (NG > 1 ? 1 : 0)>(k, kend); }
+        bool more = fill_from<ROWS, 0>(k, kend);
+        if constexpr (NF % NG != 0) {
+            if (more) more = groups_from<ROWS, NF % NG>(k, kend);
+        }
         while (more) more = groups_from<ROWS, 0>(k, kend);
     }
 };
@@ -998,8 +1033,7 @@ __device__ __forceinline__ void jpipe_stage(const JacobiPass& P, int lane, int b
         for (int q = 0; q < 3; q++) St.H[l][q].v = f2{0.0f, 0.0f};
 #pragma unroll
     for (int q = 0; q < S_t::NB; q++) { St.In[q].v = f2{0.0f, 0.0f}; St.Lin[q].v = f2{0.0f, 0.0f}; }
-    const int kfirst = St.r0 - T - 1;
-    const int k0 = kfirst - md(kfirst, 6);
+    const int k0 = St.r0 - T - 1;  // ring slots count from k0: no alignment (JLag)
     const int kend = St.r1 + 2 * T;
     constexpr int QO = -2 * S_t::TB + 2;
     if constexpr (SI == 0) {
@@ -1008,13 +1042,12 @@ __device__ __forceinline__ void jpipe_stage(const JacobiPass& P, int lane, int b
     }
 #pragma unroll
     for (int r = 0; r < S_t::PF; r++) St.Lin[md(QO + r, S_t::NB)] = St.load_row(St.lnorm, k0 + QO + r);
-    const int g0 = md(k0, S_t::R) / 6;
     const int wlo = k0 - 2 * T, whi = kend + 3;
     const bool rows = (St.h0 >= wlo && St.h0 <= whi) || (St.h1 >= wlo && St.h1 <= whi);
     // rows is uniform over the workgroup (it depends on the chunk only), so every stage takes the
     // same branch and runs the same number of steps (= barriers)
-    if (rows) St.template run<true>(k0, kend, g0);
-    else St.template run<false>(k0, kend, g0);
+    if (rows) St.template run<true>(k0, kend);
+    else St.template run<false>(k0, kend);
 }
 
 template <int TS, int S, int SRC, bool OUT16>
