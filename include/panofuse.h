@@ -150,11 +150,17 @@ int pf_fuse_finish_level(pf_ctx* ctx, const float* lsum, const float* cnt, int o
 /* pf_fuse_seed + pf_fuse_finish_level in one: the level is seeded (level 0 from emap, else
  * the 2x upsample of prev, the previous level's plane) inside its first sweep pass, as
  * pf_merge does it, with no seeded plane and no full-plane copies.  buf receives the level
- * (every row), except on the last level with out != NULL, where only out is written.  The
- * replicated levels of the row-sharded C5 flow (pf_dist.fuse_row_sharded).  Round 5. */
+ * (every row), except on the last level with out != NULL, where only out is written.  cnt ==
+ * NULL: lsum holds the normalised targets (pf_fuse_targets).  The replicated levels of the
+ * row-sharded C5 flow (pf_dist.fuse_row_sharded).  Round 5. */
 int pf_fuse_level(pf_ctx* ctx, const float* emap, int ew, int eh, int ec, const float* prev,
                   const float* lsum, const float* cnt, int out_w, int out_h, float zr0,
                   float zr1, int level, float* buf, uint16_t* out);
+/* One level's normalised targets (every tile, one panorama; [h_l][w_l] fp32, the band rows
+ * written) -- what pf_fuse_level takes as lsum with cnt == NULL, when no partial sums need to
+ * travel (the one-rank row-sharded fusion).  Round 5. */
+int pf_fuse_targets(pf_ctx* ctx, const float* tiles, const float* coeffs, int out_w, int out_h,
+                    float zr0, float zr1, int level, float* lnorm);
 /* Exactness of the summed grids.  Per pixel the reference adds the covering tiles' Laplacians
  * one at a time (Depth.cpp:1609-1617); summing per-rank partials reproduces that for pixels
  * covered by at most two tiles, not for the few covered by three or more (sector corners on

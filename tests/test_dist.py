@@ -171,8 +171,23 @@ class OracleRowBackend(OracleBackend):
         return torch.from_numpy(np.ascontiguousarray(res).ravel().copy())
 
     def level(self, level, prev, lsum, cnt, last):  # pf_fuse_level's contract
-        res = self.finish(level, lsum, cnt, self.seed(level, prev), last)
+        buf = self.seed(level, prev)
+        if cnt is None:  # lsum holds the normalised targets (pf_fuse_targets)
+            lv = self._lv(level)
+            res = self.O.jacobi(buf.numpy().reshape(lv.h, lv.w), lsum.numpy().reshape(lv.h, lv.w),
+                                lv, lv.iters)
+            if last:
+                self.out.copy_(torch.from_numpy(self.O.quantize(res).view(np.int16).ravel()))
+                return None
+            return torch.from_numpy(np.ascontiguousarray(res).ravel().copy())
+        res = self.finish(level, lsum, cnt, buf, last)
         return None if last else res
+
+    def targets(self, level):  # pf_fuse_targets: every tile, normalised
+        lv = self._lv(level)
+        Ls, n = self._subset(level, 0, len(self.tiles))
+        Ln = self.O.normalize(Ls.reshape(lv.h, lv.w), n.reshape(lv.h, lv.w).astype(np.int32), lv)
+        return torch.from_numpy(np.ascontiguousarray(Ln, dtype=np.float32).ravel().copy())
 
     def _subset(self, level, t0, t1):
         key = (level, t0, t1)
@@ -282,12 +297,12 @@ def _row_worker(rank, world, port, q, rep=0):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world,rep", [(2, 0), (3, 1), (2, 3)])
+@pytest.mark.parametrize("world,rep", [(1, 0), (2, 0), (3, 1), (2, 3)])
 def test_row_sharded_fusion_gloo(world, rep):
     """tiles and rows sharded, halo rows exchanged between passes; rank 0 ends
     with the u16 panorama of the unsharded oracle fusion, bit for bit.  rep = the coarse levels
     replicated on every rank instead (an all-gather of the partial target rows, no pass halos):
-    none, the first, all three."""
+    none, the first, all three.  World 1: every level from pf_fuse_targets + pf_fuse_level."""
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()

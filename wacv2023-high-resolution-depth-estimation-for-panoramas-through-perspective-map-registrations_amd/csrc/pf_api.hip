@@ -2137,17 +2137,39 @@ int pf_fuse_finish_level(pf_ctx* c, const float* lsum, const float* cnt, int out
     return PF_OK;
 }
 
+// One level's normalised targets of one panorama from every tile (the one-GPU gather,
+// k_targets_patch with one-panorama blocks): the replicated levels of a one-rank row-sharded
+// fusion need no partial sums.
+int pf_fuse_targets(pf_ctx* c, const float* tiles, const float* coeffs, int out_w, int out_h,
+                    float zr0, float zr1, int level, float* lnorm)
+{
+    int rc;
+    if ((rc = check_common(c, 1))) return rc;
+    if (!tiles || !lnorm) return fail(c, PF_EINVAL, "NULL buffer");
+    if ((rc = prepare_levels(c, out_w, out_h, zr0, zr1))) return rc;
+    const LevelCache& lc = c->lc;
+    if (level < 0 || level >= lc.nlevels) return fail(c, PF_EINVAL, "bad level %d", level);
+    const LevelDims& L = lc.dims[level];
+    launch_targets_patch(c->stream, (const TileGeom*)c->geom.p, (const TileBox*)lc.box[level].p,
+                         (const TapBox*)lc.tapbox[level].p, c->ntiles,
+                         (const int32_t*)lc.tapmap[level].p, tiles, c->tile_elems, coeffs, L,
+                         lnorm, (long long)L.w * L.h, 1);
+    HIPCHK(c, hipGetLastError());
+    return PF_OK;
+}
+
 // One whole level of one panorama from its summed targets, seeded inside the sweeps: the
 // one-call path's level (fuse_range) for a caller that gathered (lsum, cnt) itself -- the
 // replicated levels of pf_dist.fuse_row_sharded.  pf_fuse_seed + pf_fuse_finish_level give the
-// same planes, through a seeded full-level plane and two copies.
+// same planes, through a seeded full-level plane and two copies.  cnt == NULL: lsum already holds
+// the normalised targets (pf_fuse_targets).
 int pf_fuse_level(pf_ctx* c, const float* emap, int ew, int eh, int ec, const float* prev,
                   const float* lsum, const float* cnt, int out_w, int out_h, float zr0, float zr1,
                   int level, float* buf, uint16_t* out)
 {
     int rc;
     if ((rc = check_common(c, 1))) return rc;
-    if (!lsum || !cnt || !buf) return fail(c, PF_EINVAL, "NULL buffer");
+    if (!lsum || !buf) return fail(c, PF_EINVAL, "NULL buffer");
     if ((rc = prepare_levels(c, out_w, out_h, zr0, zr1))) return rc;
     LevelCache& lc = c->lc;
     if (level < 0 || level >= lc.nlevels) return fail(c, PF_EINVAL, "bad level %d", level);
@@ -2157,29 +2179,40 @@ int pf_fuse_level(pf_ctx* c, const float* emap, int ew, int eh, int ec, const fl
     } else if (!prev) {
         return fail(c, PF_EINVAL, "level %d needs the previous level's buffer", level);
     }
-    if (jacobi_tcap(L) < 1) {  // the plain sweep form seeds a full plane first
-        if ((rc = pf_fuse_seed(c, emap, ew, eh, ec, prev, out_w, out_h, zr0, zr1, level, buf)))
-            return rc;
-        return pf_fuse_finish_level(c, lsum, cnt, out_w, out_h, zr0, zr1, level, buf, out);
-    }
     const long long st = (long long)L.w * L.h;
     if ((rc = ensure(c, c->lnorm, sizeof(float) * st))) return rc;
     if ((rc = ensure(c, c->lsum_ws, sizeof(float) * st))) return rc;
-    if (level == 0 && (rc = seed_tables(c, L, ew, eh, ec))) return rc;
     const bool last = level == lc.nlevels - 1;
     uint16_t* o = last ? out : nullptr;
+    if (cnt) launch_normalize(c->stream, lsum, cnt, L, (float*)c->lnorm.p);
+    const float* ln = cnt ? (const float*)c->lnorm.p : lsum;
+    float* other = (float*)c->lsum_ws.p;
+    const int ba = std::max(L.h0, 0), bb = std::min(L.h1 + 1, L.h);  // band rows [ba, bb)
+    float* res = nullptr;
+    if (jacobi_tcap(L) < 1) {  // the plain sweep form: a seeded full plane, copied, swept
+        if ((rc = pf_fuse_seed(c, emap, ew, eh, ec, prev, out_w, out_h, zr0, zr1, level, buf)))
+            return rc;
+        HIPCHK(c, hipMemcpyAsync(other, buf, sizeof(float) * st, hipMemcpyDeviceToDevice,
+                                 c->stream));
+        launch_jacobi(c->stream, buf, other, ln, st, L, L.iters, 1, &res);
+        if (res != buf && bb > ba)
+            HIPCHK(c, hipMemcpyAsync(buf + (size_t)ba * L.w, res + (size_t)ba * L.w,
+                                     sizeof(float) * (size_t)L.w * (bb - ba),
+                                     hipMemcpyDeviceToDevice, c->stream));
+        if (o) launch_quantize(c->stream, buf, st, (int)st, o, st, 1);
+        HIPCHK(c, hipGetLastError());
+        return PF_OK;
+    }
+    if (level == 0 && (rc = seed_tables(c, L, ew, eh, ec))) return rc;
     const JresPlan jp = jres_plan(c, L, 1, lc.full[level]);
     if (jp.on && (rc = jres_prepare(c, L, 1, jp))) return rc;
-    launch_normalize(c->stream, lsum, cnt, L, (float*)c->lnorm.p);
-    float* other = (float*)c->lsum_ws.p;
     // the rows outside the band, in both planes (the u16 rows too on the last level)
     launch_border(c->stream, level == 0 ? nullptr : prev, 0, L, buf, other, st, o, st, 1);
-    float* res = run_jacobi(c, L, level == 0 ? 2 : 1, emap, ew, eh, ec, 0,
-                            (const GridCol*)lc.cols[level].p, (const GridRow*)lc.rows[level].p,
-                            prev, 0, (const float*)c->lnorm.p, buf, other, o, st, 1, nullptr,
-                            lc.full[level] ? (const float*)lc.hcol[level].p : nullptr, &jp);
+    res = run_jacobi(c, L, level == 0 ? 2 : 1, emap, ew, eh, ec, 0,
+                     (const GridCol*)lc.cols[level].p, (const GridRow*)lc.rows[level].p, prev, 0,
+                     ln, buf, other, o, st, 1, nullptr,
+                     lc.full[level] ? (const float*)lc.hcol[level].p : nullptr, &jp);
     if (!res) return fail(c, PF_EINVAL, "level-0 seed tables missing");
-    const int ba = std::max(L.h0, 0), bb = std::min(L.h1 + 1, L.h);  // band rows [ba, bb)
     if (res != buf && bb > ba && !o)  // the band back into buf (its other rows are equal)
         HIPCHK(c, hipMemcpyAsync(buf + (size_t)ba * L.w, res + (size_t)ba * L.w,
                                  sizeof(float) * (size_t)L.w * (bb - ba),

@@ -31,11 +31,12 @@ EXPORTS = [
     "pf_jres_errors", "pf_set_jacobi_engine", "pf_stream_wait_level", "pf_debug_jres_fault",
     "pf_probe_warp_coords", "pf_probe_rgb_taps", "pf_debug_smooth_fault",
     "pf_fuse_partial_rows", "pf_fuse_coverage_rows", "pf_fuse_normalize_rows",
-    "pf_fuse_tile_rows", "pf_rows_add", "pf_fuse_level",
+    "pf_fuse_tile_rows", "pf_rows_add", "pf_fuse_level", "pf_fuse_targets",
 ]
 NEW_R4 = {"pf_debug_jres_fault", "pf_probe_warp_coords", "pf_probe_rgb_taps",
           "pf_debug_smooth_fault", "pf_fuse_partial_rows", "pf_fuse_coverage_rows",
-          "pf_fuse_normalize_rows", "pf_fuse_tile_rows", "pf_rows_add", "pf_fuse_level"}
+          "pf_fuse_normalize_rows", "pf_fuse_tile_rows", "pf_rows_add", "pf_fuse_level",
+          "pf_fuse_targets"}
 METRICS_ORDERS = {"tree": 0, "sequential": 1}  # PF_METRICS_*; "sequential" = the reference's
 SOLVERS = {"normal": 0, "lm": 1}  # PF_SOLVER_*; "lm" = the reference's Ceres LM (default)
 
@@ -119,6 +120,7 @@ def load():
                      ("pf_rows_add", [vp, vp, vp, C.c_longlong]),
                      ("pf_fuse_level", [vp, vp, ip, ip, ip, vp, vp, vp, ip, ip, fp, fp, ip, vp,
                                         vp]),
+                     ("pf_fuse_targets", [vp, vp, vp, ip, ip, fp, fp, ip, vp]),
                      ("pf_probe_warp_coords", [C.POINTER(Window), ip, ip, ip, ip, vp, vp]),
                      ("pf_probe_rgb_taps", [C.POINTER(Window), ip, ip, ip, ip, vp])):
         if hasattr(L, name):
@@ -370,6 +372,11 @@ class Fuser:
         self._check(self.L.pf_fuse_level(self.h, _ptr(emap), ew, eh, ec, _ptr(prev), _ptr(lsum),
                                          _ptr(cnt), out_w, out_w // 2, float(zr[0]),
                                          float(zr[1]), level, _ptr(buf), _ptr(out)))
+
+    def fuse_targets(self, tiles, coeffs, out_w, zr, level, lnorm):
+        """pf_fuse_targets: one level's normalised targets of one panorama from every tile."""
+        self._check(self.L.pf_fuse_targets(self.h, _ptr(tiles), _ptr(coeffs), out_w, out_w // 2,
+                                           float(zr[0]), float(zr[1]), level, _ptr(lnorm)))
 
     def multicover_count(self, out_w, zr, level):
         n = C.c_int(0)

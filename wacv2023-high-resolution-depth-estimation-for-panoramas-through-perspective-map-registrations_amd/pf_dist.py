@@ -300,6 +300,8 @@ def fuse_row_sharded(backend, nlevels, ntiles, rank, world, comm=None, log=None,
       normalize_rows(level, lsum, cnt, row0, row1, lnorm)
       level(level, prev, lsum, cnt, last) -> the level's plane (None after the last level)
                                                a replicated level: normalise + seeded sweeps
+                                               (cnt None: lsum holds normalised targets)
+      targets(level) -> the level's normalised targets from every tile (world 1)
       plan(level, nbands) -> [T, ...]          identical on every rank
       border(level, prev, a, b)               rows outside [h0, h1] (u16 `out` on the last level)
       band_pass(level, lnorm, src_mode, src, dst, T, row0, row1, last, prev)
@@ -368,6 +370,9 @@ def fuse_row_sharded(backend, nlevels, ntiles, rank, world, comm=None, log=None,
             comm.exchange(sends, recvs)
             if log:
                 log.add("prev_halo", sum(4 * t.numel() for _, t in sends))
+        if world == 1:  # nothing travels: the level's normalised targets from every tile
+            prev = backend.level(level, prev, backend.targets(level), None, last)
+            continue
         # targets: this rank's tiles on the rows it needs and the rows it sends
         lsum, cnt, lnorm = backend.plane(level), backend.plane(level), backend.plane(level)
         mlo, mhi = ext[rank][0], ext[rank][1] + 1
@@ -575,6 +580,11 @@ class HipRowShardBackend:
 
     def normalize_rows(self, level, lsum, cnt, row0, row1, lnorm):
         self.fz.fuse_normalize_rows(lsum, cnt, self.out_w, self.zr, level, row0, row1, lnorm)
+
+    def targets(self, level):
+        lnorm = self.plane(level)
+        self.fz.fuse_targets(self.tiles, self.coeffs, self.out_w, self.zr, level, lnorm)
+        return lnorm
 
     def level(self, level, prev, lsum, cnt, last):
         """A replicated level: the one-GPU level from the summed targets (pf_fuse_level: seeded
