@@ -146,3 +146,63 @@ def test_tile_sharded_c5_threads_equals_fuse():
     """fuse_tile_sharded at world 8 (reduce to rank 0, the 7 pixels per level covered by four
     tiles re-added in tile order): rank 0's u16 == the one-GPU fusion."""
     _run("C5", 8, 20261015 + 13, flow="tiles")
+
+
+@pytest.mark.parametrize("cfg", ["C2", "C5"])
+def test_row_sharded_world1_equals_fuse(cfg):
+    """World 1: every level through pf_fuse_targets + pf_fuse_level (no partial sums, the seed
+    inside the first pass) equals the one-GPU pf_fuse bit for bit."""
+    _run(cfg, 1, 20261015 + 15)
+
+
+def test_fuse_level_forms_agree():
+    """The three ways to one level at C2, plane by plane and bit for bit: pf_fuse_seed +
+    pf_fuse_finish_level, pf_fuse_level on (lsum, cnt), and pf_fuse_level on pf_fuse_targets'
+    normalised plane; and pf_fuse_targets == pf_fuse_normalize_rows of the all-tile partial
+    sums (pf_fuse_partial_rows), sNaN markers included."""
+    lay = PL.config_layout("C2")
+    out_w, ew = PL.CONFIGS["C2"]
+    seeds = pf_synth.seeds_for(1, 20261015 + 16)
+    gt = pf_synth.scene_depth(seeds, out_w, out_w // 2, DEV).contiguous()
+    emap = pf_synth.baseline_emap(seeds, ew, ew // 2, DEV).contiguous()
+    fz = panofuse.Fuser(0)
+    fz.set_tiles(lay)
+    tiles = torch.zeros((1, fz.tile_elems), dtype=torch.float32, device=DEV)
+    fz.warp_depth(gt, tiles, panofuse.make_responses(pf_synth.responses(seeds, lay.ntiles), DEV))
+    coeffs = torch.zeros((1, lay.ntiles, 4), dtype=torch.float32, device=DEV)
+    fz.register(emap, tiles, ZR, apply=False, coeffs=coeffs)
+    nlev = panofuse.level_info(out_w, out_w // 2, ZR, 0)[5]
+    prev = {k: None for k in ("a", "b", "c")}
+    outs = {k: torch.zeros(out_w * (out_w // 2), dtype=torch.int16, device=DEV)
+            for k in ("a", "b", "c")}
+    for lv in range(nlev):
+        w, h, h0, h1 = panofuse.level_info(out_w, out_w // 2, ZR, lv)[:4]
+        last = lv == nlev - 1
+        lsum = torch.zeros(h * w, dtype=torch.float32, device=DEV)
+        cnt = torch.zeros_like(lsum)
+        lnorm = torch.zeros_like(lsum)
+        tgt = torch.zeros_like(lsum)
+        fz.fuse_partial_rows(tiles, coeffs[0], 0, lay.ntiles, out_w, ZR, lv, h0, h1 + 1, lsum, cnt)
+        fz.fuse_normalize_rows(lsum, cnt, out_w, ZR, lv, h0, h1 + 1, lnorm)
+        fz.fuse_targets(tiles, coeffs[0], out_w, ZR, lv, tgt)
+        band = slice(h0 * w, (h1 + 1) * w)
+        assert torch.equal(lnorm[band].view(torch.int32), tgt[band].view(torch.int32)), lv
+        bufs = {k: torch.zeros(h * w, dtype=torch.float32, device=DEV) for k in ("a", "b", "c")}
+        e = emap if lv == 0 else None
+        fz.fuse_seed(e, prev["a"], out_w, ZR, lv, bufs["a"])
+        fz.fuse_finish_level(lsum, cnt, out_w, ZR, lv, bufs["a"],
+                             outs["a"].view(h, w) if last else None)
+        fz.fuse_level(e, prev["b"], lsum, cnt, out_w, ZR, lv, bufs["b"],
+                      outs["b"].view(h, w) if last else None)
+        fz.fuse_level(e, prev["c"], tgt, None, out_w, ZR, lv, bufs["c"],
+                      outs["c"].view(h, w) if last else None)
+        torch.cuda.synchronize()
+        if not last:
+            assert torch.equal(bufs["a"], bufs["b"]) and torch.equal(bufs["a"], bufs["c"]), lv
+        prev = bufs
+    assert torch.equal(outs["a"], outs["b"]) and torch.equal(outs["a"], outs["c"])
+    ref = torch.zeros((1, out_w // 2, out_w), dtype=torch.int16, device=DEV)
+    fz.fuse(emap, tiles, ref, ZR, coeffs=coeffs)
+    torch.cuda.synchronize()
+    assert torch.equal(outs["a"].view(out_w // 2, out_w), ref[0])
+    fz.close()
