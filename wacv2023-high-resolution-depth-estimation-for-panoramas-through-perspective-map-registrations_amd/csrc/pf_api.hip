@@ -1971,10 +1971,11 @@ int pf_fuse_partial(pf_ctx* c, const float* tiles, const float* coeffs, int t0, 
     const LevelDims& L = lc.dims[level];
     HIPCHK(c, hipMemsetAsync(lsum, 0, sizeof(float) * L.w * L.h, c->stream));
     HIPCHK(c, hipMemsetAsync(cnt, 0, sizeof(float) * L.w * L.h, c->stream));
-    launch_targets_map_partial(c->stream, (const TileGeom*)c->geom.p,
+    HIPCHK(c, launch_targets_map_partial(c->stream, (const TileGeom*)c->geom.p,
                                (const TileBox*)lc.box[level].p, (const TapBox*)lc.tapbox[level].p,
-                               t0, t1, (const int32_t*)lc.tapmap[level].p, tiles, coeffs, L, lsum,
-                               cnt, L.h0, L.h1 + 1);
+                               (const uint32_t*)lc.tmask[level].p, (c->ntiles + 31) / 32, t0, t1,
+                               (const int32_t*)lc.tapmap[level].p, tiles, coeffs, L, lsum, cnt,
+                               L.h0, L.h1 + 1));
     HIPCHK(c, hipGetLastError());
     return PF_OK;
 }
@@ -2008,10 +2009,11 @@ int pf_fuse_partial_rows(pf_ctx* c, const float* tiles, const float* coeffs, int
     if (t0 < 0 || t1 > c->ntiles || t0 > t1)
         return fail(c, PF_EINVAL, "tile range [%d,%d) outside [0,%d)", t0, t1, c->ntiles);
     const LevelCache& lc = c->lc;
-    launch_targets_map_partial(c->stream, (const TileGeom*)c->geom.p,
+    HIPCHK(c, launch_targets_map_partial(c->stream, (const TileGeom*)c->geom.p,
                                (const TileBox*)lc.box[level].p, (const TapBox*)lc.tapbox[level].p,
-                               t0, t1, (const int32_t*)lc.tapmap[level].p, tiles, coeffs, *L, lsum,
-                               cnt, row0, std::max(row0, row1));
+                               (const uint32_t*)lc.tmask[level].p, (c->ntiles + 31) / 32, t0, t1,
+                               (const int32_t*)lc.tapmap[level].p, tiles, coeffs, *L, lsum, cnt,
+                               row0, std::max(row0, row1)));
     HIPCHK(c, hipGetLastError());
     return PF_OK;
 }
@@ -2153,7 +2155,8 @@ int pf_fuse_targets(pf_ctx* c, const float* tiles, const float* coeffs, int out_
     launch_targets_patch(c->stream, (const TileGeom*)c->geom.p, (const TileBox*)lc.box[level].p,
                          (const TapBox*)lc.tapbox[level].p, c->ntiles,
                          (const int32_t*)lc.tapmap[level].p, tiles, c->tile_elems, coeffs, L,
-                         lnorm, (long long)L.w * L.h, 1);
+                         lnorm, (long long)L.w * L.h, 1, (const uint32_t*)lc.tmask[level].p,
+                         (c->ntiles + 31) / 32);
     HIPCHK(c, hipGetLastError());
     return PF_OK;
 }

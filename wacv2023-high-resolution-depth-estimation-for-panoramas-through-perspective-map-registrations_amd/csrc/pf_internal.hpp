@@ -251,7 +251,8 @@ void launch_targets_map(hipStream_t s, const TileGeom* geom, const TileBox* box,
 void launch_targets_patch(hipStream_t s, const TileGeom* geom, const TileBox* box,
                           const TapBox* tb, int ntiles, const int32_t* map, const float* tiles,
                           long long tstride, const float* coeffs, LevelDims L, float* lnorm,
-                          long long lstride, int batch);
+                          long long lstride, int batch, const uint32_t* tmask = nullptr,
+                          int nmw = 0);
 // All levels' targets in one launch (pf_targets.hip): per level its tables and plane, and a host
 // table of (level, patch) entries in gather order (fuse_range builds it once per level set).
 struct TgtLevel {
@@ -294,10 +295,11 @@ void launch_targets(hipStream_t s, const TileGeom* geom, const TileBox* box, int
                     long long tstride, const float* coeffs, int ntiles_total, LevelDims L,
                     float* lnorm, long long lstride, int batch);
  // rows [r0,r1), -1: band
-void launch_targets_map_partial(hipStream_t s, const TileGeom* geom, const TileBox* box,
-                                const TapBox* tb, int t0, int t1, const int32_t* map,
-                                const float* tiles, const float* coeffs, LevelDims L, float* lsum,
-                                float* cnt, int r0, int r1);
+// the tile masks of the level's targets patches (LevelCache::tmask, targets_patch_w/h grid)
+hipError_t launch_targets_map_partial(hipStream_t s, const TileGeom* geom, const TileBox* box,
+                                const TapBox* tb, const uint32_t* tmask, int nmw, int t0, int t1,
+                                const int32_t* map, const float* tiles, const float* coeffs,
+                                LevelDims L, float* lsum, float* cnt, int r0, int r1);
 void launch_coverage_rows(hipStream_t s, const TileBox* box, int ntiles, LevelDims L, float* cnt,
                           int r0, int r1);
 void launch_rows_add(hipStream_t s, float* dst, const float* src, long long n);

@@ -291,14 +291,16 @@ __global__ void __launch_bounds__(256) k_targets_patch(const TileGeom* __restric
                                                        const float* __restrict__ coeffs,
                                                        LevelDims L, int npx, int npatch,
                                                        float* __restrict__ lnorm,
-                                                       long long lstride, int batch)
+                                                       long long lstride, int batch,
+                                                       const uint32_t* __restrict__ tmask,
+                                                       int nmw)
 {
     __shared__ float sv[NB][kTG];
     // XCD-contiguous runs of patches (neighbouring patches read the same tile lines)
     const unsigned lb = xcd_remap(blockIdx.x, gridDim.x);
     const int pid = (int)(lb % (unsigned)npatch), bgrp = (int)(lb / (unsigned)npatch);
     targets_patch<XFORM, NB>(geom, box, tb, ntiles, map, tiles, tstride, coeffs, L, npx, pid, bgrp,
-                         lnorm, lstride, batch, sv);
+                             lnorm, lstride, batch, sv, tmask, nmw);
 }
 
 // Every level's targets in ONE launch (round 4).  The per-level launches each streamed the
@@ -354,7 +356,7 @@ void launch_targets_multi(hipStream_t s, const TileGeom* geom, int ntiles, const
 void launch_targets_patch(hipStream_t s, const TileGeom* geom, const TileBox* box,
                           const TapBox* tb, int ntiles, const int32_t* map, const float* tiles,
                           long long tstride, const float* coeffs, LevelDims L, float* lnorm,
-                          long long lstride, int batch)
+                          long long lstride, int batch, const uint32_t* tmask, int nmw)
 {
     const int npx = (L.w + kTPW - 1) / kTPW;
     const int npy = (L.h1 - L.h0 + 1 + kTPH - 1) / kTPH;
@@ -363,18 +365,20 @@ void launch_targets_patch(hipStream_t s, const TileGeom* geom, const TileBox* bo
     const dim3 g((unsigned)((long long)npatch * ((batch + nb - 1) / nb)));
     if (nb == 1 && coeffs)
         hipLaunchKernelGGL((k_targets_patch<true, 1>), g, dim3(256), 0, s, geom, box, tb, ntiles,
-                           map, tiles, tstride, coeffs, L, npx, npatch, lnorm, lstride, batch);
+                           map, tiles, tstride, coeffs, L, npx, npatch, lnorm, lstride, batch,
+                           tmask, nmw);
     else if (nb == 1)
         hipLaunchKernelGGL((k_targets_patch<false, 1>), g, dim3(256), 0, s, geom, box, tb, ntiles,
-                           map, tiles, tstride, coeffs, L, npx, npatch, lnorm, lstride, batch);
+                           map, tiles, tstride, coeffs, L, npx, npatch, lnorm, lstride, batch,
+                           tmask, nmw);
     else if (coeffs)
         hipLaunchKernelGGL((k_targets_patch<true, kTNB>), g, dim3(256), 0, s, geom, box, tb,
                            ntiles, map, tiles, tstride, coeffs, L, npx, npatch, lnorm, lstride,
-                           batch);
+                           batch, tmask, nmw);
     else
         hipLaunchKernelGGL((k_targets_patch<false, kTNB>), g, dim3(256), 0, s, geom, box, tb,
                            ntiles, map, tiles, tstride, coeffs, L, npx, npatch, lnorm, lstride,
-                           batch);
+                           batch, tmask, nmw);
 }
 
 void launch_tapmap(hipStream_t s, const TileGeom* geom, const TapBox* tb, int ntiles,
@@ -389,47 +393,49 @@ void launch_tapmap(hipStream_t s, const TileGeom* geom, const TapBox* tb, int nt
 
 // Partial sums of tiles [t0, t1) for one panorama on rows [r0, r1) of the band (pf_fuse_partial,
 // pf_fuse_partial_rows: the sharded fusion): lsum = the tiles' Laplacians added in tile order,
-// cnt = how many, with k_targets_map's per-pixel arithmetic.  Patch-staged like targets_patch,
-// for one panorama: a block owns a kPPW x kPPH patch of rows [r0, r1); for every tile of the range
-// whose box meets the patch (index order) the tap values of the patch plus a one-pixel ring are
-// gathered once from the tap-index map, transformed once (Depth2DepthTransform) and staged in
-// LDS, and the five-point stencils read LDS.  The per-pixel gather form re-read every tile value
-// five times and tested all t1-t0 boxes per pixel: C5 at world 1 spent 1.17 ms per panorama in it
-// against 0.55 ms for the one-call path's k_targets_multi (profiles/r05/c5).
-static constexpr int kPPW = 64, kPPH = 16, kPPP = kPPW * kPPH / 256;
-static constexpr int kPGW = kPPW + 2, kPG = kPGW * (kPPH + 2);
+// cnt = how many, with k_targets_map's per-pixel arithmetic.  Staged like targets_patch, for one
+// panorama: a block owns one patch of the level's targets grid (kTPW x kTPH from row h0, the
+// grid of the host's per-patch tile masks) and, for every tile of the range whose box meets the
+// patch (the mask words ANDed with the range, index order), gathers the tap values of the patch
+// plus a one-pixel ring once from the tap-index map, transforms them once
+// (Depth2DepthTransform), stages them in LDS and reads the five-point stencils from LDS.  The
+// launch covers the grid's patch rows that meet [r0, r1).  The per-pixel gather form re-read
+// every tile value five times and tested all t1-t0 boxes per pixel: C5 at world 1 spent 1.17 ms
+// per panorama in it, against 0.55 ms for the one-call path's k_targets_multi.
 template <bool XFORM>
 __global__ void __launch_bounds__(256) k_targets_patch_partial(const TileGeom* __restrict__ geom,
                                                                const TileBox* __restrict__ box,
                                                                const TapBox* __restrict__ tb,
-                                                               int t0, int t1,
+                                                               const uint32_t* __restrict__ tmask,
+                                                               int nmw, int t0, int t1,
                                                                const int32_t* __restrict__ map,
                                                                const float* __restrict__ tiles,
                                                                const float* __restrict__ coeffs,
                                                                LevelDims L, float* __restrict__ lsum,
                                                                float* __restrict__ cnt, int r0,
-                                                               int r1, int npx)
+                                                               int r1, int npx, int py0)
 {
-    __shared__ float sv[kPG];
+    __shared__ float sv[kTG];
     const unsigned lb = xcd_remap(blockIdx.x, gridDim.x);
-    const int X0 = (int)(lb % (unsigned)npx) * kPPW, Y0 = r0 + (int)(lb / (unsigned)npx) * kPPH;
+    const int px = (int)(lb % (unsigned)npx), py = py0 + (int)(lb / (unsigned)npx);
+    const int pid = py * npx + px;
+    const int X0 = px * kTPW, Y0 = L.h0 + py * kTPH;
     const int t = threadIdx.x;
-    const int X = X0 + (t & (kPPW - 1));
-    const int X1 = min(X0 + kPPW - 1, L.w - 1);
-    // band rows of the patch: Depth.cpp's targets exist on h0 < Y < h1 only
-    const int ya = max(Y0, L.h0 + 1), yb = min(min(Y0 + kPPH - 1, r1 - 1), L.h1 - 1);
-    float acc[kPPP], n[kPPP];
+    const int X = X0 + (t & (kTPW - 1));
+    const int X1 = min(X0 + kTPW - 1, L.w - 1);
+    // rows of the patch in [r0, r1) where Depth.cpp has targets (h0 < Y < h1)
+    const int ya = max(max(Y0, r0), L.h0 + 1), yb = min(min(Y0 + kTPH - 1, r1 - 1), L.h1 - 1);
+    float acc[kTPP], n[kTPP];
 #pragma unroll
-    for (int j = 0; j < kPPP; j++) acc[j] = n[j] = 0.0f;
-    for (int p = t0; ya <= yb && p < t1; p++) {
+    for (int j = 0; j < kTPP; j++) acc[j] = n[j] = 0.0f;
+    auto tile = [&](const int p) {
         const TileBox bx = box[p];
-        if (!box_meets(bx, X0, X1, ya, yb)) continue;  // block-uniform
         const TapBox B = tb[p];
         const float* tv = tiles + geom[p].off;
         float4 k = make_float4(0.f, 0.f, 0.f, 0.f);
         if constexpr (XFORM) k = *reinterpret_cast<const float4*>(coeffs + (long long)p * 4);
-        for (int g = t; g < kPG; g += 256) {
-            const int gx = X0 - 1 + g % kPGW - B.xmin, gy = Y0 - 1 + g / kPGW - B.ymin;
+        for (int g = t; g < kTG; g += 256) {
+            const int gx = X0 - 1 + g % kTGW - B.xmin, gy = Y0 - 1 + g / kTGW - B.ymin;
             if (gx < 0 || gx >= B.nx || gy < 0 || gy >= B.ny) continue;
             float x = tv[map[B.off + (long long)gy * B.nx + gx]];
             if constexpr (XFORM) x = cubic_map(x, k.x, k.y, k.z, k.w);
@@ -437,48 +443,76 @@ __global__ void __launch_bounds__(256) k_targets_patch_partial(const TileGeom* _
         }
         __syncthreads();
 #pragma unroll
-        for (int j = 0; j < kPPP; j++) {
-            const int r = t / kPPW + j * (256 / kPPW);
+        for (int j = 0; j < kTPP; j++) {
+            const int r = t / kTPW + j * (256 / kTPW);
             const int Y = Y0 + r;
             if (X <= X1 && Y >= ya && Y <= yb && in_box2(bx, X, Y)) {
-                const int c = (r + 1) * kPGW + (t & (kPPW - 1)) + 1;
+                const int c = (r + 1) * kTGW + (t & (kTPW - 1)) + 1;
                 // taps in std::map key order: (X-1,Y), (X,Y-1), (X,Y), (X,Y+1), (X+1,Y)
                 float Lp = 0;
                 Lp += sv[c - 1] * -0.25f;
-                Lp += sv[c - kPGW] * -0.25f;
+                Lp += sv[c - kTGW] * -0.25f;
                 Lp += sv[c] * 1.0f;
-                Lp += sv[c + kPGW] * -0.25f;
+                Lp += sv[c + kTGW] * -0.25f;
                 Lp += sv[c + 1] * -0.25f;
                 acc[j] += Lp;
                 n[j] += 1.0f;
             }
         }
         __syncthreads();
+    };
+    if (ya <= yb && t0 < t1) {
+        for (int w = t0 >> 5; w <= (t1 - 1) >> 5; w++) {
+            const int lo = max(t0 - 32 * w, 0), hi = min(t1 - 32 * w, 32);
+            const uint32_t range = (hi >= 32 ? 0xFFFFFFFFu : ((1u << hi) - 1u)) & ~((1u << lo) - 1u);
+            uint32_t m = tmask[(long long)pid * nmw + w] & range;  // block-uniform
+            while (m) {
+                tile(w * 32 + __builtin_ctz(m));
+                m &= m - 1;
+            }
+        }
     }
 #pragma unroll
-    for (int j = 0; j < kPPP; j++) {
-        const int Y = Y0 + t / kPPW + j * (256 / kPPW);
-        if (X > X1 || Y >= r1) continue;
+    for (int j = 0; j < kTPP; j++) {
+        const int Y = Y0 + t / kTPW + j * (256 / kTPW);
+        if (X > X1 || Y < r0 || Y >= r1 || Y > L.h1) continue;
         const long long o = (long long)Y * L.w + X;
         lsum[o] = acc[j];
         cnt[o] = n[j];
     }
 }
 
-void launch_targets_map_partial(hipStream_t s, const TileGeom* geom, const TileBox* box,
-                                const TapBox* tb, int t0, int t1, const int32_t* map,
-                                const float* tiles, const float* coeffs, LevelDims L, float* lsum,
-                                float* cnt, int r0, int r1)
+hipError_t launch_targets_map_partial(hipStream_t s, const TileGeom* geom, const TileBox* box,
+                                const TapBox* tb, const uint32_t* tmask, int nmw, int t0, int t1,
+                                const int32_t* map, const float* tiles, const float* coeffs,
+                                LevelDims L, float* lsum, float* cnt, int r0, int r1)
 {
-    if (r1 <= r0 || L.w <= 0) return;
-    const int npx = (L.w + kPPW - 1) / kPPW, npy = (r1 - r0 + kPPH - 1) / kPPH;
-    const unsigned g = (unsigned)npx * (unsigned)npy;
+    if (r1 <= r0 || L.w <= 0) return hipSuccess;
+    // rows of [r0, r1) outside the band [h0, h1]: no targets (zero sums and counts)
+    const size_t rowb = sizeof(float) * (size_t)L.w;
+    const int za = r0, zb = min(r1, L.h0);
+    hipError_t e = hipSuccess;
+    if (zb > za) {
+        if (e == hipSuccess) e = hipMemsetAsync(lsum + (size_t)za * L.w, 0, rowb * (zb - za), s);
+        if (e == hipSuccess) e = hipMemsetAsync(cnt + (size_t)za * L.w, 0, rowb * (zb - za), s);
+    }
+    const int wa = max(r0, L.h1 + 1), wb = r1;
+    if (wb > wa) {
+        if (e == hipSuccess) e = hipMemsetAsync(lsum + (size_t)wa * L.w, 0, rowb * (wb - wa), s);
+        if (e == hipSuccess) e = hipMemsetAsync(cnt + (size_t)wa * L.w, 0, rowb * (wb - wa), s);
+    }
+    const int ba = max(r0, L.h0), bb = min(r1, L.h1 + 1);  // band rows of the range
+    if (e != hipSuccess || bb <= ba) return e;
+    const int npx = (L.w + kTPW - 1) / kTPW;
+    const int py0 = (ba - L.h0) / kTPH, py1 = (bb - 1 - L.h0) / kTPH;
+    const unsigned g = (unsigned)npx * (unsigned)(py1 - py0 + 1);
     if (coeffs)
         hipLaunchKernelGGL(k_targets_patch_partial<true>, dim3(g), dim3(256), 0, s, geom, box, tb,
-                           t0, t1, map, tiles, coeffs, L, lsum, cnt, r0, r1, npx);
+                           tmask, nmw, t0, t1, map, tiles, coeffs, L, lsum, cnt, r0, r1, npx, py0);
     else
         hipLaunchKernelGGL(k_targets_patch_partial<false>, dim3(g), dim3(256), 0, s, geom, box, tb,
-                           t0, t1, map, tiles, coeffs, L, lsum, cnt, r0, r1, npx);
+                           tmask, nmw, t0, t1, map, tiles, coeffs, L, lsum, cnt, r0, r1, npx, py0);
+    return hipGetLastError();
 }
 
 void launch_targets_map(hipStream_t s, const TileGeom* geom, const TileBox* box,
