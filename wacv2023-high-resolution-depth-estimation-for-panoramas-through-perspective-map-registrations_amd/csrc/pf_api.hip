@@ -1081,8 +1081,10 @@ static JresPlan jres_plan(pf_ctx* c, const LevelDims& L, int batch, bool fast)
     if (mode == 0 || !fast || batch < 1) return jp;
     const int rows = jres_region_rows(L.w);  // region rows of one workgroup
     if (rows <= 0 || L.iters < 1) return jp;
-    static int bpc = -1;
-    if (bpc < 0) bpc = jres_blocks_per_cu(512);
+    static int bpc_w[3] = {-1, -1, -1};  // resident blocks per CU at widths 256, 512, 1024
+    const int wi = L.w == 256 ? 0 : (L.w == 512 ? 1 : 2);
+    if (bpc_w[wi] < 0) bpc_w[wi] = jres_blocks_per_cu(L.w);
+    const int bpc = bpc_w[wi];
     if (bpc < 1) return jp;
     const int band = L.h1 - L.h0 + 1;
     // cost in sweep units: the blocks run in ceil(blocks / resident) rounds of residency, each
@@ -1109,6 +1111,11 @@ static JresPlan jres_plan(pf_ctx* c, const LevelDims& L, int batch, bool fast)
         const int rounds = (L.iters + K - 1) / K;
         const long long resident = (long long)c->num_cu * bpc;
         const long long waves = ((long long)batch * nb + resident - 1) / resident;
+        // 1024 wide (one workgroup per CU, two waves per SIMD): only where every block of the
+        // launch is resident at once -- the latency-bound one-panorama levels (C5); at C3's batch
+        // its passes are not measured against the streaming engine's (PF_JRES1024_ANY=1: allow)
+        static const bool any1024 = getenv("PF_JRES1024_ANY") && atoi(getenv("PF_JRES1024_ANY"));
+        if (L.w == 1024 && waves > 1 && !any1024) continue;
         const double cost = (double)waves * (L.iters + (rounds - 1) * xcost);
         if (cost < best) {
             best = cost;

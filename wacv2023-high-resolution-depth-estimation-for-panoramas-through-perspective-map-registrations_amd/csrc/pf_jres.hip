@@ -634,8 +634,24 @@ int jres_words_per_value() { return PF_JRES_GRANULE ? 2 : 1; }
 int jres_flags_per_block(int K) { return PF_JRES_LDSFLAG ? 2 * K : 1; }
 static constexpr int kRS512 = 64 / kJW, kRS256 = 128 / kJW;
 
+// 1024-wide levels (round 5, off): 16 columns per lane, 8 waves of 4 rows (a 32-row region; the
+// LDS edge rows of 16 waves would need 256 KB, 8 waves need 128 KB: one workgroup per CU, two
+// waves per SIMD at 236 VGPRs, no spills).  Measured slower than the streaming passes: C5's one
+// call 2.42 ms against 2.16 (its 1024-wide level 0 at batch 1), and C3's batch-64 level 1
+// (PF_JRES1024_ANY=1) 14.2k against 16.7k panoramas/s (profiles/r05/jres1024.txt).
+#ifndef PF_JRES_1024
+#define PF_JRES_1024 0
+#endif
+static constexpr int kJW1024 = 8, kRS1024 = 4;
+
 // region rows of the resident kernel's workgroup at this width (0: not supported)
-int jres_region_rows(int w) { return w == 512 ? 64 : (w == 256 ? 128 : 0); }
+int jres_region_rows(int w)
+{
+    if (w == 512) return 64;
+    if (w == 256) return 128;
+    if (w == 1024 && PF_JRES_1024) return kJW1024 * kRS1024;
+    return 0;
+}
 int jres_threads() { return 64 * kJW; }
 
 void launch_jres(hipStream_t s, const JresArgs& A)
@@ -643,14 +659,25 @@ void launch_jres(hipStream_t s, const JresArgs& A)
     const int grid = A.nb * A.batch;
     if (A.w == 512) launch_cr<8, kRS512, kJW>(s, A, grid, A.src_mode, A.out != nullptr);
     else if (A.w == 256) launch_cr<4, kRS256, kJW>(s, A, grid, A.src_mode, A.out != nullptr);
+#if PF_JRES_1024
+    else if (A.w == 1024)
+        launch_cr<16, kRS1024, kJW1024>(s, A, grid, A.src_mode, A.out != nullptr);
+#endif
 }
 
 int jres_blocks_per_cu(int w)
 {
     int nb = 0;
-    const void* f = w == 256 ? reinterpret_cast<const void*>(k_jres<4, kRS256, kJW, 0, false>)
-                             : reinterpret_cast<const void*>(k_jres<8, kRS512, kJW, 0, false>);
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, f, 64 * kJW, 0) != hipSuccess) nb = 0;
+    const void* f = reinterpret_cast<const void*>(k_jres<8, kRS512, kJW, 0, false>);
+    int threads = 64 * kJW;
+    if (w == 256) f = reinterpret_cast<const void*>(k_jres<4, kRS256, kJW, 0, false>);
+#if PF_JRES_1024
+    if (w == 1024) {
+        f = reinterpret_cast<const void*>(k_jres<16, kRS1024, kJW1024, 0, false>);
+        threads = 64 * kJW1024;
+    }
+#endif
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, f, threads, 0) != hipSuccess) nb = 0;
     return nb;
 }
 
