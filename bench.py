@@ -961,7 +961,7 @@ def main():
             "per_rank": per_rank if world > 1 else None,
             "sample_pano": per_rank[0]["sample"],
         }
-        if not args.no_cpu_baseline:
+        if not args.no_cpu_baseline and world == 1:  # the contract: rank 0 at N = 1 only
             line["cpu_baseline"] = cpu_baseline(args.cpu_seconds)
         print(json.dumps(line), flush=True)
     if world > 1:
