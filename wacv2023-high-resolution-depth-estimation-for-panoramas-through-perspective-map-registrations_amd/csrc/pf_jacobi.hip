@@ -56,6 +56,22 @@
 // with the levels they do not need compiled out (JLag::fill_from); 0 = off, -1 = per depth
 #define PF_JFILL -1
 #endif
+#ifndef PF_JDRAIN
+// the last PF_JDRAIN 6-step groups of a row chunk with the idle shallow levels compiled out (the
+// last group alone holds 39 of the 45 idle level-steps at T = 10); 0 = off
+#define PF_JDRAIN 1
+#endif
+#ifndef PF_JLAG_WAVES_FAST
+// the packed passes: 3 waves per SIMD (<= 168 VGPRs).  With the drain compiled out (PF_JDRAIN)
+// hipcc's free allocation lands at 168-171 (checked in the ISA); the bound holds it at 168
+#define PF_JLAG_WAVES_FAST 3
+#endif
+#ifndef PF_JDRAIN_BIN
+#define PF_JDRAIN_BIN 0
+#endif
+#ifndef PF_JDRAIN_ROT
+#define PF_JDRAIN_ROT 1  // the drain as one copy after rotating the L ring to its group
+#endif
 #ifndef PF_JPIPE_FILL
 #define PF_JPIPE_FILL 3  // fill groups of the pipelined engine (PF_JFILL = -1)
 #endif
@@ -505,32 +521,34 @@ struct JLag {
     // skipped with one wave-uniform branch -- its ring slots then hold stale rows, read only by
     // unneeded updates.  At the default depths this drops 10-30% of the issued updates (the
     // lagged start fills T levels over 3T steps, the drain empties them over T).
-    // NA: levels 1..NA are computed this step (the rest are idle in the chunk's fill, below)
-    template <int PH, int GB, int T0, bool ROWS, int NA>
+    // levels LA..NA are computed this step (the rest are idle: NA < T in the chunk's fill,
+    // LA > 1 in its drain, below)
+    template <int PH, int GB, int T0, bool ROWS, int NA, int LA = 1>
     __device__ __forceinline__ void sweep_packed(Row<C>* nw, int k) const
     {
         constexpr int T1 = T0 + PF_JPK_GROUP < T ? T0 + PF_JPK_GROUP : T;
         // the groups run from the deepest level down: level t+1 reads the oldest row of level
         // t's ring before level t overwrites it, so the new row can take that row's registers
         // (all reads of a step are rows of earlier steps, so the order is free)
-        if constexpr (T1 < T) sweep_packed<PH, GB, T1, ROWS, NA>(nw, k);
+        if constexpr (T1 < T) sweep_packed<PH, GB, T1, ROWS, NA, LA>(nw, k);
         constexpr int TB = T1 < NA ? T1 : NA;
-        if constexpr (T0 < TB)
+        constexpr int TA = T0 > LA - 1 ? T0 : LA - 1;  // levels TA+1 .. TB
+        if constexpr (TA < TB)
 #if PF_JGATE
         if (k - kr0 >= 3 * (T0 + 1) && k - kr1 < T1)
 #endif
         {
-            Row<C> Lv[TB - T0];
-            ring_get_range<GB, PH, T0 + 1, TB>(Lv);
-            if constexpr (C == 4) sweep_packed_group4<PH, T0, TB, ROWS>(Lv, nw, k);
-            else sweep_packed_group<PH, T0, TB, ROWS>(Lv, nw, k);
+            Row<C> Lv[TB - TA];
+            ring_get_range<GB, PH, TA + 1, TB>(Lv);
+            if constexpr (C == 4) sweep_packed_group4<PH, TA, TB, ROWS>(Lv, nw, k);
+            else sweep_packed_group<PH, TA, TB, ROWS>(Lv, nw, k);
         }
     }
 
     // Step k = (group base) + PH; GB = (group base - k0) mod R: ring slots count from the
     // chunk's first step, so they are compile-time constants without aligning k0.  NA < T only
     // in the fill (fill_from).
-    template <int PH, bool ROWS, int GB, int NA = T>
+    template <int PH, bool ROWS, int GB, int NA = T, int LA = 1>
     __device__ __forceinline__ void step(int k)
     {
         // level-0 row k-1 (loaded last step) joins the ring
@@ -548,16 +566,16 @@ struct JLag {
 #endif
         Row<C> nw[T];
         if constexpr (FAST) {
-            sweep_packed<PH, GB, 0, ROWS, NA>(nw, k);
+            sweep_packed<PH, GB, 0, ROWS, NA, LA>(nw, k);
         } else {
-            static_assert(NA == T, "the general form has no fill specialisation");
+            static_assert(NA == T && LA == 1, "the general form has no fill / drain specialisation");
             Row<C> Lv[T];
             ring_get_range<GB, PH, 1, T>(Lv);
             sweep_general<PH>(Lv, nw);
         }
 #pragma unroll
         for (int t = 1; t < T; t++)
-            if (t <= NA) H[t][slot(PH, 2 * t)] = nw[t - 1];  // an idle level keeps its rows
+            if (t >= LA && t <= NA) H[t][slot(PH, 2 * t)] = nw[t - 1];  // idle: keeps its rows
         if constexpr (NA < T) return;  // no stored row before every level runs (fill_from)
         const int j = k - 2 * T;  // final-level row finished this step
         // xs0, vlo, vhi and C are even, so a lane's columns are all inside [vlo, vhi) or all
@@ -648,22 +666,95 @@ struct JLag {
             return true;
         }
     }
-    // the step loop from the chunk's first step k0 (ring group 0): the fill, the rest of its
-    // ring period, then whole periods
+    // The chunk's drain, likewise: level t is last needed at step kend - 1 - (T - t), so in the
+    // last T steps the shallow levels go idle one by one.  The last ND groups run as their own
+    // steps with levels 1 .. la(p) - 1 compiled out, p = the step within those groups.  The
+    // chunk's step count kend - k0 is not a multiple of 6: the groups end o = 0..5 steps past
+    // kend, and la() assumes o = 0, the largest active set (a few idle level-steps remain when
+    // o > 0; nothing needed is skipped).  The drain starts at a run-time ring group, hence one
+    // copy per group of the ring period (drain_switch).
+    static constexpr int ND_ALL = (T + 5) / 6;  // groups with an idle level (o = 0)
+    static constexpr int ND = !(PF_JDRAIN && FAST) ? 0 : (PF_JDRAIN < ND_ALL ? PF_JDRAIN : ND_ALL);
+    static constexpr int la(int p)
+    {
+        const int a = T - 6 * ND + p + 1;
+        return a < 1 ? 1 : a;
+    }
+    template <bool ROWS, int G0, int I>
+    __device__ __forceinline__ void drain_from(int& k)
+    {
+        if constexpr (I < ND) {
+            constexpr int GB = 6 * ((G0 + I) % NG);
+            step<0, ROWS, GB, T, la(6 * I + 0)>(k);
+            step<1, ROWS, GB, T, la(6 * I + 1)>(k + 1);
+            step<2, ROWS, GB, T, la(6 * I + 2)>(k + 2);
+            step<3, ROWS, GB, T, la(6 * I + 3)>(k + 3);
+            step<4, ROWS, GB, T, la(6 * I + 4)>(k + 4);
+            step<5, ROWS, GB, T, la(6 * I + 5)>(k + 5);
+            k += 6;
+            drain_from<ROWS, G0, I + 1>(k);
+        }
+    }
+    // the drain code is written for ring group 0: the L ring (registers) is rotated so that the
+    // drain's first group sits at slot 0 (a register permutation once per chunk), instead of one
+    // copy of the drain per ring group (which took the T = 10 pass from 166 to 214 VGPRs)
+    template <int SH>
+    __device__ __forceinline__ void ring_rotate()
+    {
+        Row<C> t[R];
+#pragma unroll
+        for (int x = 0; x < R; x++) t[x] = Lr[(x + SH) % R];
+#pragma unroll
+        for (int x = 0; x < R; x++) Lr[x] = t[x];
+    }
+    template <int G>
+    __device__ __forceinline__ void ring_to_zero(int g)
+    {
+#if PF_JDRAIN_BIN
+        // by binary parts of g: a rotation by 6 groups' worth of slots per set bit
+        if constexpr (G == 1) {
+            if (g & 1) ring_rotate<6>();
+            if constexpr (NG > 2) { if (g & 2) ring_rotate<12 % R>(); }
+        }
+#else
+        if constexpr (G < NG) {
+            if (g == G) ring_rotate<6 * G>();
+            else ring_to_zero<G + 1>(g);
+        }
+#endif
+    }
+    template <bool ROWS, int G>
+    __device__ __forceinline__ void drain_switch(int g, int& k)
+    {
+        if constexpr (LREG && PF_JDRAIN_ROT) {
+            if constexpr (NG > 1) ring_to_zero<1>(g);
+            drain_from<ROWS, 0, 0>(k);
+        } else if constexpr (G < NG) {
+            if (g == G) drain_from<ROWS, G, 0>(k);
+            else drain_switch<ROWS, G + 1>(g, k);
+        }
+    }
+    // the step loop from the chunk's first step k0 (ring group 0): the fill, whole groups up to
+    // the drain (or to the end, for a chunk too short for both), the drain
     template <bool ROWS>
     __device__ __forceinline__ void run(int k0, int kend)
     {
         int k = k0;
-        bool more = fill_from<ROWS, 0>(k, kend);
-        if constexpr (NF % NG != 0) {
-            if (more) more = groups_from<ROWS, NF % NG>(k, kend);
+        const int gt = (kend - k0 + 5) / 6;  // groups of the chunk
+        const bool dr = ND > 0 && gt >= NF + ND;
+        if (!fill_from<ROWS, 0>(k, kend)) return;
+        const int kd = dr ? k0 + 6 * (gt - ND) : kend;
+        if (k < kd) {
+            bool more = true;
+            if constexpr (NF % NG != 0) more = groups_from<ROWS, NF % NG>(k, kd);
+            while (more) more = groups_from<ROWS, 0>(k, kd);
         }
-        while (more) more = groups_from<ROWS, 0>(k, kend);
+        if (dr) drain_switch<ROWS, 0>(__builtin_amdgcn_readfirstlane((gt - ND) % NG), k);
     }
 };
 
 template <int C, int T, int SRC, bool OUT16, bool FAST>
-__global__ void __launch_bounds__(256, PF_JLAG_WAVES) k_jlag(JacobiPass P)
+__global__ void __launch_bounds__(256, FAST ? PF_JLAG_WAVES_FAST : PF_JLAG_WAVES) k_jlag(JacobiPass P)
 {
     using S_t = JLag<C, T, SRC, OUT16, FAST>;
     const int lane = threadIdx.x & 63;
