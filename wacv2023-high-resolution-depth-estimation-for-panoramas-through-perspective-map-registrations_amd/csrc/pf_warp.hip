@@ -1260,31 +1260,13 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) k
         return;
     }
 
-    // staging: thread t owns units t and t + 256 of the patch's footprint (units past it reload
-    // its first unit, so every load is issued unconditionally).  LDS holds the u8 rows as they
-    // are (one 16-B store per unit, consecutive lanes on consecutive 16 B: no bank conflicts);
-    // a pixel's corner pair is the 6 bytes at its byte offset a, read as the 3 dwords from
-    // a & ~3 and aligned with v_alignbyte (round 5: the fp32-widened box of the first version
-    // spent 70 % of its LDS cycles in bank conflicts, SQ_LDS_BANK_CONFLICT, profiles/r05/rgb)
-    constexpr int NU = kRgbUnits / 256;
-    uint32_t goff[NU];
-#pragma unroll
-    for (int u = 0; u < NU; u++) {
-        const int e = t + 256 * u;
-        goff[u] = unit_tbl[(long long)pid * kRgbUnits + (e < P.units ? e : 0)];
-    }
-    u4v stg[2][NU];
-    auto fetch = [&](int sl, int q) {
-        const auto pr = rsrc(pano + (long long)(bbeg + (q < nb ? q : nb - 1)) * pstride, pbytes);
-#pragma unroll
-        for (int u = 0; u < NU; u++)
-            stg[sl][u] = __builtin_amdgcn_raw_buffer_load_b128(pr, (int)goff[u], 0, 0);
-    };
-    auto put = [&](int pa, const u4v* v) {
-#pragma unroll
-        for (int u = 0; u < NU; u++)
-            *reinterpret_cast<u4v*>(boxw + pa * (kRgbCap / 4) + 4 * (t + 256 * u)) = v[u];
-    };
+    // staging: thread t owns units t (and t + 256 when the footprint has more than 256 units: NU
+    // = 2, a block-uniform choice) of the patch's footprint; units past it reload its first unit,
+    // so every load is issued unconditionally.  LDS holds the u8 rows as they are (one 16-B
+    // store per unit, consecutive lanes on consecutive 16 B: no bank conflicts); a pixel's
+    // corner pair is the 6 bytes at its byte offset a, read as the 3 dwords from a & ~3 and
+    // aligned with v_alignbyte (round 5: the fp32-widened box of the first version spent 70 % of
+    // its LDS cycles in bank conflicts, SQ_LDS_BANK_CONFLICT, profiles/r05/rgb)
     // the 6 bytes R0 G0 B0 R1 G1 B1 at byte offset a of parity L, as floats into c[0..5]: the
     // three dwords from a & ~3 (the lanes of a tile row 3 dwords apart: an odd stride over the
     // banks), aligned with v_alignbyte (two 8-B reads from a & ~7 measured slower, 0.71 ms)
@@ -1300,27 +1282,52 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) k
         c[4] = (float)(hi & 0xFFu);
         c[5] = (float)((hi >> 8) & 0xFFu);
     };
-    auto iter = [&](auto parity, int q) {
-        constexpr int PA = decltype(parity)::value;
-        fetch(PA, q + 2);  // stg[PA] held panorama q, put into parity PA last iteration
-        const uint32_t* L = boxw + PA * (kRgbCap / 4);
-        blend_store([&](int k, float* c) {
-            pair6(L, la[k] & 0xFFFFu, c);
-            pair6(L, la[k] >> 16, c + 6);
-        }, tiles + (long long)(bbeg + q) * tstride);
-        put(1 - PA, stg[1 - PA]);  // panorama q+1 (a duplicate past the chunk: unread)
+    auto staged = [&](auto nu) {
+        constexpr int NU = decltype(nu)::value;
+        uint32_t goff[NU];
+#pragma unroll
+        for (int u = 0; u < NU; u++) {
+            const int e = t + 256 * u;
+            goff[u] = unit_tbl[(long long)pid * kRgbUnits + (e < P.units ? e : 0)];
+        }
+        u4v stg[2][NU];
+        auto fetch = [&](int sl, int q) {
+            const auto pr = rsrc(pano + (long long)(bbeg + (q < nb ? q : nb - 1)) * pstride,
+                                 pbytes);
+#pragma unroll
+            for (int u = 0; u < NU; u++)
+                stg[sl][u] = __builtin_amdgcn_raw_buffer_load_b128(pr, (int)goff[u], 0, 0);
+        };
+        auto put = [&](int pa, const u4v* v) {
+#pragma unroll
+            for (int u = 0; u < NU; u++)
+                *reinterpret_cast<u4v*>(boxw + pa * (kRgbCap / 4) + 4 * (t + 256 * u)) = v[u];
+        };
+        auto iter = [&](auto parity, int q) {
+            constexpr int PA = decltype(parity)::value;
+            fetch(PA, q + 2);  // stg[PA] held panorama q, put into parity PA last iteration
+            const uint32_t* L = boxw + PA * (kRgbCap / 4);
+            blend_store([&](int k, float* c) {
+                pair6(L, la[k] & 0xFFFFu, c);
+                pair6(L, la[k] >> 16, c + 6);
+            }, tiles + (long long)(bbeg + q) * tstride);
+            put(1 - PA, stg[1 - PA]);  // panorama q+1 (a duplicate past the chunk: unread)
+            __syncthreads();
+        };
+        fetch(0, 0);
+        fetch(1, 1);
+        put(0, stg[0]);
         __syncthreads();
+        using I0 = std::integral_constant<int, 0>;
+        using I1 = std::integral_constant<int, 1>;
+        for (int q = 0; q < nb; q += 2) {
+            iter(I0{}, q);
+            if (q + 1 < nb) iter(I1{}, q + 1);
+        }
     };
-    fetch(0, 0);
-    fetch(1, 1);
-    put(0, stg[0]);
-    __syncthreads();
-    using I0 = std::integral_constant<int, 0>;
-    using I1 = std::integral_constant<int, 1>;
-    for (int q = 0; q < nb; q += 2) {
-        iter(I0{}, q);
-        if (q + 1 < nb) iter(I1{}, q + 1);
-    }
+    static_assert(kRgbUnits <= 512, "two units per thread at most");
+    if (P.units <= 256) staged(std::integral_constant<int, 1>{});  // block-uniform
+    else staged(std::integral_constant<int, 2>{});
 }
 
 void launch_warp_rgb_box(hipStream_t s, const TileGeom* geom, const RgbPatch* patches,
