@@ -1071,6 +1071,7 @@ static int seed_tables(pf_ctx* c, const LevelDims& L, int ew, int eh, int ec)
 struct JresPlan {
     bool on = false;
     int nb = 0, core = 0, K = 0, rounds = 0;
+    bool half = false;  // half-height regions (jres_region_rows)
 };
 
 static JresPlan jres_plan(pf_ctx* c, const LevelDims& L, int batch, bool fast)
@@ -1093,37 +1094,47 @@ static JresPlan jres_plan(pf_ctx* c, const LevelDims& L, int batch, bool fast)
     static const double xcost = getenv("PF_JRES_X") ? atof(getenv("PF_JRES_X")) : 2.5;
     static const int nb_env = getenv("PF_JRES_NB") ? atoi(getenv("PF_JRES_NB")) : 0;
     const int nb_force = c->jres_nb > 0 ? c->jres_nb : nb_env;
+    // a sweep of the half-height region costs each wave ~half the updates, plus the fixed
+    // barrier / edge exchange (PF_JRES_HALFCOST: its cost in full-region sweeps)
+    static const double hcost = getenv("PF_JRES_HALFCOST") ? atof(getenv("PF_JRES_HALFCOST")) : 0.6;
     double best = 1e300;
-    for (int nb = 1; nb <= band && nb <= 64; nb++) {
-        if (nb_force > 0 && nb != nb_force) continue;
-        const int core = (band + nb - 1) / nb;
-        if ((band + core - 1) / core != nb) continue;
-        int K;
-        if (nb == 1) {
-            if (core > rows) continue;
-            K = L.iters;
-        } else {
-            K = (rows - core) / 2;
-            if (K > core) K = core;
-            if (K > L.iters) K = L.iters;
-            if (K < 1) continue;
-        }
-        const int rounds = (L.iters + K - 1) / K;
-        const long long resident = (long long)c->num_cu * bpc;
-        const long long waves = ((long long)batch * nb + resident - 1) / resident;
-        // 1024 wide (one workgroup per CU, two waves per SIMD): only where every block of the
-        // launch is resident at once -- the latency-bound one-panorama levels (C5); at C3's batch
-        // its passes are not measured against the streaming engine's (PF_JRES1024_ANY=1: allow)
-        static const bool any1024 = getenv("PF_JRES1024_ANY") && atoi(getenv("PF_JRES1024_ANY"));
-        if (L.w == 1024 && waves > 1 && !any1024) continue;
-        const double cost = (double)waves * (L.iters + (rounds - 1) * xcost);
-        if (cost < best) {
-            best = cost;
-            jp.on = true;
-            jp.nb = nb;
-            jp.core = core;
-            jp.K = K;
-            jp.rounds = rounds;
+    for (int hv = 0; hv < 2; hv++) {
+        const int rows_h = hv ? jres_region_rows(L.w, true) : rows;
+        if (rows_h <= 0) continue;
+        const double sweep = hv ? hcost : 1.0;
+        for (int nb = 1; nb <= band && nb <= 64; nb++) {
+            if (nb_force > 0 && nb != nb_force) continue;
+            const int core = (band + nb - 1) / nb;
+            if ((band + core - 1) / core != nb) continue;
+            int K;
+            if (nb == 1) {
+                if (core > rows_h) continue;
+                K = L.iters;
+            } else {
+                K = (rows_h - core) / 2;
+                if (K > core) K = core;
+                if (K > L.iters) K = L.iters;
+                if (K < 1) continue;
+            }
+            const int rounds = (L.iters + K - 1) / K;
+            const long long resident = (long long)c->num_cu * bpc;
+            const long long waves = ((long long)batch * nb + resident - 1) / resident;
+            // 1024 wide (one workgroup per CU, two waves per SIMD): only where every block of
+            // the launch is resident at once -- the latency-bound one-panorama levels (C5); at
+            // C3's batch its passes are not measured against the streaming engine's
+            // (PF_JRES1024_ANY=1: allow)
+            static const bool any1024 = getenv("PF_JRES1024_ANY") && atoi(getenv("PF_JRES1024_ANY"));
+            if (L.w == 1024 && waves > 1 && !any1024) continue;
+            const double cost = (double)waves * (L.iters * sweep + (rounds - 1) * xcost);
+            if (cost < best) {
+                best = cost;
+                jp.on = true;
+                jp.nb = nb;
+                jp.core = core;
+                jp.K = K;
+                jp.rounds = rounds;
+                jp.half = hv == 1;
+            }
         }
     }
     return jp;
@@ -1174,7 +1185,7 @@ static float* run_jacobi(pf_ctx* c, const LevelDims& L, int first, const float* 
         A.dst = dst; A.dstride = st;
         A.out = out; A.ostride = ostride;
         A.w = L.w; A.h = L.h; A.h0 = L.h0; A.h1 = L.h1; A.iters = L.iters; A.batch = batch;
-        A.nb = jp->nb; A.core = jp->core; A.K = jp->K;
+        A.nb = jp->nb; A.core = jp->core; A.K = jp->K; A.half = jp->half ? 1 : 0;
         uint32_t* sync = (uint32_t*)c->jres_sync.p;
         A.xbuf = (float*)c->jres_x.p;
         A.ticket = sync;

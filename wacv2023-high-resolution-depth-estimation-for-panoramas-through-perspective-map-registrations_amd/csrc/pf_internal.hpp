@@ -223,6 +223,7 @@ struct JresArgs {
     uint16_t* out; long long ostride;       // non-null: store the u16 quantisation instead
     int w, h, h0, h1, iters, batch, src_mode;
     int nb, core, K;       // row blocks per panorama, core rows per block, sweeps per round
+    int half;              // 1: the half-height region (rows per wave halved; jres_region_rows)
     float* xbuf;           // hand-off rows [batch][nb][2 parity][2 edge][K][w]
     uint32_t* flags;       // [batch][nb] last round published (monotone across launches)
     uint32_t* ticket;      // workgroup ticket counter (monotone across launches)
@@ -233,7 +234,7 @@ struct JresArgs {
                            // barriers; 16 (pf_debug_jres_fault): row block 0 withholds its flag
     int spin_log2;         // a hand-off wait gives up (and counts into err) after 2^spin_log2 polls
 };
-int jres_region_rows(int w);
+int jres_region_rows(int w, bool half = false);  // 0: not supported
 int jres_threads();
 int jres_words_per_value();
 int jres_flags_per_block(int K);  // 2: the hand-off rows travel as {value, tag} granules

@@ -644,9 +644,19 @@ static constexpr int kRS512 = 64 / kJW, kRS256 = 128 / kJW;
 #endif
 static constexpr int kJW1024 = 8, kRS1024 = 4;
 
+// Half-height regions (round 5): the same workgroup with half the rows per wave (512 wide: 2
+// rows, a 32-row region).  A sweep then costs each wave half the updates, which is what a
+// launch whose blocks are all resident at once waits for (one panorama: C2's level 0 is 200
+// sequential sweeps); a full batch wants the taller region (fewer redundant halo rows per core
+// row).  jres_plan weighs both.
+#ifndef PF_JRES_HALF
+#define PF_JRES_HALF 1
+#endif
+
 // region rows of the resident kernel's workgroup at this width (0: not supported)
-int jres_region_rows(int w)
+int jres_region_rows(int w, bool half)
 {
+    if (half) return (PF_JRES_HALF && w == 512) ? 32 : 0;
     if (w == 512) return 64;
     if (w == 256) return 128;
     if (w == 1024 && PF_JRES_1024) return kJW1024 * kRS1024;
@@ -657,6 +667,10 @@ int jres_threads() { return 64 * kJW; }
 void launch_jres(hipStream_t s, const JresArgs& A)
 {
     const int grid = A.nb * A.batch;
+#if PF_JRES_HALF
+    if (A.w == 512 && A.half) launch_cr<8, kRS512 / 2, kJW>(s, A, grid, A.src_mode, A.out != nullptr);
+    else
+#endif
     if (A.w == 512) launch_cr<8, kRS512, kJW>(s, A, grid, A.src_mode, A.out != nullptr);
     else if (A.w == 256) launch_cr<4, kRS256, kJW>(s, A, grid, A.src_mode, A.out != nullptr);
 #if PF_JRES_1024
