@@ -461,6 +461,16 @@ struct WarpLanes {  // one thread's kLPx pixels, all panorama-invariant
 // last one), so the loads for panorama q+2 go out before panorama q is interpolated and the wait
 // for panorama q+1's loads -- an in-order vmcnt -- never covers them.  A thread's four pixels
 // are consecutive in one tile row: one 16-B store per panorama when they are all inside.
+#ifndef PF_WARP_MASKU
+// 1: staging slots past a patch's footprint issue no load (exec-masked lanes) instead of
+// reloading a valid unit.  Measured (round 5, two alternating rounds, serial C3 steps): the
+// depth warp 0.510-0.516 ms against 0.501-0.502 unmasked; the RGB warp 0.668 ms against
+// 0.594-0.610 (the masks push it to 15 spilled VGPRs).  Off.
+#define PF_WARP_MASKU 0
+#endif
+#ifndef PF_RGB_MASKU
+#define PF_RGB_MASKU 0  // the same in the RGB warp
+#endif
 typedef uint32_t u4v __attribute__((ext_vector_type(4)));
 #if !PF_WARP_WAVEBOX  // the block form (default)
 template <int NS, bool RESP, bool V4, bool RAG = false>
@@ -476,9 +486,11 @@ __device__ __forceinline__ void warp_staged(float* box, float* xbuf, const RespK
     constexpr int U = V4 ? 4 : 1;  // floats per staging unit
     const int bw2 = 2 * P.bw, bwu = RAG ? 1 : P.bw / U, units = RAG ? P.units : bwu * P.bh;
     uint32_t goff[NS];  // unit e = t + 256*s of the box -> panorama byte offset
+    bool live[NS];      // PF_WARP_MASKU: slots past the box load nothing (exec-masked lanes)
 #pragma unroll
     for (int s = 0; s < NS; s++) {
         int e = t + s * kWB;
+        live[s] = e < units;
         e = e < units ? e : units - 1;
         if constexpr (RAG) {
             goff[s] = unit_tbl[P.uoff + e];
@@ -501,9 +513,11 @@ __device__ __forceinline__ void warp_staged(float* box, float* xbuf, const RespK
             if constexpr (PF_WARP_DIAG == 2) {
                 for (int j = 0; j < U; j++) dst[s][j] = (float)(goff[s] & 1023u) * 1e-3f;
             } else if constexpr (V4) {
-                const u4v v = __builtin_amdgcn_raw_buffer_load_b128(pr, (int)goff[s], 0, 0);
+                if (!PF_WARP_MASKU || live[s]) {
+                    const u4v v = __builtin_amdgcn_raw_buffer_load_b128(pr, (int)goff[s], 0, 0);
 #pragma unroll
-                for (int j = 0; j < 4; j++) dst[s][j] = __uint_as_float(v[j]);
+                    for (int j = 0; j < 4; j++) dst[s][j] = __uint_as_float(v[j]);
+                }
             } else {
                 dst[s][0] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(pr, (int)goff[s], 0, 0));
             }
@@ -1291,12 +1305,16 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) k
             goff[u] = unit_tbl[(long long)pid * kRgbUnits + (e < P.units ? e : 0)];
         }
         u4v stg[2][NU];
+        bool live[NU];  // PF_RGB_MASKU: units past the footprint load nothing
+#pragma unroll
+        for (int u = 0; u < NU; u++) live[u] = t + 256 * u < P.units;
         auto fetch = [&](int sl, int q) {
             const auto pr = rsrc(pano + (long long)(bbeg + (q < nb ? q : nb - 1)) * pstride,
                                  pbytes);
 #pragma unroll
             for (int u = 0; u < NU; u++)
-                stg[sl][u] = __builtin_amdgcn_raw_buffer_load_b128(pr, (int)goff[u], 0, 0);
+                if (!PF_RGB_MASKU || live[u])
+                    stg[sl][u] = __builtin_amdgcn_raw_buffer_load_b128(pr, (int)goff[u], 0, 0);
         };
         auto put = [&](int pa, const u4v* v) {
 #pragma unroll
