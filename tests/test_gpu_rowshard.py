@@ -55,11 +55,13 @@ class ThreadComm:
                 self.all_reduce_sum(t)
 
             def exchange(self, sends, recvs):
+                # several messages per pair arrive in the order they were sent (as batched
+                # isend/irecv pairs match)
                 for peer, t in sends:
-                    outer.box[("x", r, peer)] = t.clone()
+                    outer.box.setdefault(("x", r, peer), []).append(t.clone())
                 outer.bar.wait()
                 for peer, t in recvs:
-                    t.copy_(outer.box[("x", peer, r)])
+                    t.copy_(outer.box[("x", peer, r)].pop(0))
                 outer.bar.wait()
 
             def broadcast(self, t, src):

@@ -126,7 +126,10 @@ def fuse_tile_sharded(backend, nlevels, ntiles, rank, world, comm=None):
 #    one boundary row its neighbour shares.  A rank computes its tiles' partial sums only on the
 #    rows it needs (its band + halo) and the rows it sends (pf_fuse_partial_rows); it sends each
 #    other rank the rows of that rank's band + halo where its tiles are non-zero -- in practice the
-#    K = T+1 halo rows to each neighbour -- and adds what it receives (pf_rows_add).  The coverage
+#    K = T+1 halo rows to each neighbour -- and adds what it receives (pf_rows_add).  The targets
+#    depend on the tiles alone, so the replicated levels' rows travel in one round and the
+#    row-sharded levels' in another (each group's multicover terms in one all-reduce).  The
+#    coverage
 #    count is layout-only, so every rank counts it itself, once per level and backend
 #    (pf_fuse_coverage_rows, coverage_plane): only fp32 sums travel, never counts.
 #  * Between levels: no broadcast of the bands.  The next level's first pass reads the 2x
@@ -321,8 +324,9 @@ def fuse_row_sharded(backend, nlevels, ntiles, rank, world, comm=None, log=None,
             backend._row_geo = geo
         except AttributeError:
             pass
+    # per-level geometry (plans agreed once per backend)
+    G = []
     for level in range(nlevels):
-        last = level == nlevels - 1
         # replicated: the whole level on this rank (at world 1, every level: the one-GPU path)
         rep = world == 1 or level < rep_levels
         w, h, h0, h1 = backend.dims(level)
@@ -347,41 +351,29 @@ def fuse_row_sharded(backend, nlevels, ntiles, rank, world, comm=None, log=None,
                 need = [(max(h0, bnd[d] - K), min(h1 + 1, bnd[d + 1] + K))
                         for d in range(world)]
             geo[key] = (plan, K, ext, bnd, need)
-        plan, K, ext, bounds, need = geo[key]
-        r0, r1 = (h0, h1 + 1) if rep else (bounds[rank], bounds[rank + 1])
-        e0, e1 = need[rank]
-        # the previous level's rows this rank's first pass / border read, from their owners
-        # (after a replicated level every rank holds all of them)
-        if level > 0 and world > 1 and pbounds is not None:
-            hp = backend.dims(level - 1)[1]
-            wp = backend.dims(level - 1)[0]
-            sends, recvs = [], []
-            mine = owned_rows(pbounds, hp, rank)
-            for d in range(world):
-                if d == rank:
-                    continue
-                sp = _span(prev_rows_needed(bounds, h0, h1, K, hp, d), mine)
-                if sp:
-                    sends.append((d, prev[sp[0] * wp:sp[1] * wp]))
-                rp = _span(prev_rows_needed(bounds, h0, h1, K, hp, rank),
-                           owned_rows(pbounds, hp, d))
-                if rp:
-                    recvs.append((d, prev[rp[0] * wp:rp[1] * wp]))
-            comm.exchange(sends, recvs)
-            if log:
-                log.add("prev_halo", sum(4 * t.numel() for _, t in sends))
-        if world == 1:  # nothing travels: the level's normalised targets from every tile
-            prev = backend.level(level, prev, backend.targets(level), None, last)
-            continue
-        # targets: this rank's tiles on the rows it needs and the rows it sends
-        lsum, cnt, lnorm = backend.plane(level), backend.plane(level), backend.plane(level)
-        mlo, mhi = ext[rank][0], ext[rank][1] + 1
-        lo, hi = (min(e0, mlo), max(e1, mhi)) if mlo < mhi else (e0, e1)
-        backend.partial_rows(level, t0, t1, lo, hi, lsum, cnt)  # rep: lo, hi = the whole band
-        if world > 1:
-            # every tile's coverage count (layout-only: counted once per backend and level)
-            cnt = backend.coverage_plane(level)
-            sends, recvs, bufs = [], [], []
+        G.append((rep, geo[key]))
+    if world == 1:  # nothing travels: each level's normalised targets from every tile
+        for level in range(nlevels):
+            prev = backend.level(level, prev, backend.targets(level), None,
+                                 level == nlevels - 1)
+        return G[-1][1][3]
+    # The targets depend on the tiles alone, so several levels' partial rows travel in ONE
+    # exchange round and their multicover terms in ONE all-reduce (per-level rounds would each be
+    # a latency on the critical path).  Two groups: the replicated levels, then the row-sharded
+    # ones -- the second group's host work is queued while the GPU sweeps the first.  A rank sums
+    # its tiles only on the rows it needs (its band + halo) and the rows it sends.
+    tgt = {}
+
+    def gather_targets(levels):
+        sends, recvs, bufs = [], [], []
+        for level in levels:
+            rep, (plan, K, ext, bounds, need) = G[level]
+            w = backend.dims(level)[0]
+            e0, e1 = need[rank]
+            lsum = backend.plane(level)
+            mlo, mhi = ext[rank][0], ext[rank][1] + 1
+            lo, hi = (min(e0, mlo), max(e1, mhi)) if mlo < mhi else (e0, e1)
+            backend.partial_rows(level, t0, t1, lo, hi, lsum, backend.plane(level))
             for d in range(world):
                 if d == rank:
                     continue
@@ -393,49 +385,93 @@ def fuse_row_sharded(backend, nlevels, ntiles, rank, world, comm=None, log=None,
                 if rp:
                     buf = backend.scratch((rp[1] - rp[0]) * w)
                     recvs.append((d, buf))
-                    bufs.append((rp, buf))
-            comm.exchange(sends, recvs)
+                    bufs.append((level, rp, buf))
+            # every tile's coverage count (layout-only: counted once per backend and level)
+            tgt[level] = (lsum, backend.coverage_plane(level))
+        comm.exchange(sends, recvs)  # level-major on both sides: the pairs match in order
+        if log:
+            log.add("targets", sum(4 * t.numel() for _, t in sends))
+        for level, (a, b), buf in bufs:  # one addend per covering tile: exact up to 2 (3+: below)
+            w = backend.dims(level)[0]
+            backend.rows_add(tgt[level][0][a * w:b * w], buf)
+        mcl = [lv for lv in levels if backend.multicover_count(lv)]
+        if mcl:  # exact sums where 3+ tiles meet, the group's terms in one all-reduce
+            import torch
+            parts = [backend.multicover(lv, t0, t1) for lv in mcl]
+            allc = torch.cat(parts) if len(parts) > 1 else parts[0]
+            comm.all_reduce_sum(allc)
             if log:
-                log.add("targets", sum(4 * t.numel() for _, t in sends))
-            for (a, b), buf in bufs:  # one addend per covering tile: exact up to 2 (below: 3+)
-                backend.rows_add(lsum[a * w:b * w], buf)
-            if backend.multicover_count(level):  # exact sums where 3+ tiles meet
-                contrib = backend.multicover(level, t0, t1)
-                comm.all_reduce_sum(contrib)
-                if log:
-                    log.add("multicover", 4 * contrib.numel())
-                backend.multicover_patch(level, contrib, lsum)
+                log.add("multicover", 4 * allc.numel())
+            o = 0
+            for lv, part in zip(mcl, parts):
+                backend.multicover_patch(lv, allc[o:o + part.numel()], tgt[lv][0])
+                o += part.numel()
+
+    nrep = sum(1 for r_, _ in G if r_)
+    if nrep:
+        gather_targets(range(nrep))
+    for level in range(nlevels):
+        last = level == nlevels - 1
+        rep, (plan, K, ext, bounds, need) = G[level]
+        if level == nrep:
+            gather_targets(range(nrep, nlevels))
+        w, h, h0, h1 = backend.dims(level)
+        r0, r1 = (h0, h1 + 1) if rep else (bounds[rank], bounds[rank + 1])
+        e0, e1 = need[rank]
+        # the previous level's rows this rank's first pass / border read, from their owners
+        # (after a replicated level every rank holds all of them)
+        if level > 0 and pbounds is not None:
+            hp = backend.dims(level - 1)[1]
+            wp = backend.dims(level - 1)[0]
+            psends, precvs = [], []
+            mine = owned_rows(pbounds, hp, rank)
+            for d in range(world):
+                if d == rank:
+                    continue
+                sp = _span(prev_rows_needed(bounds, h0, h1, K, hp, d), mine)
+                if sp:
+                    psends.append((d, prev[sp[0] * wp:sp[1] * wp]))
+                rp = _span(prev_rows_needed(bounds, h0, h1, K, hp, rank),
+                           owned_rows(pbounds, hp, d))
+                if rp:
+                    precvs.append((d, prev[rp[0] * wp:rp[1] * wp]))
+            comm.exchange(psends, precvs)
+            if log:
+                log.add("prev_halo", sum(4 * t.numel() for _, t in psends))
+        lsum, cnt = tgt[level]
         if rep:  # the whole level on this rank: the one-GPU level (seed, normalise, sweeps)
             prev = backend.level(level, prev, lsum, cnt, last)
             pbounds = None
             continue
+        lnorm = backend.plane(level)
         backend.normalize_rows(level, lsum, cnt, e0, e1, lnorm)
         a, b = backend.plane(level), backend.plane(level)
         if rank == 0 or rank == world - 1:  # the rows above / below the band
             backend.border(level, prev, a, b)
         src, dst = None, a
         for i, T in enumerate(plan):
-            if i > 0 and world > 1:
+            if i > 0:
                 k = T + 1
-                sends, recvs = [], []
+                hsends, hrecvs = [], []
                 if rank > 0:
                     lo_ = max(r0 - k, h0)
-                    sends.append((rank - 1, src[r0 * w:min(r0 + k, r1) * w]))
-                    recvs.append((rank - 1, src[lo_ * w:r0 * w]))
+                    hsends.append((rank - 1, src[r0 * w:min(r0 + k, r1) * w]))
+                    hrecvs.append((rank - 1, src[lo_ * w:r0 * w]))
                 if rank < world - 1:
                     hi_ = min(r1 + k, h1 + 1)
-                    sends.append((rank + 1, src[max(r1 - k, r0) * w:r1 * w]))
-                    recvs.append((rank + 1, src[r1 * w:hi_ * w]))
-                comm.exchange(sends, recvs)
+                    hsends.append((rank + 1, src[max(r1 - k, r0) * w:r1 * w]))
+                    hrecvs.append((rank + 1, src[r1 * w:hi_ * w]))
+                comm.exchange(hsends, hrecvs)
                 if log:
-                    log.add("pass_halo", sum(4 * t.numel() for _, t in sends))
+                    log.add("pass_halo", sum(4 * t.numel() for _, t in hsends))
             mode = (2 if level == 0 else 1) if i == 0 else 0
             fin = last and i == len(plan) - 1
             backend.band_pass(level, lnorm, mode, src, dst, T, r0, r1, fin, prev)
             src, dst = dst, (b if dst is a else a)
         prev, pbounds = (None if last else src), bounds
+    bounds = G[-1][1][3]
     # the u16 result: every rank's owned rows to rank 0 (a replicated last level: all local)
-    if world > 1 and pbounds is not None:
+    if pbounds is not None:
         import torch
         w, h = backend.dims(nlevels - 1)[:2]
 
