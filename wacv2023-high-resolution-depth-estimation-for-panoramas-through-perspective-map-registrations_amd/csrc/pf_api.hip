@@ -1989,7 +1989,7 @@ int pf_fuse_partial(pf_ctx* c, const float* tiles, const float* coeffs, int t0, 
     const LevelDims& L = lc.dims[level];
     HIPCHK(c, hipMemsetAsync(lsum, 0, sizeof(float) * L.w * L.h, c->stream));
     HIPCHK(c, hipMemsetAsync(cnt, 0, sizeof(float) * L.w * L.h, c->stream));
-    HIPCHK(c, launch_targets_map_partial(c->stream, (const TileGeom*)c->geom.p,
+    HIPCHK(c, launch_targets_partial(c->stream, (const TileGeom*)c->geom.p,
                                (const TileBox*)lc.box[level].p, (const TapBox*)lc.tapbox[level].p,
                                (const uint32_t*)lc.tmask[level].p, (c->ntiles + 31) / 32, t0, t1,
                                (const int32_t*)lc.tapmap[level].p, tiles, coeffs, L, lsum, cnt,
@@ -2027,7 +2027,7 @@ int pf_fuse_partial_rows(pf_ctx* c, const float* tiles, const float* coeffs, int
     if (t0 < 0 || t1 > c->ntiles || t0 > t1)
         return fail(c, PF_EINVAL, "tile range [%d,%d) outside [0,%d)", t0, t1, c->ntiles);
     const LevelCache& lc = c->lc;
-    HIPCHK(c, launch_targets_map_partial(c->stream, (const TileGeom*)c->geom.p,
+    HIPCHK(c, launch_targets_partial(c->stream, (const TileGeom*)c->geom.p,
                                (const TileBox*)lc.box[level].p, (const TapBox*)lc.tapbox[level].p,
                                (const uint32_t*)lc.tmask[level].p, (c->ntiles + 31) / 32, t0, t1,
                                (const int32_t*)lc.tapmap[level].p, tiles, coeffs, *L, lsum, cnt,

@@ -297,7 +297,7 @@ void launch_targets(hipStream_t s, const TileGeom* geom, const TileBox* box, int
                     float* lnorm, long long lstride, int batch);
  // rows [r0,r1), -1: band
 // the tile masks of the level's targets patches (LevelCache::tmask, targets_patch_w/h grid)
-hipError_t launch_targets_map_partial(hipStream_t s, const TileGeom* geom, const TileBox* box,
+hipError_t launch_targets_partial(hipStream_t s, const TileGeom* geom, const TileBox* box,
                                 const TapBox* tb, const uint32_t* tmask, int nmw, int t0, int t1,
                                 const int32_t* map, const float* tiles, const float* coeffs,
                                 LevelDims L, float* lsum, float* cnt, int r0, int r1);

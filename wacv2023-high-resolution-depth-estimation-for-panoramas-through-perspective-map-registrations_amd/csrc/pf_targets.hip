@@ -482,7 +482,7 @@ __global__ void __launch_bounds__(256) k_targets_patch_partial(const TileGeom* _
     }
 }
 
-hipError_t launch_targets_map_partial(hipStream_t s, const TileGeom* geom, const TileBox* box,
+hipError_t launch_targets_partial(hipStream_t s, const TileGeom* geom, const TileBox* box,
                                 const TapBox* tb, const uint32_t* tmask, int nmw, int t0, int t1,
                                 const int32_t* map, const float* tiles, const float* coeffs,
                                 LevelDims L, float* lsum, float* cnt, int r0, int r1)
