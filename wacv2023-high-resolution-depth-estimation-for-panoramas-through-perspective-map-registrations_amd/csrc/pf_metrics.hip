@@ -26,6 +26,9 @@ namespace {
 constexpr int MB = 256;        // threads per block
 constexpr int MNBLK = 128;     // blocks per panorama (fixed: the fp64 reduction order is fixed)
 constexpr int HBINS = 2048;    // bins of one radix digit (11 bits)
+#ifndef PF_MED_RUN
+#define PF_MED_RUN 1           // first-digit histogram: per-thread run counts (else wave ballots)
+#endif
 
 struct MArgs {
     const float* gt;
@@ -167,6 +170,19 @@ __global__ __launch_bounds__(MB) void k_med_hist(MArgs a, int pass, const SelSta
         pre[1] = st[b * 2 + 1].prefix;
     }
     const int psh = pass == 1 ? 21 : 10;
+    // PF_MED_RUN: the top digit of a depth map is spatially coherent, so each thread counts a run
+    // of equal bins in a register and adds it to LDS when the bin changes (and once at the end)
+    uint32_t rb[2] = {0u, 0u}, rc[2] = {0u, 0u};
+    auto run_add = [&](int st, uint32_t bin, bool act) {
+        if (!act) return;
+        if (rc[st] && bin == rb[st]) {
+            ++rc[st];
+        } else {
+            if (rc[st]) atomicAdd(&h[st][rb[st]], rc[st]);
+            rb[st] = bin;
+            rc[st] = 1u;
+        }
+    };
     // rows of the band round-robin over the blocks of this panorama, a row's pixels over the
     // threads; block-uniform trip counts so the wave-aggregated atomics see whole waves
     for (int y = a.h0 + blockIdx.x; y <= a.h1; y += gridDim.x)
@@ -178,7 +194,10 @@ __global__ __launch_bounds__(MB) void k_med_hist(MArgs a, int pass, const SelSta
                 const uint32_t k0 = fkey(v0[k]), k1 = fkey(v1[k]);
                 const bool a0 = ok[k] && (pass == 0 || (k0 >> psh) == pre[0]);
                 const bool a1 = ok[k] && (pass == 0 || (k1 >> psh) == pre[1]);
-                if (pass == 0) {  // the top digit clusters: aggregate over the wave
+                if (pass == 0 && PF_MED_RUN) {
+                    run_add(0, (k0 >> sh) & msk, a0);
+                    run_add(1, (k1 >> sh) & msk, a1);
+                } else if (pass == 0) {  // the top digit clusters: aggregate over the wave
                     agg_add(h[0], (k0 >> sh) & msk, a0);
                     agg_add(h[1], (k1 >> sh) & msk, a1);
                 } else {          // lower digits spread: plain LDS atomics
@@ -187,6 +206,8 @@ __global__ __launch_bounds__(MB) void k_med_hist(MArgs a, int pass, const SelSta
                 }
             }
         }
+    if (rc[0]) atomicAdd(&h[0][rb[0]], rc[0]);
+    if (rc[1]) atomicAdd(&h[1][rb[1]], rc[1]);
     __syncthreads();
     uint32_t* g = hist + (long long)b * 2 * HBINS;
     for (int i = threadIdx.x; i < 2 * HBINS; i += MB) {
@@ -332,6 +353,7 @@ __global__ __launch_bounds__(MB) void k_err_sums(MArgs a, int align_way, const A
     const int b = blockIdx.y;
     const Align A = al[b];
     double s[NSUM + 1] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
+    uint32_t cn[5] = {0, 0, 0, 0, 0};  // s[4..8] are counts: integer adds per thread
     for (int y = a.h0 + blockIdx.x; y <= a.h1; y += gridDim.x)
     for (int x0 = 4 * threadIdx.x; x0 < a.w; x0 += 4 * MB) {
       float V0[4], V1[4];
@@ -352,20 +374,21 @@ __global__ __launch_bounds__(MB) void k_err_sums(MArgs a, int align_way, const A
         if ((double)v0 > 1e-4 && (double)v1 > 1e-4) {
             const float lg = log10f(v0) - log10f(v1);
             s[3] += (double)lg * (double)lg;
-            s[5] += 1.0;
+            ++cn[1];
         }
         if (v0 > 0 && v1 > 0) {
             // MAX2(v0 / v1, v1 / v0) with one division: the quotient of the larger by the
             // smaller is >= 1 and the other <= 1 after rounding (rounding is monotonic), so the
             // max is exactly fl(larger / smaller)
             const float rm = v0 > v1 ? v0 / v1 : v1 / v0;
-            if ((double)rm >= 1.25) s[6] += 1.0;
-            if ((double)rm >= 1.5625) s[7] += 1.0;
-            if ((double)rm >= 1.953125) s[8] += 1.0;
+            cn[2] += (double)rm >= 1.25;
+            cn[3] += (double)rm >= 1.5625;
+            cn[4] += (double)rm >= 1.953125;
         }
-        s[4] += 1.0;
+        ++cn[0];
       }
     }
+    for (int k = 0; k < 5; ++k) s[4 + k] = (double)cn[k];
     __shared__ double red[MB / 64][NSUM + 1];
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     for (int k = 0; k <= NSUM; ++k) {
