@@ -217,12 +217,12 @@ __global__ __launch_bounds__(MB) void k_med_hist(MArgs a, int pass, const SelSta
 }
 
 // One block per (panorama, stream): find the bin holding the element of rank `rank`.
-__global__ __launch_bounds__(MB) void k_med_scan(int pass, const uint32_t* hist, SelState* st)
+__global__ __launch_bounds__(MB) void k_med_scan(int pass, uint32_t* hist, SelState* st)
 {
     constexpr int PER = HBINS / MB;  // 8 bins per thread
     __shared__ uint32_t part[MB];
     const int s = blockIdx.x;  // b * 2 + stream
-    const uint32_t* g = hist + (long long)s * HBINS;
+    uint32_t* g = hist + (long long)s * HBINS;
     const int nb = pass == 2 ? 1024 : HBINS;
     uint32_t loc[PER], sum = 0;
     for (int j = 0; j < PER; ++j) {
@@ -230,6 +230,9 @@ __global__ __launch_bounds__(MB) void k_med_scan(int pass, const uint32_t* hist,
         loc[j] = bin < nb ? g[bin] : 0u;
         sum += loc[j];
     }
+    // the next pass histograms into the same bins: each thread clears the bins it read (all
+    // HBINS, so the workspace leaves the last pass zeroed as well)
+    for (int j = 0; j < PER; ++j) g[threadIdx.x * PER + j] = 0u;
     part[threadIdx.x] = sum;
     __syncthreads();
     // inclusive Hillis-Steele scan over 256 partial sums
@@ -699,8 +702,7 @@ void launch_metrics(hipStream_t s, const MetricsJob& j, void* ws, pf_metrics* ou
         const dim3 grid(MNBLK, nb);
         if (j.align_way == 1) {
             (void)hipMemsetAsync(hc, 0, sizeof(uint32_t) * 2 * HBINS * nb, s);
-            for (int pass = 0; pass < 3; ++pass) {
-                if (pass) (void)hipMemsetAsync(hc, 0, sizeof(uint32_t) * 2 * HBINS * nb, s);
+            for (int pass = 0; pass < 3; ++pass) {  // k_med_scan re-zeroes the bins it read
                 hipLaunchKernelGGL(k_med_hist, grid, dim3(MB), 0, s, c, pass, sc, hc);
                 hipLaunchKernelGGL(k_med_scan, dim3(2 * nb), dim3(MB), 0, s, pass, hc, sc);
             }
