@@ -9,7 +9,7 @@ Two summation orders (pf_set_metrics_order):
   oracle, like the g++ build of the reference, calls) is not correctly rounded (9.3 % of the
   floats in [1e-4, 2] differ from the correctly rounded value), so single terms differ by an
   ulp.
-* "tree" (the library default since round 5: 1.1 ms against 24 ms per call): fp64 partial
+* "tree" (the library default since round 5: 0.9 ms against 15.6 ms per call): fp64 partial
   sums.  Bars: medians, shift, counts and deltas bit-exact; the means within
   1e-2 relative of the oracle's fp32 sequential sums (measured 1.1e-3 drift on mselog at C2; the
   a-priori bound n*u is 7e-2) and within 1e-5 of an fp64 numpy sum of the same fp32 terms; the
@@ -244,3 +244,24 @@ def test_metrics_batch16_and_fast_float_path(fuser):
     got = fuser.error_metrics(_dev(gt[:2]), _dev(gv), ZR, 1, True)
     for b in range(2):
         _check(got[b], O.error_metrics(gt[b], gv[b], ZR, 1, True), 1)
+
+
+@pytest.mark.parametrize("align_way", [1, 2])
+def test_sequential_redo_path_is_exact(fuser, merged, align_way, monkeypatch):
+    """The sequential mse/mselog chains run fma(v, v, acc) and check every step against the
+    reference's (float)((double)acc + (double)v * v); a mismatch (rare: a double sum on a float
+    tie) redoes the rest of the chunk exactly.  PF_METRICS_SEQ_FORCE_FIX=1 flags one step per
+    1024-pixel chunk as a mismatch, so the redo path runs ~1,500 times per panorama here: the
+    results must stay bit-exact against the oracle."""
+    emap, gt, out = merged
+    monkeypatch.setenv("PF_METRICS_SEQ_FORCE_FIX", "1")
+    fuser.set_metrics_order("sequential")
+    try:
+        got = fuser.error_metrics(_dev(gt), out, ZR, align_way, True)
+        got_e = fuser.error_metrics(_dev(gt), _dev(emap), ZR, align_way, True)
+    finally:
+        fuser.set_metrics_order("tree")
+    res = out.cpu().numpy().view(np.uint16)
+    for b in range(out.shape[0]):
+        _check_exact(got[b], O.error_metrics(gt[b], res[b], ZR, align_way, True))
+        _check_exact(got_e[b], O.error_metrics(gt[b], emap[b], ZR, align_way, True))

@@ -19,6 +19,8 @@
 // MFMA.
 #include "pf_internal.hpp"
 
+#include <cstdlib>
+
 namespace pf {
 
 namespace {
@@ -452,7 +454,7 @@ __global__ __launch_bounds__(MB) void k_err_final(const double* part, int nblk, 
 // (`mse += pow(val0 - val1, 2)` is float = (float)((double)float + double)), mae and mre in
 // float, the least-squares sums a_00..b_1 in float (Depth.cpp:2119-2123, 2178-2186).  Each
 // pixel's terms are computed in parallel (k_seq_terms) and written in that order; one lane per
-// panorama then adds them in sequence (k_ls_seq / k_err_seq).  A pixel that the reference skips
+// plane then adds them in sequence (k_ls_seq / k_err_seq, below).  A pixel that the reference skips
 // contributes exact zeros (x + 0 == x for every finite x >= 0), so the lanes need no masks; the
 // counts (n, nlog, delta fails) are integers and stay in the parallel pass (k_err_sums).
 struct SeqTerms {  // four planes per panorama: component k of band pixel i = (y - h0) * w + x of
@@ -501,82 +503,201 @@ __global__ __launch_bounds__(MB) void k_seq_terms(MArgs a, int align_way, const 
     }
 }
 
-// The sequential sums: one wave per panorama.  The whole wave streams the panorama's term planes
-// through LDS in chunks of SCH pixels (16 B per lane per load, the next chunk's loads in flight
-// while the current one is added), and lane k adds plane sel[k] in row-major order into its own
-// float accumulator: acc = (float)((double)acc + term), term = (double)v * (double)v for the
-// squared planes (exact: 48 significant bits), v > 0 ? 1 : 0 for an indicator, (double)v else --
-// for a float term that is exactly the float sum acc + v (double rounding is innocuous for +).
-// The wave's critical path is then the dependent add chain of one pixel per step, not a load.
-constexpr int SCH = 1024, SPS = SCH + 16;  // LDS plane stride: the summing lanes' planes in
-                                          // different banks
-struct SeqLane {
-    int plane;  // 0..3
-    bool sq, ind;
-};
-__device__ __forceinline__ float seq_sum_wave(const float* __restrict__ pl, long long band,
-                                              long long bandp, SeqLane m, float (*lds)[4 * SPS])
+// The sequential sums.  The reference's accumulators are floats: for a float term the double sum
+// rounded to float IS the float sum (double rounding is innocuous for + of two floats), so mae,
+// mre and the least-squares sums are one dependent fp32 add per pixel.  mse and mselog add an
+// exact double square, acc = (float)((double)acc + (double)v * (double)v), whose cvt/add-f64/cvt
+// chain costs ~38 cycles per pixel; there the wave runs the single-rounding fma(v, v, acc) -- equal
+// to the reference except when the double sum lands exactly on a float tie -- and then checks
+// every step of the chunk in parallel (lane l recomputes the reference's step j = l, l + 64, ...
+// from the stored previous value).  All steps before the first mismatch are exact by induction;
+// from a mismatch on (rare: ~2^-29 per step) the lane recomputes the rest of the chunk with the
+// reference's formula, so the result is the reference's in every case.
+//
+// One wave streams NPL of the panorama's term planes through LDS in chunks of SCH pixels (16 B
+// per lane per load, the next chunk's loads in flight while the current one is added); lane
+// k < NPL adds plane pid[k] in row-major order.
+constexpr int SCH = 1024, SPS = SCH + 16;  // LDS plane stride: the lanes' planes in different banks
+
+__device__ __forceinline__ void wave_sync()
+{  // one wave's LDS operations complete in order: wait for this lane's LDS operations and keep
+   // the compiler from moving memory operations across.  A wavefront-scope fence would also
+   // wait for the next chunk's global loads in flight (vmcnt(0)), stalling every chunk.
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_wave_barrier();
+}
+
+__device__ __forceinline__ float sq_step(float acc, float v)
+{  // the reference's step for a squared term (Depth.cpp:2178-2186: mse += pow(d, 2))
+    const double t = (double)v;
+    return (float)((double)acc + t * t);
+}
+
+// SQ: NPL == 2 squared planes (fast fma chain + verification, accb = 2 x SCH floats of LDS);
+// else plain float adds.  cnt (all lanes): number of positive terms of plane pid[NPL - 1].
+// force (tests): one step per chunk counts as a mismatch, so the exact redo path runs.
+template <int NPL, bool SQ>
+__device__ __forceinline__ float seq_chain(const float* __restrict__ pl, long long band,
+                                           long long bandp, const int (&pid)[NPL], float* lds,
+                                           float* accb, uint32_t* cnt, int force = 0)
 {
-    const int lane = threadIdx.x;
+    static_assert(!SQ || NPL == 2, "squared chains come in pairs");
+    const int lane = threadIdx.x & 63;
     constexpr int NM = SCH / 256;  // float4 loads per lane per plane and chunk
-    float4 R[4][NM];
+    float4 R[NPL][NM];
     auto load = [&](long long c) {
 #pragma unroll
-        for (int p = 0; p < 4; ++p)
+        for (int p = 0; p < NPL; ++p)
 #pragma unroll
             for (int u = 0; u < NM; ++u) {
                 const long long off = c * SCH + u * 256 + lane * 4;  // < bandp => off + 3 < bandp
-                R[p][u] = off < bandp ? *reinterpret_cast<const float4*>(pl + p * bandp + off)
+                R[p][u] = off < bandp ? *reinterpret_cast<const float4*>(pl + pid[p] * bandp + off)
                                       : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
             }
     };
     auto put = [&](float* L) {
 #pragma unroll
-        for (int p = 0; p < 4; ++p)
+        for (int p = 0; p < NPL; ++p)
 #pragma unroll
             for (int u = 0; u < NM; ++u)
                 *reinterpret_cast<float4*>(L + p * SPS + u * 256 + lane * 4) = R[p][u];
     };
+    const int my = lane < NPL ? lane : 0;
     float acc = 0.0f;
-    auto add = [&](float v) {
-        const double t = m.ind ? (v > 0.0f ? 1.0 : 0.0) : (m.sq ? (double)v * (double)v : (double)v);
-        acc = (float)((double)acc + t);
-    };
+    uint32_t pos = 0;
     const long long nch = (band + SCH - 1) / SCH;
-    if (nch == 0) return acc;
+    if (nch == 0) {
+        if (cnt) *cnt = 0;
+        return acc;
+    }
     load(0);
-    put(lds[0]);
-    __syncthreads();
+    put(lds);
+    wave_sync();
     for (long long c = 0; c < nch; ++c) {
         if (c + 1 < nch) load(c + 1);
-        const float* L = lds[c & 1] + m.plane * SPS;
+        const float* L = lds + (c & 1) * (NPL * SPS);
+        const float* Lm = L + my * SPS;
         const int n = (int)(band - c * SCH < SCH ? band - c * SCH : SCH);
-        int j = 0;
-        for (; j + 4 <= n; j += 4) {
-            const float4 v = *reinterpret_cast<const float4*>(L + j);
-            add(v.x);
-            add(v.y);
-            add(v.z);
-            add(v.w);
+        float st[2] = {0.0f, 0.0f};
+        if constexpr (SQ) {
+            st[0] = __shfl(acc, 0);
+            st[1] = __shfl(acc, 1);
         }
-        for (; j < n; ++j) add(L[j]);
-        if (c + 1 < nch) put(lds[(c + 1) & 1]);
-        __syncthreads();
+        // 16 pixels per step; the next step's LDS reads are issued before this step's accb
+        // writes (the compiler may not hoist them past possibly-aliasing stores), so one LDS
+        // latency is paid per 16 pixels.  Reads past n stay inside the SPS-padded planes.
+        int j = 0;
+        if (n >= 16) {
+            float4 cur[4];
+#pragma unroll
+            for (int k = 0; k < 4; ++k) cur[k] = *reinterpret_cast<const float4*>(Lm + 4 * k);
+            for (; j + 16 <= n; j += 16) {
+                float4 nxt[4];
+#pragma unroll
+                for (int k = 0; k < 4; ++k)
+                    nxt[k] = *reinterpret_cast<const float4*>(Lm + j + 16 + 4 * k);
+#pragma unroll
+                for (int k = 0; k < 4; ++k) {
+                    const float4 v = cur[k];
+                    if constexpr (SQ) {
+                        const float a1 = __builtin_fmaf(v.x, v.x, acc);
+                        const float a2 = __builtin_fmaf(v.y, v.y, a1);
+                        const float a3 = __builtin_fmaf(v.z, v.z, a2);
+                        const float a4 = __builtin_fmaf(v.w, v.w, a3);
+                        cur[k] = make_float4(a1, a2, a3, a4);
+                        acc = a4;
+                    } else {
+                        acc = acc + v.x;
+                        acc = acc + v.y;
+                        acc = acc + v.z;
+                        acc = acc + v.w;
+                    }
+                }
+                if constexpr (SQ) {
+                    if (lane < 2) {
+#pragma unroll
+                        for (int k = 0; k < 4; ++k)
+                            *reinterpret_cast<float4*>(accb + lane * SCH + j + 4 * k) = cur[k];
+                    }
+                }
+#pragma unroll
+                for (int k = 0; k < 4; ++k) cur[k] = nxt[k];
+            }
+        }
+        for (; j < n; ++j) {
+            const float v = Lm[j];
+            if constexpr (SQ) {
+                acc = __builtin_fmaf(v, v, acc);
+                if (lane < 2) accb[lane * SCH + j] = acc;
+            } else {
+                acc = acc + v;
+            }
+        }
+        if (cnt) {
+            const float* Lc = L + (NPL - 1) * SPS;
+            for (int i = lane; i < n; i += 64) pos += Lc[i] > 0.0f ? 1u : 0u;
+        }
+        if constexpr (SQ) {
+            wave_sync();
+            // no early exit: the loads and f64 steps of successive 64-step blocks overlap
+            int first[2] = {n, n};
+            int fj[2] = {-1, -1};  // forced mismatch steps (tests), one 64-bit modulo per chunk
+            if (force) {
+                fj[0] = (int)((c * 613) % n);
+                fj[1] = (int)((c * 613 + 17) % n);
+            }
+#pragma unroll 4
+            for (int jb = 0; jb < SCH; jb += 64) {  // fixed trip count (steps past n are idle)
+                const int jj = jb + lane;
+                bool bad[2] = {false, false};
+                if (jj < n) {
+#pragma unroll
+                    for (int q = 0; q < 2; ++q) {
+                        const float* A = accb + q * SCH;
+                        const float ex = sq_step(jj ? A[jj - 1] : st[q], L[q * SPS + jj]);
+                        bad[q] = __float_as_uint(ex) != __float_as_uint(A[jj]) || jj == fj[q];
+                    }
+                }
+#pragma unroll
+                for (int q = 0; q < 2; ++q) {
+                    const uint64_t m = __ballot(bad[q]);
+                    if (m && first[q] == n) first[q] = jb + __ffsll((unsigned long long)m) - 1;
+                }
+            }
+#pragma unroll
+            for (int q = 0; q < 2; ++q) {
+                if (first[q] < n && lane == q) {  // redo the rest of the chunk the reference's way
+                    const float* A = accb + q * SCH;
+                    const float* Lp = L + q * SPS;
+                    float a = first[q] ? A[first[q] - 1] : st[q];
+                    for (int i = first[q]; i < n; ++i) a = sq_step(a, Lp[i]);
+                    acc = a;
+                }
+            }
+        }
+        if (c + 1 < nch) put(lds + ((c + 1) & 1) * (NPL * SPS));
+        wave_sync();
+    }
+    if (cnt) {
+        for (int o = 32; o > 0; o >>= 1) pos += __shfl_xor(pos, o);
+        *cnt = pos;
     }
     return acc;
 }
 
-// Depth.cpp:2119-2134 in the reference's float order, one wave per panorama: lanes 0..4 add
-// a00 (v1*v1), a01 (v1), a11 (count of compared pixels), b0 (v0*v1), b1 (v0).
+// Depth.cpp:2119-2134 in the reference's float order, one wave per panorama: lanes 0..3 add
+// a00 (v1*v1), a01 (v1), b0 (v0*v1), b1 (v0); a11 counts the compared pixels in a float, which
+// is the count itself up to 2^24 and stays at 2^24 after (2^24 + 1 rounds to even).
 __global__ __launch_bounds__(64) void k_ls_seq(SeqTerms T, long long band, Align* al)
 {
-    __shared__ float lds[2][4 * SPS];
+    __shared__ float lds[2 * 4 * SPS];
     const int b = blockIdx.x, lane = threadIdx.x;
-    static constexpr int plane[5] = {0, 1, 3, 2, 3};
-    const SeqLane m{lane < 5 ? plane[lane] : 0, false, lane == 2};
-    const float r = seq_sum_wave(T.t + (long long)b * 4 * T.bandp, band, T.bandp, m, lds);
-    const float a00 = __shfl(r, 0), a01 = __shfl(r, 1), a11 = __shfl(r, 2), b0 = __shfl(r, 3),
-                b1 = __shfl(r, 4);
+    const int pid[4] = {0, 1, 2, 3};
+    uint32_t n = 0;
+    const float r = seq_chain<4, false>(T.t + (long long)b * 4 * T.bandp, band, T.bandp, pid, lds,
+                                        nullptr, &n);
+    const float a00 = __shfl(r, 0), a01 = __shfl(r, 1), b0 = __shfl(r, 2), b1 = __shfl(r, 3);
+    const float a11 = (float)(n < (1u << 24) ? n : (1u << 24));
     if (lane != 0) return;
     const float det = a00 * a11 - a01 * a01;
     Align A{1.0f, 0.0f, 0.0f, 0.0f, 0.0f};
@@ -585,18 +706,31 @@ __global__ __launch_bounds__(64) void k_ls_seq(SeqTerms T, long long band, Align
     al[b] = A;
 }
 
-// Depth.cpp:2178-2186, 2207-2210 in the reference's order, one wave per panorama: lanes 0..3
-// add mse (through a double), mae, mre, mselog (through a double); the integer counts come from
-// the parallel pass's part[] (exact in any order).
-__global__ __launch_bounds__(64) void k_err_seq(SeqTerms T, long long band, const double* part,
-                                                int nblk, const Align* al, pf_metrics* out)
+// Depth.cpp:2178-2186, 2207-2210 in the reference's order, two waves per panorama: wave 0 adds
+// mse (plane 0) and mselog (plane 3) through the double square, wave 1 mae (plane 1) and mre
+// (plane 2) in float; the integer counts come from the parallel pass's part[] (exact in any
+// order).
+__global__ __launch_bounds__(128) void k_err_seq(SeqTerms T, long long band, const double* part,
+                                                 int nblk, const Align* al, pf_metrics* out,
+                                                 int force)
 {
-    __shared__ float lds[2][4 * SPS];
-    const int b = blockIdx.x, lane = threadIdx.x;
-    const SeqLane m{lane < 4 ? lane : 0, lane == 0 || lane == 3, false};
-    const float r = seq_sum_wave(T.t + (long long)b * 4 * T.bandp, band, T.bandp, m, lds);
-    const float mse = __shfl(r, 0), mae = __shfl(r, 1), mre = __shfl(r, 2), mselog = __shfl(r, 3);
-    if (lane != 0) return;
+    __shared__ float lds[2][2 * 2 * SPS];
+    __shared__ float accb[2 * SCH];
+    __shared__ float res[4];
+    const int b = blockIdx.x, lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const float* pl = T.t + (long long)b * 4 * T.bandp;
+    if (wv == 0) {
+        const int pid[2] = {0, 3};
+        const float r = seq_chain<2, true>(pl, band, T.bandp, pid, lds[0], accb, nullptr, force);
+        if (lane < 2) res[lane == 0 ? 0 : 3] = r;
+    } else {
+        const int pid[2] = {1, 2};
+        const float r = seq_chain<2, false>(pl, band, T.bandp, pid, lds[1], nullptr, nullptr);
+        if (lane < 2) res[lane + 1] = r;
+    }
+    __syncthreads();
+    if (threadIdx.x != 0) return;
+    const float mse = res[0], mae = res[1], mre = res[2], mselog = res[3];
     double cnt[5] = {0, 0, 0, 0, 0};  // n, nlog, fail1..3: integer-valued, order-free
     for (int i = 0; i < nblk; ++i)
         for (int k = 0; k < 5; ++k) cnt[k] += part[((long long)b * nblk + i) * (NSUM + 1) + 4 + k];
@@ -677,6 +811,9 @@ void launch_metrics(hipStream_t s, const MetricsJob& j, void* ws, pf_metrics* ou
     double* part = (double*)carve(sizeof(double) * (NSUM + 1) * MNBLK * j.batch);
     Align* al = (Align*)carve(sizeof(Align) * j.batch);
     const long long band = (long long)(j.h1 - j.h0 + 1) * j.w;
+    // tests only: PF_METRICS_SEQ_FORCE_FIX=1 sends one step per chunk down the exact redo path
+    const char* ff = getenv("PF_METRICS_SEQ_FORCE_FIX");
+    const int seq_force = ff && ff[0] == '1' ? 1 : 0;
     SeqTerms T{};
     if (j.sequential) {
         T.bandp = (band + 3) & ~3LL;
@@ -720,8 +857,8 @@ void launch_metrics(hipStream_t s, const MetricsJob& j, void* ws, pf_metrics* ou
         if (j.sequential) {
             hipLaunchKernelGGL(k_seq_terms<false>, grid, dim3(MB), 0, s, c, j.align_way, ac, Tc,
                                band);
-            hipLaunchKernelGGL(k_err_seq, dim3(nb), dim3(64), 0, s, Tc, band, pc, MNBLK, ac,
-                               out + b0);
+            hipLaunchKernelGGL(k_err_seq, dim3(nb), dim3(128), 0, s, Tc, band, pc, MNBLK, ac,
+                               out + b0, seq_force);
         } else {
             hipLaunchKernelGGL(k_err_final, dim3(nb), dim3(MB), 0, s, pc, MNBLK, ac, out + b0);
         }
