@@ -9,7 +9,7 @@ Two summation orders (pf_set_metrics_order):
   oracle, like the g++ build of the reference, calls) is not correctly rounded (9.3 % of the
   floats in [1e-4, 2] differ from the correctly rounded value), so single terms differ by an
   ulp.
-* "tree" (the library default since round 5: 0.9 ms against 15.6 ms per call): fp64 partial
+* "tree" (the library default since round 5: 0.9 ms against ~8 ms per call): fp64 partial
   sums.  Bars: medians, shift, counts and deltas bit-exact; the means within
   1e-2 relative of the oracle's fp32 sequential sums (measured 1.1e-3 drift on mselog at C2; the
   a-priori bound n*u is 7e-2) and within 1e-5 of an fp64 numpy sum of the same fp32 terms; the

@@ -517,6 +517,12 @@ __global__ __launch_bounds__(MB) void k_seq_terms(MArgs a, int align_way, const 
 // One wave streams NPL of the panorama's term planes through LDS in chunks of SCH pixels (16 B
 // per lane per load, the next chunk's loads in flight while the current one is added); lane
 // k < NPL adds plane pid[k] in row-major order.
+#ifndef PF_SEQ_SB
+#define PF_SEQ_SB 0  // schedule barrier after the chain's next-group LDS reads (A/B knob)
+#endif
+#ifndef PF_SEQ_GRP
+#define PF_SEQ_GRP 64  // pixels per chain group (one LDS round trip each; one checked per lane)
+#endif
 constexpr int SCH = 1024, SPS = SCH + 16;  // LDS plane stride: the lanes' planes in different banks
 
 __device__ __forceinline__ void wave_sync()
@@ -535,13 +541,20 @@ __device__ __forceinline__ float sq_step(float acc, float v)
 
 // SQ: NPL == 2 squared planes (fast fma chain + verification, accb = 2 x SCH floats of LDS);
 // else plain float adds.  cnt (all lanes): number of positive terms of plane pid[NPL - 1].
-// force (tests): one step per chunk counts as a mismatch, so the exact redo path runs.
+// SQ (NPL == 1): one squared plane per wave, every lane runs the same chain; lane g keeps the
+// chain's value at the end of GRP-pixel group g of the chunk, so the check is one group per lane
+// (from the previous group's end value, the reference's 16 steps must reach this group's end
+// value) with no LDS writes on the chain's path.  Matching group ends make the chunk's result
+// the reference's by induction, whatever the steps inside did.  force (tests): one group per
+// chunk counts as a mismatch, so the exact redo path runs.
 template <int NPL, bool SQ>
 __device__ __forceinline__ float seq_chain(const float* __restrict__ pl, long long band,
                                            long long bandp, const int (&pid)[NPL], float* lds,
-                                           float* accb, uint32_t* cnt, int force = 0)
+                                           uint32_t* cnt, int force = 0)
 {
-    static_assert(!SQ || NPL == 2, "squared chains come in pairs");
+    static_assert(!SQ || NPL == 1, "one squared chain per wave");
+    constexpr int GRP = PF_SEQ_GRP, GQ = GRP / 4;  // pixels, float4 reads per group
+    static_assert(SCH % GRP == 0 && SCH / GRP <= 64, "at most one group per lane");
     const int lane = threadIdx.x & 63;
     constexpr int NM = SCH / 256;  // float4 loads per lane per plane and chunk
     float4 R[NPL][NM];
@@ -578,102 +591,76 @@ __device__ __forceinline__ float seq_chain(const float* __restrict__ pl, long lo
         const float* L = lds + (c & 1) * (NPL * SPS);
         const float* Lm = L + my * SPS;
         const int n = (int)(band - c * SCH < SCH ? band - c * SCH : SCH);
-        float st[2] = {0.0f, 0.0f};
-        if constexpr (SQ) {
-            st[0] = __shfl(acc, 0);
-            st[1] = __shfl(acc, 1);
-        }
-        // 16 pixels per step; the next step's LDS reads are issued before this step's accb
-        // writes (the compiler may not hoist them past possibly-aliasing stores), so one LDS
-        // latency is paid per 16 pixels.  Reads past n stay inside the SPS-padded planes.
-        int j = 0;
-        if (n >= 16) {
-            float4 cur[4];
+        if (SQ && n < SCH) {  // the band's last, partial chunk: the reference's steps directly
+            for (int j = 0; j < n; ++j) acc = sq_step(acc, Lm[j]);
+        } else {
+            const float st = acc;
+            float mine = 0.0f;  // SQ: lane g holds the value at the end of group g
+            // 16 pixels per group; the next group's LDS reads are issued before this group's
+            // chain.  Reads past n stay inside the SPS-padded planes.
+            int j = 0;
+            if (n >= GRP) {
+                float4 cur[GQ];
 #pragma unroll
-            for (int k = 0; k < 4; ++k) cur[k] = *reinterpret_cast<const float4*>(Lm + 4 * k);
-            for (; j + 16 <= n; j += 16) {
-                float4 nxt[4];
+                for (int k = 0; k < GQ; ++k) cur[k] = *reinterpret_cast<const float4*>(Lm + 4 * k);
+                for (; j + GRP <= n; j += GRP) {
+                    float4 nxt[GQ];
 #pragma unroll
-                for (int k = 0; k < 4; ++k)
-                    nxt[k] = *reinterpret_cast<const float4*>(Lm + j + 16 + 4 * k);
+                    for (int k = 0; k < GQ; ++k)  // the last group's reads run past n: inside
+                        nxt[k] = *reinterpret_cast<const float4*>(  // the padded LDS region
+                            Lm + (j + GRP < SCH ? j + GRP : 0) + 4 * k);
+#if PF_SEQ_SB
+                    __builtin_amdgcn_sched_barrier(0);  // keep the reads a whole group ahead
+#endif
 #pragma unroll
-                for (int k = 0; k < 4; ++k) {
-                    const float4 v = cur[k];
-                    if constexpr (SQ) {
-                        const float a1 = __builtin_fmaf(v.x, v.x, acc);
-                        const float a2 = __builtin_fmaf(v.y, v.y, a1);
-                        const float a3 = __builtin_fmaf(v.z, v.z, a2);
-                        const float a4 = __builtin_fmaf(v.w, v.w, a3);
-                        cur[k] = make_float4(a1, a2, a3, a4);
-                        acc = a4;
-                    } else {
-                        acc = acc + v.x;
-                        acc = acc + v.y;
-                        acc = acc + v.z;
-                        acc = acc + v.w;
+                    for (int k = 0; k < GQ; ++k) {
+                        const float4 v = cur[k];
+                        if constexpr (SQ) {
+                            acc = __builtin_fmaf(v.x, v.x, acc);
+                            acc = __builtin_fmaf(v.y, v.y, acc);
+                            acc = __builtin_fmaf(v.z, v.z, acc);
+                            acc = __builtin_fmaf(v.w, v.w, acc);
+                        } else {
+                            acc = acc + v.x;
+                            acc = acc + v.y;
+                            acc = acc + v.z;
+                            acc = acc + v.w;
+                        }
                     }
-                }
-                if constexpr (SQ) {
-                    if (lane < 2) {
+                    if constexpr (SQ) mine = lane == j / GRP ? acc : mine;
 #pragma unroll
-                        for (int k = 0; k < 4; ++k)
-                            *reinterpret_cast<float4*>(accb + lane * SCH + j + 4 * k) = cur[k];
-                    }
+                    for (int k = 0; k < GQ; ++k) cur[k] = nxt[k];
                 }
-#pragma unroll
-                for (int k = 0; k < 4; ++k) cur[k] = nxt[k];
             }
-        }
-        for (; j < n; ++j) {
-            const float v = Lm[j];
+            for (; j < n; ++j) acc = acc + Lm[j];  // plain chains only (SQ chunks here are full)
             if constexpr (SQ) {
-                acc = __builtin_fmaf(v, v, acc);
-                if (lane < 2) accb[lane * SCH + j] = acc;
-            } else {
-                acc = acc + v;
+                // lane g: the reference's GRP steps of group g from the end of group g - 1
+                constexpr int NG = SCH / GRP;
+                const float up = __shfl_up(mine, 1);
+                float e = lane ? up : st;
+                const float4* G = reinterpret_cast<const float4*>(Lm + GRP * (lane < NG ? lane : 0));
+#pragma unroll
+                for (int k = 0; k < GQ; ++k) {
+                    const float4 v = G[k];
+                    e = sq_step(e, v.x);
+                    e = sq_step(e, v.y);
+                    e = sq_step(e, v.z);
+                    e = sq_step(e, v.w);
+                }
+                const int fg = force ? (int)((c * 613) % NG) : -1;
+                const uint64_t m = __ballot(lane < NG && (__float_as_uint(e) != __float_as_uint(mine) ||
+                                                          lane == fg));
+                if (m) {  // rare: redo from the first bad group the reference's way
+                    const int g0 = __ffsll((unsigned long long)m) - 1;
+                    float a = g0 ? __shfl(mine, g0 - 1) : st;
+                    for (int i = GRP * g0; i < n; ++i) a = sq_step(a, Lm[i]);
+                    acc = a;
+                }
             }
         }
         if (cnt) {
             const float* Lc = L + (NPL - 1) * SPS;
             for (int i = lane; i < n; i += 64) pos += Lc[i] > 0.0f ? 1u : 0u;
-        }
-        if constexpr (SQ) {
-            wave_sync();
-            // no early exit: the loads and f64 steps of successive 64-step blocks overlap
-            int first[2] = {n, n};
-            int fj[2] = {-1, -1};  // forced mismatch steps (tests), one 64-bit modulo per chunk
-            if (force) {
-                fj[0] = (int)((c * 613) % n);
-                fj[1] = (int)((c * 613 + 17) % n);
-            }
-#pragma unroll 4
-            for (int jb = 0; jb < SCH; jb += 64) {  // fixed trip count (steps past n are idle)
-                const int jj = jb + lane;
-                bool bad[2] = {false, false};
-                if (jj < n) {
-#pragma unroll
-                    for (int q = 0; q < 2; ++q) {
-                        const float* A = accb + q * SCH;
-                        const float ex = sq_step(jj ? A[jj - 1] : st[q], L[q * SPS + jj]);
-                        bad[q] = __float_as_uint(ex) != __float_as_uint(A[jj]) || jj == fj[q];
-                    }
-                }
-#pragma unroll
-                for (int q = 0; q < 2; ++q) {
-                    const uint64_t m = __ballot(bad[q]);
-                    if (m && first[q] == n) first[q] = jb + __ffsll((unsigned long long)m) - 1;
-                }
-            }
-#pragma unroll
-            for (int q = 0; q < 2; ++q) {
-                if (first[q] < n && lane == q) {  // redo the rest of the chunk the reference's way
-                    const float* A = accb + q * SCH;
-                    const float* Lp = L + q * SPS;
-                    float a = first[q] ? A[first[q] - 1] : st[q];
-                    for (int i = first[q]; i < n; ++i) a = sq_step(a, Lp[i]);
-                    acc = a;
-                }
-            }
         }
         if (c + 1 < nch) put(lds + ((c + 1) & 1) * (NPL * SPS));
         wave_sync();
@@ -695,7 +682,7 @@ __global__ __launch_bounds__(64) void k_ls_seq(SeqTerms T, long long band, Align
     const int pid[4] = {0, 1, 2, 3};
     uint32_t n = 0;
     const float r = seq_chain<4, false>(T.t + (long long)b * 4 * T.bandp, band, T.bandp, pid, lds,
-                                        nullptr, &n);
+                                        &n);
     const float a00 = __shfl(r, 0), a01 = __shfl(r, 1), b0 = __shfl(r, 2), b1 = __shfl(r, 3);
     const float a11 = (float)(n < (1u << 24) ? n : (1u << 24));
     if (lane != 0) return;
@@ -706,26 +693,26 @@ __global__ __launch_bounds__(64) void k_ls_seq(SeqTerms T, long long band, Align
     al[b] = A;
 }
 
-// Depth.cpp:2178-2186, 2207-2210 in the reference's order, two waves per panorama: wave 0 adds
-// mse (plane 0) and mselog (plane 3) through the double square, wave 1 mae (plane 1) and mre
-// (plane 2) in float; the integer counts come from the parallel pass's part[] (exact in any
-// order).
-__global__ __launch_bounds__(128) void k_err_seq(SeqTerms T, long long band, const double* part,
+// Depth.cpp:2178-2186, 2207-2210 in the reference's order, three waves per panorama: mse (plane
+// 0) and mselog (plane 3) through the double square, one wave each; mae (plane 1) and mre (plane
+// 2) in float, lanes 0 and 1 of the third; the integer counts come from the parallel pass's
+// part[] (exact in any order).
+__global__ __launch_bounds__(192) void k_err_seq(SeqTerms T, long long band, const double* part,
                                                  int nblk, const Align* al, pf_metrics* out,
                                                  int force)
 {
-    __shared__ float lds[2][2 * 2 * SPS];
-    __shared__ float accb[2 * SCH];
+    __shared__ float lds_sq[2][2 * SPS];
+    __shared__ float lds_pl[2 * 2 * SPS];
     __shared__ float res[4];
     const int b = blockIdx.x, lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     const float* pl = T.t + (long long)b * 4 * T.bandp;
-    if (wv == 0) {
-        const int pid[2] = {0, 3};
-        const float r = seq_chain<2, true>(pl, band, T.bandp, pid, lds[0], accb, nullptr, force);
-        if (lane < 2) res[lane == 0 ? 0 : 3] = r;
+    if (wv < 2) {
+        const int pid[1] = {wv == 0 ? 0 : 3};
+        const float r = seq_chain<1, true>(pl, band, T.bandp, pid, lds_sq[wv], nullptr, force);
+        if (lane == 0) res[wv == 0 ? 0 : 3] = r;
     } else {
         const int pid[2] = {1, 2};
-        const float r = seq_chain<2, false>(pl, band, T.bandp, pid, lds[1], nullptr, nullptr);
+        const float r = seq_chain<2, false>(pl, band, T.bandp, pid, lds_pl, nullptr);
         if (lane < 2) res[lane + 1] = r;
     }
     __syncthreads();
@@ -857,7 +844,7 @@ void launch_metrics(hipStream_t s, const MetricsJob& j, void* ws, pf_metrics* ou
         if (j.sequential) {
             hipLaunchKernelGGL(k_seq_terms<false>, grid, dim3(MB), 0, s, c, j.align_way, ac, Tc,
                                band);
-            hipLaunchKernelGGL(k_err_seq, dim3(nb), dim3(128), 0, s, Tc, band, pc, MNBLK, ac,
+            hipLaunchKernelGGL(k_err_seq, dim3(nb), dim3(192), 0, s, Tc, band, pc, MNBLK, ac,
                                out + b0, seq_force);
         } else {
             hipLaunchKernelGGL(k_err_final, dim3(nb), dim3(MB), 0, s, pc, MNBLK, ac, out + b0);
