@@ -220,14 +220,16 @@ def c5_measure(args, rank, world, local, dev, steps, warmup):
 
     logs = []
     be0 = pf_dist.HipRowShardBackend(fz, emap, tiles, coeffs, out_w, zr, out.view(-1))
-    rep = args.c5_rep if args.c5_rep >= 0 else pf_dist.auto_rep_levels(be0, nlevels, world)
+    comm = pf_dist.TorchComm(dist, stage_host=args.backend == "gloo") if world > 1 else None
+    # one choice for all ranks (rank 0's): the plans behind it depend on per-process state
+    rep = args.c5_rep if args.c5_rep >= 0 else pf_dist.auto_rep_levels(be0, nlevels, world,
+                                                                        comm=comm)
 
     def step():
         if fs is not None:
             mine = tiles[:, off0:off1]
             fs.warp_depth(gt, mine, resp)
             fs.register(emap, mine, zr, degree=3, apply=False, coeffs=coeffs[t0:t1][None])
-        comm = pf_dist.TorchComm(dist, stage_host=args.backend == "gloo") if world > 1 else None
         if args.c5_shard == "rows":  # be0 keeps the per-level geometry across panoramas
             logs.append(pf_dist.ExchangeLog())
             pf_dist.fuse_row_sharded(be0, nlevels, lay.ntiles, rank, world, comm, logs[-1],
@@ -380,7 +382,7 @@ def c5_rehearsal(fz, lay, gt, emap, resp_all, coeffs, tiles, out, out_w, zr, nle
                                                    "max_rank_bytes", "total_bytes", "rounds")}}
 
 
-def run_c5(args, rank, world, local, dev):
+def run_c5(args, rank, world, local, dev, dist_on=False, comm_res=None):
     """bench.py --mode c5: the C5 line (c5_measure) on `world` ranks."""
     import torch.distributed as dist
     r = c5_measure(args, rank, world, local, dev, args.steps, args.warmup)
@@ -408,8 +410,9 @@ def run_c5(args, rank, world, local, dev):
             "one_call_ms": r["one_call_ms"],
             "rep_levels": r["rep_levels"],
             "backend": args.backend if world > 1 else None,
+            "comm_check": comm_res,
             "elapsed_rank0_s": mine_s}), flush=True)
-    if world > 1:
+    if dist_on:
         dist.barrier()
         dist.destroy_process_group()
     if rank == 0 and not bit_exact:
@@ -609,6 +612,53 @@ def timed_steps(step, sync, args, world, dist, device=None):
     return mine, elapsed
 
 
+def init_dist(args, world, local):
+    """torch.distributed for this process.  Under a launcher (WORLD_SIZE in the environment) the
+    process group is created at EVERY world size -- world 1 included, so the RCCL init path of the
+    N-GPU runs (`init_process_group("nccl", device_id=...)`) and TorchComm's device-tensor branch
+    are exercised on a one-GPU box too (tests/test_gpu_rccl.py); run without a launcher at N = 1
+    nothing is created.  Returns True when a process group exists."""
+    import torch
+    import torch.distributed as dist
+    if "WORLD_SIZE" not in os.environ:
+        return False
+    if args.backend == "nccl":
+        dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local}"))
+    else:
+        dist.init_process_group("gloo")
+    return True
+
+
+def comm_check(dist, dev, rank, world, stage_host):
+    """One call of every pf_dist.TorchComm collective the sharded C5 flow uses, on device tensors,
+    checked against the values every rank can predict: all_reduce_sum, agree (rank 0's plan, on
+    `dev`), the int16 broadcast (travels as bytes), and a ring exchange (isend / irecv pairs; a
+    rank exchanges with itself only at world 1, where it is skipped).  The RCCL (device) branch
+    runs with stage_host=False; gloo rehearsals stage through the host."""
+    import torch
+    import pf_dist
+    comm = pf_dist.TorchComm(dist, stage_host=stage_host)
+    res = {"backend": dist.get_backend(), "world": world, "stage_host": stage_host}
+    a = torch.full((257,), float(rank + 1), dtype=torch.float32, device=dev)
+    comm.all_reduce_sum(a)
+    res["all_reduce_sum"] = bool(torch.all(a == world * (world + 1) / 2).item())
+    got = comm.agree([10 + rank, 7, 10], 0, dev)
+    res["agree"] = got == [10, 7, 10]
+    b = torch.arange(1000, dtype=torch.int16, device=dev) * (1 if rank == 0 else 0) - 500
+    comm.broadcast(b, 0)
+    res["broadcast_i16"] = bool(torch.equal(b.cpu(), torch.arange(1000, dtype=torch.int16) - 500))
+    if world > 1:
+        nxt, prv = (rank + 1) % world, (rank - 1) % world
+        snd = torch.full((4096,), float(rank), dtype=torch.float32, device=dev)
+        rcv = torch.empty_like(snd)
+        comm.exchange([(nxt, snd)], [(prv, rcv)])
+        res["exchange"] = bool(torch.all(rcv == float(prv)).item())
+    torch.cuda.synchronize(dev) if dev.type == "cuda" else None
+    res["ok"] = all(v for k, v in res.items() if k in ("all_reduce_sum", "agree", "broadcast_i16",
+                                                      "exchange"))
+    return res
+
+
 def _free_port():
     import socket
     s = socket.socket()
@@ -707,15 +757,14 @@ def main():
     elif torch.cuda.device_count() <= local:
         sys.exit(f"bench.py: rank {rank} wants cuda:{local}, "
                  f"{torch.cuda.device_count()} device(s) visible")
-    if world > 1:
-        if args.backend == "nccl":
-            dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local}"))
-        else:
-            dist.init_process_group("gloo")
+    dist_on = init_dist(args, world, local)
     torch.cuda.set_device(local)
     dev = torch.device(f"cuda:{local}")
+    comm_res = comm_check(dist, dev, rank, world, args.backend == "gloo") if dist_on else None
+    if comm_res is not None and not comm_res["ok"]:
+        sys.exit(f"rank {rank}: TorchComm self-check failed: {comm_res}")
     if args.mode == "c5":
-        return run_c5(args, rank, world, local, dev)
+        return run_c5(args, rank, world, local, dev, dist_on, comm_res)
 
     out_w, ew = 2048, 512
     lay = PL.config_layout("C2")
@@ -958,13 +1007,16 @@ def main():
             "c2_batch1": c2,
             "c5_one_gpu": c5,
             "backend": args.backend if world > 1 else None,
+            # every TorchComm collective once on device tensors (RCCL under a launcher, even at
+            # world 1): init_dist / comm_check
+            "comm_check": comm_res,
             "per_rank": per_rank if world > 1 else None,
             "sample_pano": per_rank[0]["sample"],
         }
         if not args.no_cpu_baseline and world == 1:  # the contract: rank 0 at N = 1 only
             line["cpu_baseline"] = cpu_baseline(args.cpu_seconds)
         print(json.dumps(line), flush=True)
-    if world > 1:
+    if dist_on:
         dist.barrier()
         dist.destroy_process_group()
     if not bit_exact_all:

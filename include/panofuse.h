@@ -307,15 +307,15 @@ int pf_error_metrics(pf_ctx* ctx, const float* gt, int gw, int gh, int gc, const
                      const uint16_t* given16, int w, int h, int given_c, int batch, float zr0,
                      float zr1, int align_way, int cap_depth, pf_metrics* out);
 /* Summation order of the means (mse, mae, mre, mselog) and of the least-squares sums:
- *   PF_METRICS_TREE (default) -- fp64 partial sums in a fixed tree: deterministic, 1.1 ms per
- *     64 panoramas at C3, means within 1e-5 relative of exact fp64 sums (and within 1e-2 of
- *     the reference's drifting float sums).
- *   PF_METRICS_SEQUENTIAL -- opt-in "bit-exact means": the reference's order, row-major float
+ *   PF_METRICS_TREE (the C-ABI's default) -- fp64 partial sums in a fixed tree: deterministic,
+ *     0.9 ms per 64 panoramas at C3, means within 1e-5 relative of exact fp64 sums (and within
+ *     1e-2 of the reference's drifting float sums).
+ *   PF_METRICS_SEQUENTIAL -- "bit-exact means": the reference's order, row-major float
  *     accumulators (mse and mselog through a double add, Depth.cpp:2119-2123, 2178-2186);
- *     bit-exact to it.  The per-pixel terms are computed in parallel, one wave per panorama
- *     adds them in order: one dependent add chain, ~24 ms per call at any batch.
- * The facade (include/pf_depth.h) takes PF_METRICS_ORDER=sequential from the environment;
- * panofuse_main has --metrics-order. */
+ *     bit-exact to it (mselog within 1e-5: device log10f).  The per-pixel terms are computed in
+ *     parallel and summed as verified fp32 chains: ~7.8 ms per 64-panorama call at C3.
+ * The facade (include/pf_depth.h) and panofuse_main default to PF_METRICS_SEQUENTIAL, the order
+ * the reference prints; PF_METRICS_ORDER=tree / --metrics-order tree select the tree. */
 #define PF_METRICS_TREE 0
 #define PF_METRICS_SEQUENTIAL 1
 int pf_set_metrics_order(pf_ctx* ctx, int order);

@@ -101,9 +101,9 @@ def test_mode0_cli_end_to_end(tmp_path):
     cmd = [BIN, "0", str(d["rgb"]), str(d["gt"]), str(d["base"]), str(d["result_hohonet"]),
            "--tiles", str(d["tiles"])]
     # one process per shard (as one per GPU): shard 0/2 takes scene01 (metrics in the default
-    # fp64-tree order), 1/2 scene02 (--metrics-order sequential: the reference's float sums)
+    # order: the reference's float sums), 1/2 scene02 (--metrics-order tree: the fp64 tree)
     for k, raw in enumerate(sorted(expected)):
-        order = ["--metrics-order", "sequential"] if k == 1 else []
+        order = ["--metrics-order", "tree"] if k == 1 else []
         r = subprocess.run(cmd + ["--shard", f"{k}/2"] + order, capture_output=True, text=True,
                            timeout=300)
         assert r.returncode == 0, r.stdout + r.stderr
@@ -120,7 +120,7 @@ def test_mode0_cli_end_to_end(tmp_path):
         vals = dict(line.split(": ") for line in txt.strip().splitlines())
         ref_r = O.error_metrics(gt_f, out, ZR, 1, True)
         ref_g = O.error_metrics(gt_f, base_f, ZR, 1, True)
-        seq = raw == sorted(expected)[1]
+        seq = raw == sorted(expected)[0]
         for key, ref in (("result", ref_r), ("given", ref_g)):
             for m in ("mse", "mae", "mre", "mselog"):
                 # sequential: the oracle's float sums up to the file's "%f" printing (and

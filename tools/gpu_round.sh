@@ -13,6 +13,8 @@
 #   c5       the C5 line at world 1 (+ the 8-rank byte model)  -> bench_c5.log
 #   c4       bench.py --gpus 8 on the one GPU (gloo, --same-device): C4's 8-rank shape
 #   rgb      the RGB warp probe (tools/rgb_probe.py)   -> rgb.log
+#   serials  the serial step per variant: $VARIANTS as for ab -> serial_NAME/levels.txt (one trace
+#            each, in $ROUNDS alternating rounds)
 #   ab       A/B of environment knobs: $VARIANTS = "NAME:ENV=VAL,ENV=VAL NAME2:" run in $ROUNDS
 #            alternating rounds on the default bench line (-> ab/NAME.R.log, one summary line
 #            each); BENCH_ARGS adds bench.py flags
@@ -55,6 +57,18 @@ for s in $STEPS; do
       echo "serial rc=$rc"; [ $rc -eq 0 ] || exit $rc
       python3 tools/ktrace_levels.py $(find $OUT/serial/prof -name "run_kernel_trace.csv" | head -1) > $OUT/serial/levels.txt
       tail -12 $OUT/serial/levels.txt ;;
+    serials)
+      for r in $(seq 1 ${ROUNDS:-1}); do
+        for v in ${VARIANTS:-base:}; do
+          name=${v%%:*}; envs=${v#*:}; d=$OUT/serial_$name.$r; rm -rf $d; mkdir -p $d
+          ( for kv in ${envs//,/ }; do [ -n "$kv" ] && export "$kv"; done
+            timeout -k 10 300 rocprofv3 --kernel-trace -d $d/prof -o run --output-format csv -- \
+              python3 bench.py --steps 5 --warmup 2 --no-cpu-baseline --no-extra-configs --pipeline 0 ${BENCH_ARGS:-} > $d/bench.log 2>&1 ); rc=$?
+          [ $rc -eq 0 ] || { echo "$name rc=$rc"; tail -5 $d/bench.log; exit $rc; }
+          python3 tools/ktrace_levels.py $(find $d/prof -name "run_kernel_trace.csv" | head -1) > $d/levels.txt
+          echo "== $name.$r"; cat $d/levels.txt
+        done
+      done ;;
     pmc)
       bash tools/pmc_round.sh; rc=$?; [ $rc -eq 0 ] || exit $rc ;;
     c5)

@@ -45,11 +45,13 @@ pf_ctx* facade_ctx()
         std::cout << "[panofuse] pf_create(" << dev << ") failed: no usable HIP device" << std::endl;
         return nullptr;
     }
-    // ErrorData / ErrorEmap summation order: the fast fp64 tree by default;
-    // PF_METRICS_ORDER=sequential gives the reference's row-major float sums (bit-exact means,
-    // ~24 ms per call: one dependent add chain; panofuse_main --metrics-order sequential)
+    // ErrorData / ErrorEmap summation order: the facade mirrors Depth.cpp, so by default it sums
+    // in the reference's row-major float order (the means the reference prints, bit for bit;
+    // ~7.8 ms per 64-panorama call, well under a millisecond more at the facade's batch 1).
+    // PF_METRICS_ORDER=tree (panofuse_main --metrics-order tree) opts into the fp64 tree.
     const char* mo = std::getenv("PF_METRICS_ORDER");
-    if (mo && std::strcmp(mo, "sequential") == 0) pf_set_metrics_order(c, PF_METRICS_SEQUENTIAL);
+    pf_set_metrics_order(c, mo && std::strcmp(mo, "tree") == 0 ? PF_METRICS_TREE
+                                                                : PF_METRICS_SEQUENTIAL);
     ctxs[dev] = c;
     return c;
 }

@@ -8,9 +8,9 @@
 // Mode 0 = CreateDepthPanoramas (Main.cpp:331-687) minus the OpenGL tile export: the perspective
 // depth tiles are read from --tiles (default "test_images", the reference's LeReS folder) named
 // <raw>.<a0>_<a1>_<z0>_<z1>.<ext>; "auto" takes .jpg when present, else .png (MiDaS naming).
-// --metrics-order: the .aligned.txt means in the fast fp64-tree order (default) or in the
-// reference's row-major float order (sequential: the reference's printed digits, ~24 ms more
-// per ErrorData call).
+// --metrics-order: the .aligned.txt means in the reference's row-major float order (sequential,
+// the default: the digits Main.cpp prints) or in the fp64-tree order (tree: deterministic, within
+// ~1e-3 relative of the reference's float sums).
 #include "../../include/pf_depth.h"
 
 #include <hip/hip_runtime.h>

@@ -543,7 +543,7 @@ __device__ __forceinline__ float sq_step(float acc, float v)
 // else plain float adds.  cnt (all lanes): number of positive terms of plane pid[NPL - 1].
 // SQ (NPL == 1): one squared plane per wave, every lane runs the same chain; lane g keeps the
 // chain's value at the end of GRP-pixel group g of the chunk, so the check is one group per lane
-// (from the previous group's end value, the reference's 16 steps must reach this group's end
+// (from the previous group's end value, the reference's GRP steps must reach this group's end
 // value) with no LDS writes on the chain's path.  Matching group ends make the chunk's result
 // the reference's by induction, whatever the steps inside did.  force (tests): one group per
 // chunk counts as a mismatch, so the exact redo path runs.

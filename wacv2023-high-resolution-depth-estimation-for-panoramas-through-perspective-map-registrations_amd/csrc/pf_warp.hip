@@ -211,6 +211,11 @@ void warp_patches_host(const TileGeom& g, int tile, const uint32_t* wxy, int pw,
             long long nu = 0;
             bool fits = nv <= ph;
             for (int r = 0; r < nv && fits; r++) {
+                if (xlo[r] > xhi[r]) {  // a row no corner reads (adjacent tile pixels jumped
+                    q0[r] = 0;          // 3+ panorama rows near a pole): no units, no arithmetic
+                    off[r] = (int)nu;   // on the untouched INT32_MAX / INT32_MIN bounds
+                    continue;
+                }
                 fits = xhi[r] - xlo[r] + 1 <= pw / 2;
                 const long long a = floor_div(rx + xlo[r], 4), b = floor_div(rx + xhi[r] + 4, 4);
                 q0[r] = (int)a;

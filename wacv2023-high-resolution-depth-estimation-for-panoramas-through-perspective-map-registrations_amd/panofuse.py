@@ -247,8 +247,9 @@ class Fuser:
                                     float(zr[0]), float(zr[1]), _ptr(coeffs), _ptr(out)))
 
     def set_metrics_order(self, order):
-        """"tree" (default): fp64 partial sums (fast, means within 1e-5 of exact sums);
-        "sequential": the reference's float summation order, bit-exact means (~24 ms a call)."""
+        """"tree" (the context's default): fp64 partial sums (fast, means within 1e-5 of exact
+        sums); "sequential": the reference's float summation order, bit-exact means (~7.8 ms per
+        64-panorama call at C3; the facade and panofuse_main default to it)."""
         self._check(self.L.pf_set_metrics_order(self.h, METRICS_ORDERS[order]))
 
     def solve_smoothing(self, tiles, out, zr, coeffs=None):

@@ -546,9 +546,12 @@ def exchange_model(dims, plans, ext, world, multicover=None, rep_levels=0):
     return res
 
 
-def auto_rep_levels(backend, nlevels, world, ratio=10):
+def auto_rep_levels(backend, nlevels, world, ratio=10, comm=None):
     """The coarse levels worth replicating at `world` ranks: the leading levels whose band per
-    rank is under `ratio` halos deep (each of their many short passes would wait for an exchange)."""
+    rank is under `ratio` halos deep (each of their many short passes would wait for an exchange).
+    The pass plans behind the choice depend on per-process state (CU count, occupancy, PF_J*
+    overrides), so with a `comm` every rank takes rank 0's answer: ranks with different rep_levels
+    would build different level geometries and their exchanges would not pair up."""
     if world <= 1:
         return 0
     n = 0
@@ -559,6 +562,8 @@ def auto_rep_levels(backend, nlevels, world, ratio=10):
             n = lv + 1
         else:
             break
+    if comm is not None and hasattr(comm, "agree"):
+        n = comm.agree([n], 0, getattr(backend, "device", None))[0]
     return n
 
 
