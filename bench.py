@@ -96,11 +96,12 @@ def host_cpus():
     return max(1, n)
 
 
-def _oracle_rate(O, PL, pf_synth, threads, seconds, max_panos, out_w=2048, ew=512):
+def _oracle_rate(O, PL, pf_synth, threads, seconds, max_panos, cfg="C2"):
     """Panoramas/s of the oracle pipeline (warp + register + fuse) at `threads` OpenMP threads,
     over at least one panorama and until `seconds` of work or `max_panos` panoramas."""
     O.set_threads(threads)
-    lay = PL.config_layout("C2")
+    lay = PL.config_layout(cfg)
+    out_w, ew = PL.CONFIGS[cfg]
     tiles, total = O.make_tiles(lay)
     done, t_work = 0, 0.0
     while done < 1 or (t_work < seconds and done < max_panos):
@@ -127,9 +128,16 @@ def cpu_baseline(seconds):
     threads = host_cpus()
     v, done, t_work = _oracle_rate(O, PL, pf_synth, threads, seconds, 64)
     v1, done1, t1 = _oracle_rate(O, PL, pf_synth, 1, min(seconds, 5.0), 8)
+    # BASELINE config C1 (the reference's own CPU case, Main.cpp mode 0: one 512x256 panorama,
+    # 6 tiles of 256^2, 128x64 baseline), the same pipeline, a few seconds each
+    c1, n1, s1 = _oracle_rate(O, PL, pf_synth, threads, min(seconds, 3.0), 256, "C1")
+    c11, n11, s11 = _oracle_rate(O, PL, pf_synth, 1, min(seconds, 3.0), 64, "C1")
     return {"value": v, "unit": "panoramas/s", "cores": threads, "kind": "port",
             "nproc": os.cpu_count(), "cpus_usable": threads,
             "value_1core": v1,
+            "c1": {"value": c1, "value_1core": c11, "unit": "panoramas/s",
+                   "sample": f"C1 (512x256, 6 tiles of 256^2): {n1} panoramas in {s1:.1f} s on "
+                             f"{threads} threads, {n11} in {s11:.1f} s on 1"},
             "sample": f"{done} panoramas of C2 (2048x1024, 20 tiles of 512^2): warp + registration"
                       f" + 3-level fusion, {t_work:.1f} s of work, OpenMP {threads} threads "
                       f"(every CPU usable by this process; nproc={os.cpu_count()}); 1 core: "
@@ -419,7 +427,7 @@ def run_c5(args, rank, world, local, dev, dist_on=False, comm_res=None):
         sys.exit("C5: the sharded result differs from the one-GPU fusion")
 
 
-def c2_latency(local, dev, lay, zr, reps=7):
+def c2_latency(local, dev, lay, zr, reps=7, cfg="C2"):
     """BASELINE config C2 -- one 2048x1024 panorama, 20 tiles of 512^2, one GPU -- as a latency:
     warp + registration + fusion of ONE panorama (what MergeDepthMaps times per panorama,
     Depth.cpp:792-808, 907-916), hipEvents on the context's stream around each run, after the
@@ -428,14 +436,16 @@ def c2_latency(local, dev, lay, zr, reps=7):
 
     import panofuse
     import pf_synth
+    import pf_layouts as PL
+    ow, ew = PL.CONFIGS[cfg]
     seeds = pf_synth.seeds_for(1, 424242)
-    gt = pf_synth.scene_depth(seeds, 2048, 1024, dev).contiguous()
-    emap = pf_synth.baseline_emap(seeds, 512, 256, dev).contiguous()
+    gt = pf_synth.scene_depth(seeds, ow, ow // 2, dev).contiguous()
+    emap = pf_synth.baseline_emap(seeds, ew, ew // 2, dev).contiguous()
     resp = panofuse.make_responses(pf_synth.responses(seeds, lay.ntiles), dev)
     f = panofuse.Fuser(local)
     f.set_tiles(lay)
     tiles = torch.empty((1, f.tile_elems), dtype=torch.float32, device=dev)
-    out = torch.empty((1, 1024, 2048), dtype=torch.int16, device=dev)
+    out = torch.empty((1, ow // 2, ow), dtype=torch.int16, device=dev)
     coeffs = torch.empty((1, lay.ntiles, 4), dtype=torch.float32, device=dev)
     times = []
     for i in range(reps + 2):
@@ -449,9 +459,11 @@ def c2_latency(local, dev, lay, zr, reps=7):
             times.append(e0.elapsed_time(e1))
     f.synchronize()
     times.sort()
+    what = {"C2": "C2: one 2048x1024 panorama, 20 tiles of 512^2",
+            "C1": "C1: one 512x256 panorama, 6 tiles of 256^2 (the reference's CPU case)"}[cfg]
     return {"median_ms": times[len(times) // 2], "min_ms": times[0], "reps": reps,
-            "workload": "C2: one 2048x1024 panorama, 20 tiles of 512^2: warp + registration + "
-                        "3-level fusion + u16, hipEvents around each run (median)"}
+            "workload": what + ": warp + registration + 3-level fusion + u16, hipEvents around "
+                               "each run (median)"}
 
 
 def rgb_warp_measure(local, dev, lay, B, reps=7):
@@ -849,6 +861,8 @@ def main():
     rgbw = rgb_warp_measure(local, dev, lay, B) if not args.no_extra_configs else None
     # the other single-GPU BASELINE configs, for the record (outside the timed steps)
     c2 = c2_latency(local, dev, lay, zr) if not args.no_extra_configs else None
+    c1 = (c2_latency(local, dev, PL.config_layout("C1"), zr, cfg="C1")
+          if not args.no_extra_configs else None)
     c5 = None
     if world == 1 and not args.no_extra_configs:
         r5 = c5_measure(args, 0, 1, local, dev, steps=3, warmup=1)
@@ -994,15 +1008,16 @@ def main():
                                            "k_err_sums, k_align, k_err_final), fp64 tree order",
                                  "ms_per_batch": stages["metrics"]["ms_per_step"],
                                  "ms_per_batch_sequential": metrics_seq_ms,
-                                 "sequential": "the reference's float summation order (library "
-                                               "default, bit-exact means): terms in parallel, "
-                                               "one lane per panorama adds them in order"},
+                                 "sequential": "the reference's float summation order (the "
+                                               "facade's and CLI's default, bit-exact means): "
+                                               "terms in parallel, verified fp32 add chains"},
             "nonzero_px_pano0": nz,
             "smoothing_ablation": dict(smooth, note="pf_solve_smoothing (SolveDepthBySmoothing, "
                                        "500 Gauss-Seidel sweeps near tile edges), outside the step"),
             "bit_exact_vs_one_process": bit_exact,
             # every rank's own batch against a fresh one-process fusion (C4: 8 checks)
             "bit_exact_all_ranks": bit_exact_all,
+            "c1_batch1": c1,
             "c2_batch1_ms": c2["median_ms"] if c2 else None,
             "c2_batch1": c2,
             "c5_one_gpu": c5,

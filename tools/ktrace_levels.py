@@ -23,3 +23,22 @@ for (k, g), (c, t) in acc.items():
     tot += t
     print(f"{k:36s} gridx={g:>7s} n={c:3d} total={t:8.1f} us  avg={t / c:7.1f} us")
 print(f"jacobi total {tot:.1f} us")
+# the step's other kernels (warp, registration, targets, border/seed), median over the serial steps
+steps = [rows[warps[i]:warps[i + 1]] for i in range(len(warps) - 1)] if len(warps) > 1 else [rows]
+per = collections.defaultdict(list)
+for st in steps[-5:]:
+    acc2 = collections.defaultdict(float)
+    for r in st:
+        n = r["Kernel_Name"]
+        if not n.split("(")[0].replace("void ", "").startswith("pf::") or "k_jlag" in n or \
+                "k_jres" in n or "k_jpipe" in n:
+            continue
+        acc2[n.split("(")[0].replace("void pf::", "").replace("pf::", "")[:30]] += \
+            (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1000.0
+    for k, v in acc2.items():
+        per[k].append(v)
+for k, v in per.items():
+    if len(v) < 3:  # kernels of the bench's tail (smoothing, checks), not of the steps
+        continue
+    v = sorted(v)
+    print(f"{k:36s} median of {len(v)} steps {v[len(v) // 2]:8.1f} us")

@@ -62,9 +62,13 @@
 #define PF_JDRAIN 1
 #endif
 #ifndef PF_JLAG_WAVES_FAST
-// the packed passes: 3 waves per SIMD (<= 168 VGPRs).  With the drain compiled out (PF_JDRAIN)
-// hipcc's free allocation lands at 168-171 (checked in the ISA); the bound holds it at 168
-#define PF_JLAG_WAVES_FAST 3
+// the packed passes' __launch_bounds__ minimum waves per SIMD.  Round 5: 3 (<= 168 VGPRs; with
+// the drain compiled out hipcc's free allocation lands at 168-171, the bound holds it at 168 and
+// spills 2).  Round 6: 2 (<= 256 VGPRs, no spills) with the row loads issued 3 steps ahead
+// (PF_JLAG_PF) -- serial trace level 1 0.88 -> 0.84 ms, level 2 unchanged at two waves per SIMD
+// instead of three; the two-lane C3 line 17.23-17.28k -> 17.44-17.46k panoramas/s (two
+// alternating rounds on one MI355X, tools/gpu_round.sh ab)
+#define PF_JLAG_WAVES_FAST 2
 #endif
 #ifndef PF_JDRAIN_BIN
 #define PF_JDRAIN_BIN 0
@@ -76,7 +80,7 @@
 #define PF_JPIPE_FILL 3  // fill groups of the pipelined engine (PF_JFILL = -1)
 #endif
 #ifndef PF_JLAG_PF
-#define PF_JLAG_PF 2  // steps of lead for the input and L row loads (1 or 2)
+#define PF_JLAG_PF 3  // steps of lead for the input and L row loads (round 5: 2)
 #endif
 #ifndef PF_JLREG_T
 // passes of depth <= this keep their L ring in registers instead of LDS.  Round 4: at T = 10 the

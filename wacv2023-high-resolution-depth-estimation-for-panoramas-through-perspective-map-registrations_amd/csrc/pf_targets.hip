@@ -166,9 +166,9 @@ __device__ __forceinline__ void targets_patch(const TileGeom* __restrict__ geom,
                                               const float* __restrict__ coeffs, const LevelDims& L,
                                               int npx, int pid, int bgrp,
                                               float* __restrict__ lnorm, long long lstride,
-                                              int batch, float (*sv)[kTG],
+                                              int batch, float (*sv0)[kTG],
                                               const uint32_t* __restrict__ tmask = nullptr,
-                                              int nmw = 0)
+                                              int nmw = 0, float (*sv1)[kTG] = nullptr)
 {
     const int X0 = (pid % npx) * kTPW, Y0 = L.h0 + (pid / npx) * kTPH;
     const int t = threadIdx.x;
@@ -184,8 +184,13 @@ __device__ __forceinline__ void targets_patch(const TileGeom* __restrict__ geom,
     }
     const int X1 = min(X0 + kTPW - 1, L.w - 1), Y1 = min(Y0 + kTPH - 1, L.h1);
     // one tile's contribution to the patch (tiles come in index order: the reference's
-    // accumulation order)
-    auto tile = [&](const int p) {
+    // accumulation order); `last`: no staging follows, so no barrier after the stencils
+    // sv1 (PF_TGT_DBUF): tiles alternate between two staging buffers, so a tile's staging never
+    // overwrites what the previous tile's stencils read and one barrier per tile suffices
+    int nt = 0;
+    auto tile = [&](const int p, const bool last) {
+        float (*sv)[kTG] = (sv1 && (nt & 1)) ? sv1 : sv0;
+        nt++;
         const TileBox bx = box[p];
         const TapBox B = tb[p];
         const long long toff = geom[p].off;
@@ -237,19 +242,21 @@ __device__ __forceinline__ void targets_patch(const TileGeom* __restrict__ geom,
                 n[j]++;
             }
         }
-        __syncthreads();
+        if (!last && !sv1) __syncthreads();  // the next tile's staging overwrites sv
     };
     if (tmask) {  // the host's list of the tiles whose box meets this patch, as mask words
+        int left = 0;  // tiles still to come (block-uniform)
+        for (int w = 0; w < nmw; w++) left += __builtin_popcount(tmask[(long long)pid * nmw + w]);
         for (int w = 0; w < nmw; w++) {
             uint32_t m = tmask[(long long)pid * nmw + w];  // block-uniform
             while (m) {
-                tile(w * 32 + __builtin_ctz(m));
+                tile(w * 32 + __builtin_ctz(m), --left == 0);
                 m &= m - 1;
             }
         }
     } else {
         for (int p = 0; p < ntiles; p++)
-            if (box_meets(box[p], X0, X1, Y0, Y1)) tile(p);  // block-uniform
+            if (box_meets(box[p], X0, X1, Y0, Y1)) tile(p, false);  // block-uniform
     }
 #pragma unroll
     for (int j = 0; j < kTPP; j++) {
@@ -311,6 +318,9 @@ __global__ void __launch_bounds__(256) k_targets_patch(const TileGeom* __restric
 // finest level's patches come first, then each coarser level's patches of the same band (a host
 // table of (level, patch) entries).  The XCD-contiguous mapping gives every XCD a contiguous run
 // of the table, so a band's lines are re-read from its L2 / the MALL instead of HBM.
+#ifndef PF_TGT_DBUF
+#define PF_TGT_DBUF 0  // two staging buffers, one barrier per covering tile (A/B)
+#endif
 template <bool XFORM, int NB>
 __global__ void __launch_bounds__(256) k_targets_multi(const TileGeom* __restrict__ geom,
                                                        int ntiles, const float* __restrict__ tiles,
@@ -319,13 +329,14 @@ __global__ void __launch_bounds__(256) k_targets_multi(const TileGeom* __restric
                                                        TgtMulti M, const int2* __restrict__ order,
                                                        int batch)
 {
-    __shared__ float sv[NB][kTG];
+    __shared__ float sv[PF_TGT_DBUF ? 2 * NB : NB][kTG];
     const unsigned lb = xcd_remap(blockIdx.x, gridDim.x);
     const int e = (int)(lb % (unsigned)M.nentries), bgrp = (int)(lb / (unsigned)M.nentries);
     const int2 ent = order[e];  // (level, patch)
     const TgtLevel& T = M.lv[ent.x];
     targets_patch<XFORM, NB>(geom, T.box, T.tb, ntiles, T.map, tiles, tstride, coeffs, T.L, T.npx,
-                         ent.y, bgrp, T.lnorm, T.lstride, batch, sv, T.tmask, T.nmw);
+                         ent.y, bgrp, T.lnorm, T.lstride, batch, sv, T.tmask, T.nmw,
+                         PF_TGT_DBUF ? sv + NB : nullptr);
 }
 
 int targets_patch_w() { return kTPW; }

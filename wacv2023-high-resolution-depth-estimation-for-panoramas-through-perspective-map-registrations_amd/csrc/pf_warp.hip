@@ -38,7 +38,7 @@ namespace pf {
 #define PF_WARP_WB 256
 #endif
 #ifndef PF_WARP_PATCH
-#define PF_WARP_PATCH 32
+#define PF_WARP_PATCH 64
 #endif
 #ifndef PF_WARP_WAVEBOX
 // one 32x8 patch per WAVE with its own LDS box and no workgroup barrier (waves drift and overlap
@@ -51,7 +51,15 @@ namespace pf {
 #endif
 static constexpr int kWB = PF_WARP_WB;                  // threads per block
 static constexpr int kPatch = PF_WARP_PATCH;            // patch width in tile pixels
-static constexpr int kPatchH = PF_WARP_WAVEBOX ? 8 : kPatch;  // patch height
+#ifndef PF_WARP_PATCHH
+// Round 6: 64 x 32 patches (2048 pixels, 8 per thread) instead of 32 x 32.  Their ragged
+// footprints touch 37.9 cache lines per 1024 tile pixels instead of 47.4 (a host model of every
+// C3 patch; the footprint rows are longer, so fewer partial lines at the row ends): serial trace
+// 0.491-0.494 -> 0.478-0.481 ms per C3 launch; 64 x 16: 0.496-0.499 (46.2 lines); 64 x 32 with
+// 512 threads 0.481-0.484; 128 x 16 with 512 threads 0.478-0.481 (tools/gpu_round.sh serials)
+#define PF_WARP_PATCHH 32
+#endif
+static constexpr int kPatchH = PF_WARP_WAVEBOX ? 8 : PF_WARP_PATCHH;  // patch height
 static_assert(kWB % kPatch == 0 && kPatch * kPatchH % kWB == 0, "whole patch rows per slot");
 static_assert(!PF_WARP_WAVEBOX || (kPatch == 32 && kWB == 256), "wave boxes: 32x8 patches");
 static constexpr int kPx = kPatch * kPatchH / kWB;      // pixels per thread (prep passes)
@@ -180,6 +188,14 @@ void warp_patches_host(const TileGeom& g, int tile, const uint32_t* wxy, int pw,
                        uint32_t* loc)
 {
     const int cap = kCap / 4;  // 16-B units per staged footprint
+    // PF_WARP_ALIGN=n (A/B): each footprint row's units start and end on
+    // n-unit boundaries (8 = whole 128-B lines), so the 64 16-B loads of a wave instruction touch
+    // whole lines; the LDS box grows by the rounding
+    static const int align = [] {
+        const char* e = getenv("PF_WARP_ALIGN");
+        const int a = e ? atoi(e) : 1;
+        return a == 2 || a == 4 || a == 8 ? a : 1;
+    }();
     std::vector<int> xlo, xhi, q0, off;
     for (int Y0 = 0; Y0 < g.h; Y0 += kPatchH)
         for (int X0 = 0; X0 < g.w; X0 += kPatch) {
@@ -217,7 +233,11 @@ void warp_patches_host(const TileGeom& g, int tile, const uint32_t* wxy, int pw,
                     continue;
                 }
                 fits = xhi[r] - xlo[r] + 1 <= pw / 2;
-                const long long a = floor_div(rx + xlo[r], 4), b = floor_div(rx + xhi[r] + 4, 4);
+                long long a = floor_div(rx + xlo[r], 4), b = floor_div(rx + xhi[r] + 4, 4);
+                if (align > 1 && pw % (4 * align) == 0) {  // whole aligned groups of units
+                    a = floor_div(a, align) * align;
+                    b = floor_div(b + align - 1, align) * align;
+                }
                 q0[r] = (int)a;
                 off[r] = (int)nu;
                 nu += b - a;
@@ -628,6 +648,93 @@ __device__ __forceinline__ void warp_staged(float* box, float* xbuf, const RespK
     }
 }
 
+#ifndef PF_WARP_DMA
+// 1: ragged footprints of <= 2 units per thread are staged by LDS-DMA (global_load_lds_dwordx4:
+// each 16-B unit lands in LDS with no VGPR round trip and no ds_write), in three LDS buffers with
+// two panoramas in flight, counted vmcnt waits and raw barriers
+#define PF_WARP_DMA 0
+#endif
+#if PF_WARP_DMA
+typedef __attribute__((address_space(1))) const void* gptr_t;
+typedef __attribute__((address_space(3))) void* lptr_t;
+template <int NS, bool RESP>
+__device__ __forceinline__ void warp_dma(float* box, const RespK* rk, const WarpPatch& P, int t,
+                                         const WarpLanes& W, const float* __restrict__ pano,
+                                         long long pstride, float* __restrict__ tiles,
+                                         long long tstride, int bbeg, int nb,
+                                         const uint32_t* __restrict__ unit_tbl)
+{
+    constexpr int BUF = NS * kWB * 4;  // floats per buffer: unit e at [4e, 4e + 4)
+    static_assert(3 * BUF <= 2 * kCap, "three buffers fit the box");
+    static_assert(!PF_WARP_ROWPX && !PF_WARP_XPOSE, "kPx tile stores per panorama");
+    const int units = P.units;
+    uint32_t gofl[NS];  // float offset (in one panorama) of unit t + s*kWB
+#pragma unroll
+    for (int s = 0; s < NS; s++) {
+        const int e = t + s * kWB;
+        gofl[s] = unit_tbl[P.uoff + (e < units ? e : units - 1)] >> 2;
+    }
+    const int wv = t >> 6;
+    auto dma = [&](int buf, int q) {
+        const float* pp = pano + (long long)(bbeg + (q < nb ? q : nb - 1)) * pstride;
+#pragma unroll
+        for (int s = 0; s < NS; s++)  // wave-uniform destination, lane l at +16 l bytes
+            __builtin_amdgcn_global_load_lds((gptr_t)(pp + gofl[s]),
+                                             (lptr_t)(box + buf * BUF + (s * kWB + wv * 64) * 4),
+                                             16, 0, 0);
+    };
+    dma(0, 0);
+    dma(1, 1);
+    for (int q = 0; q < nb; q++) {
+        // panorama q's units are in: every VMEM op issued after them is panorama q+1's NS loads
+        // and panorama q-1's kPx tile stores (they retire in issue order)
+        if (q == 0) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NS) : "memory");
+        else asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NS + kPx) : "memory");
+        __builtin_amdgcn_s_barrier();  // every wave's units of q landed; q-1's reads are done
+        dma((q + 2) % 3, q + 2);       // into the buffer panorama q-1 was read from
+        const float* L = box + (q % 3) * BUF;
+        const int b = bbeg + q;
+        const auto orr = rsrc(tiles + b * tstride, (uint32_t)(tstride * 4));
+        f2 al{}, ka{}, be{}, si{};
+        uint32_t key = 0;
+        if (RESP) {
+            const RespK r = rk[q];
+            al = f2{r.alpha, r.alpha}; ka = f2{r.kappa, r.kappa};
+            be = f2{r.beta, r.beta}; si = f2{r.sigma, r.sigma};
+            key = r.key;
+        }
+        float out[kPx];
+#pragma unroll
+        for (int k = 0; k < kPx; k += 2) {
+            f2 v;
+#pragma unroll
+            for (int j = 0; j < 2; j++) {
+                const float* c = L + (W.la[k + j] & 0xFFFFu);
+                const float* c2 = L + (W.la[k + j] >> 16);
+                v[j] = bilinear(f2{c[0], c[1]}, f2{c2[0], c2[1]}, W.wx[k + j], W.wy[k + j]);
+            }
+            if (RESP) {
+                const f2 u = f2{noise_top24(W.hp[k], key), noise_top24(W.hp[k + 1], key)};
+                const f2 nz = __builtin_elementwise_fma(u, f2{0x1p-23f, 0x1p-23f},
+                                                        f2{-1.0f, -1.0f});
+                f2 tt = al * v;
+                tt = tt + (ka * v) * v;
+                tt = tt + be;
+                v = pk_add_clamp01(tt, si * nz);
+            }
+            out[k] = v[0];
+            out[k + 1] = v[1];
+        }
+#pragma unroll
+        for (int k = 0; k < kPx; k++)
+            __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(out[k]), orr, (int)W.oo[k], 0,
+                                                  PF_WARP_STPOL);
+    }
+    // no LDS-DMA may land after the workgroup ends (the duplicate loads past the chunk)
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+#endif
+
 template <int NS, bool V4, bool RAG = false>
 __device__ __forceinline__ void warp_staged_sel(bool resp, float* box, float* xbuf,
                                                 const RespK* rk,
@@ -659,7 +766,9 @@ k_warp_depth(const TileGeom* __restrict__ geom,
                                                     float* __restrict__ tiles,
                                                     long long tstride, int batch)
 {
-    __shared__ float box[2 * kCap];
+    // one LDS object: the staging box, then the per-panorama response keys (a second __shared__
+    // object beside an LDS-DMA target makes hipcc wait vmcnt(0) before every box read)
+    __shared__ float box[2 * kCap + kNB * (int)(sizeof(RespK) / sizeof(float))];
     // XCD-contiguous runs of patches; the host sorts the patches by panorama footprint, so the
     // blocks resident on one XCD stage overlapping boxes and re-read each other's lines from L2
     const unsigned lb = xcd_remap(blockIdx.x, gridDim.x);
@@ -735,11 +844,22 @@ k_warp_depth(const TileGeom* __restrict__ geom,
 #endif
 #pragma unroll
     for (int k = 0; k < kPx; k++) W.la[k] *= PF_WARP_SPLIT ? 1 : 2;  // parity-interleaved box
-    __shared__ RespK rk[kNB];  // published by the first barrier inside warp_staged
+    RespK* const rk = reinterpret_cast<RespK*>(box + 2 * kCap);  // published by the first barrier
     if (t < nb) rk[t] = resp_key(resp, bbeg + t, ntiles, P.tile);
     const bool rs = resp != nullptr;
     if (PF_WARP_V4 && PF_WARP_SPLIT && P.units > 0) {  // ragged footprint (warp_patches_host)
         const int nq = (P.units + kWB - 1) / kWB;  // uniform: 16-B loads per thread
+#if PF_WARP_DMA
+        if (nq <= 2) {
+            if (nq <= 1) {
+                if (rs) warp_dma<1, true>(box, rk, P, t, W, pano, pstride, tiles, tstride, bbeg, nb, unit_tbl);
+                else warp_dma<1, false>(box, rk, P, t, W, pano, pstride, tiles, tstride, bbeg, nb, unit_tbl);
+            } else {
+                if (rs) warp_dma<2, true>(box, rk, P, t, W, pano, pstride, tiles, tstride, bbeg, nb, unit_tbl);
+                else warp_dma<2, false>(box, rk, P, t, W, pano, pstride, tiles, tstride, bbeg, nb, unit_tbl);
+            }
+        } else
+#endif
         if (nq <= 1) warp_staged_sel<1, true, true>(rs, box, xbuf, rk, P, t, W, pano, pw, ph, pstride,
                                                     tiles, tstride, bbeg, nb, unit_tbl);
         else if (nq <= 2) warp_staged_sel<2, true, true>(rs, box, xbuf, rk, P, t, W, pano, pw, ph,
