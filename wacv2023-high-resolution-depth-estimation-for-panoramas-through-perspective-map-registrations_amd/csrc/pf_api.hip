@@ -895,7 +895,12 @@ static int check_emap(pf_ctx* c, const float* emap, int ew, int eh, int ec)
 // cost model of plan_level().  Env overrides for tuning runs: PF_JT (largest T), PF_JOVH (per-step
 // overhead in update units), PF_JC=4 (4 columns per lane, builds with PF_JACOBI_C4 only).
 struct JacobiTuning {
-    int C = 2, Tmax = 10;  // PF_JC=0: per level, the cheaper of 2 and 4 by the cost model
+    // columns per lane: 2 (default); PF_JC=3 / 4 force those forms, PF_JC=0 lets the cost model
+    // pick per level.  Round 6 measured C = 3 (192-column strips, 10 % less halo at level 1, 5 %
+    // at level 2, but its L ring in LDS and 224 VGPRs: two waves per SIMD) slower on MI355X: T10
+    // passes 100-103 / 343-355 us at levels 1 / 2 against 92 / 296 us for C = 2 (serial C3 trace),
+    // and the cost model, which does not see that, would pick it (with T8 / T5 passes: 4.2 ms)
+    int C = 2, Tmax = 10;
     double step_overhead = 3.0, lone_cycles = 4.0;  // swept on MI355X (profiles/r02/jacobi; recipe: tools/gpu_round.sh ab)
     double c4_eff = 23.0 / 26.0;  // packed C=4 issue per pixel-update relative to C=2
     double pipe_overhead = 1.0;   // pipelined engine: barrier + exchange per step, update units
@@ -909,7 +914,7 @@ struct JacobiTuning {
 static JacobiTuning jacobi_tuning()
 {
     JacobiTuning t;
-    if (const char* e = getenv("PF_JC")) t.C = atoi(e) == 4 ? 4 : (atoi(e) == 0 ? 0 : 2);
+    if (const char* e = getenv("PF_JC")) t.C = atoi(e) == 4 ? 4 : (atoi(e) == 3 ? 3 : (atoi(e) == 0 ? 0 : 2));
     if (const char* e = getenv("PF_JC4EFF")) t.c4_eff = atof(e);
     if (const char* e = getenv("PF_JT")) t.Tmax = atoi(e);
     if (const char* e = getenv("PF_JOVH")) t.step_overhead = atof(e);
@@ -925,6 +930,10 @@ static JacobiTuning jacobi_tuning()
 // they run in ceil(waves / resident) rounds, so the pass costs ~ rounds * steps * (T + o) with o
 // the per-step overhead (loads, LDS ring, store) in update units.  Whole rounds matter: at the
 // small levels a "one wave per slot" grid left the last round 20-80% empty.
+// The halo columns of a strip on each side: T, rounded up to C for the even forms so each lane's
+// C-vector (and the one vector store per lane) stays aligned; the C == 3 form stores per column.
+static int strip_halo(int T, int C) { return C == 3 ? T : (T + C - 1) / C * C; }
+
 struct PassPlan {
     int T = 1, nchunks = 1;
     int stages = 1;  // > 1: the pipelined engine (k_jpipe), T/stages levels per wave
@@ -937,12 +946,12 @@ static PassPlan best_chunks(int T, int C, int band_rows, int w, int batch, int p
     // VALU work of one step of one wave in update units: T/stages levels of C updates, per-update
     // issue of the C form
     const double lv = (double)T / stages;
-    const double work = C == 4 ? lv * 2.0 * c4_eff : lv;
+    const double work = C == 4 ? lv * 2.0 * c4_eff : (C == 3 ? lv * 1.5 : lv);
     PassPlan best;
     best.T = T;
     best.stages = stages;
     best.cost = 1e300;
-    const int Tp = (T + C - 1) / C * C;
+    const int Tp = strip_halo(T, C);
     const long long per = (long long)((w + 64 * C - 2 * Tp - 1) / (64 * C - 2 * Tp)) * batch;
     const long long slots = (long long)per_simd * nsimd;
     for (int n = 1; n <= band_rows; n++) {
@@ -996,12 +1005,18 @@ static std::vector<PassPlan> plan_level(pf_ctx* c, const LevelDims& L, int C, in
     if (fast && C == 2 && pmode == 1)  // forced: the single-wave engine only where no pipe fits
         for (int T : menu)
             if (opt[T].stages == 1) opt[T].cost *= 1e6;
+    // tuning runs: PF_JTONLY<w>=T restricts the level of width w to depth-T passes (and depths 1
+    // and 2 for a remainder)
+    char tkey[32];
+    snprintf(tkey, sizeof(tkey), "PF_JTONLY%d", L.w);
+    const int tonly = getenv(tkey) ? atoi(getenv(tkey)) : 0;
     std::vector<double> dp(L.iters + 1, 1e300);
     std::vector<int> choice(L.iters + 1, 1);
     dp[0] = 0;
     for (int r = 1; r <= L.iters; r++)
         for (int T : menu) {
             if (T > r || T > tcap || !jstream_supported_T(T)) continue;
+            if (tonly && T != tonly && T > 2) continue;
             const double v = dp[r - T] + opt[T].cost + tune.launch_cost;
             if (v < dp[r]) {
                 dp[r] = v;
@@ -1220,16 +1235,22 @@ static float* run_jacobi(pf_ctx* c, const LevelDims& L, int first, const float* 
     // 4 columns per lane (packed form only): fewer DPP moves and pair assemblies per pixel and a
     // wider strip per halo; 2 keeps more waves resident.  The cost model picks per level.
     const bool c4ok = jstream_supported_C(4, fast) && L.w % 4 == 0 && L.w >= 512;
+    // 3 columns per lane (packed form): a 192-column strip, so the 2T-column halo is a smaller
+    // share than in the 128-column strips of C = 2 (L.w >= 192 + 2T: jacobi_tcap's bound)
+    const bool c3ok = jstream_supported_C(3, fast) && L.w >= 256;
     int C = 2;
     std::vector<PassPlan> plan = plan_level(c, L, 2, jacobi_tcap(L), batch, fast);
-    if (c4ok && tune.C != 2) {
-        std::vector<PassPlan> p4 = plan_level(c, L, 4, jacobi_tcap(L), batch, fast);
-        double c2 = 0, c4 = 0;
-        for (const PassPlan& pp : plan) c2 += pp.cost;
-        for (const PassPlan& pp : p4) c4 += pp.cost;
-        if (tune.C == 4 || c4 < c2) {
-            C = 4;
-            plan.swap(p4);
+    double cbest = 0;
+    for (const PassPlan& pp : plan) cbest += pp.cost;
+    for (int cc : {3, 4}) {
+        if (!(cc == 3 ? c3ok : c4ok) || (tune.C != 0 && tune.C != cc)) continue;
+        std::vector<PassPlan> pc = plan_level(c, L, cc, jacobi_tcap(L), batch, fast);
+        double cost = 0;
+        for (const PassPlan& pp : pc) cost += pp.cost;
+        if (tune.C == cc || cost < cbest) {
+            C = cc;
+            cbest = cost;
+            plan.swap(pc);
         }
     }
     JacobiPass P{};
@@ -1263,7 +1284,7 @@ static float* run_jacobi(pf_ctx* c, const LevelDims& L, int first, const float* 
     int pass = 0;
     for (const PassPlan& pp : plan) {
         const int T = pp.T;
-        P.Tp = (T + C - 1) / C * C;  // keeps colbase (and each lane's C-vector) aligned
+        P.Tp = strip_halo(T, C);
         P.V = 64 * C - 2 * P.Tp;
         P.nstrips = (L.w + P.V - 1) / P.V;
         P.rows_per_chunk = (band_rows + pp.nchunks - 1) / pp.nchunks;

@@ -42,6 +42,11 @@
 #ifndef PF_JACOBI_C4P
 #define PF_JACOBI_C4P 0  // packed form at 4 columns per lane
 #endif
+#ifndef PF_JACOBI_C3
+// packed form at 3 columns per lane (round 6; built, bit-exact, measured slower than C = 2 on
+// MI355X: DESIGN.md §3; the planner takes it only under PF_JC=3)
+#define PF_JACOBI_C3 1
+#endif
 #ifndef PF_JLAG_WAVES
 #define PF_JLAG_WAVES 1  // __launch_bounds__ min waves per SIMD of the lagged kernel
 #endif
@@ -62,13 +67,9 @@
 #define PF_JDRAIN 1
 #endif
 #ifndef PF_JLAG_WAVES_FAST
-// the packed passes' __launch_bounds__ minimum waves per SIMD.  Round 5: 3 (<= 168 VGPRs; with
-// the drain compiled out hipcc's free allocation lands at 168-171, the bound holds it at 168 and
-// spills 2).  Round 6: 2 (<= 256 VGPRs, no spills) with the row loads issued 3 steps ahead
-// (PF_JLAG_PF) -- serial trace level 1 0.88 -> 0.84 ms, level 2 unchanged at two waves per SIMD
-// instead of three; the two-lane C3 line 17.23-17.28k -> 17.44-17.46k panoramas/s (two
-// alternating rounds on one MI355X, tools/gpu_round.sh ab)
-#define PF_JLAG_WAVES_FAST 2
+// the packed passes: 3 waves per SIMD (<= 168 VGPRs).  With the drain compiled out (PF_JDRAIN)
+// hipcc's free allocation lands at 168-171 (checked in the ISA); the bound holds it at 168
+#define PF_JLAG_WAVES_FAST 3
 #endif
 #ifndef PF_JDRAIN_BIN
 #define PF_JDRAIN_BIN 0
@@ -80,8 +81,11 @@
 #define PF_JPIPE_FILL 3  // fill groups of the pipelined engine (PF_JFILL = -1)
 #endif
 #ifndef PF_JLAG_PF
-#define PF_JLAG_PF 3  // steps of lead for the input and L row loads (round 5: 2)
+// steps of lead for the input and L row loads: 1 or 2 -- the step loop is unrolled by 6, so the
+// load-buffer period PF + 1 must divide 6 (PF = 3 would need a 12-step unroll)
+#define PF_JLAG_PF 2
 #endif
+static_assert(6 % (PF_JLAG_PF + 1) == 0, "the 6-step unroll needs a load-buffer period dividing 6");
 #ifndef PF_JLREG_T
 // passes of depth <= this keep their L ring in registers instead of LDS.  Round 4: at T = 10 the
 // register ring takes the packed pass from 132 VGPRs + 48 KB of LDS per 4-wave workgroup to
@@ -121,6 +125,11 @@ typedef float f4 __attribute__((ext_vector_type(4)));
 template <>
 struct Row<4> {  // the packed form works on the pairs .lo = columns 0,1 and .hi = columns 2,3
     f4 v;
+};
+typedef float f3 __attribute__((ext_vector_type(3)));
+template <>
+struct Row<3> {  // the packed form works on the pair .xy = columns 0,1 and the scalar .z
+    f3 v;
 };
 
 }  // namespace
@@ -165,6 +174,24 @@ __device__ __forceinline__ float add_scalar(float a, float b)
     asm("v_add_f32 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
     return r;
 }
+__device__ __forceinline__ float mul_scalar(float a, float b)
+{
+    float r;
+    asm("v_mul_f32 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+    return r;
+}
+__device__ __forceinline__ float sub_scalar(float a, float b)
+{
+    float r;
+    asm("v_sub_f32 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+    return r;
+}
+__device__ __forceinline__ float add_clamp01(float a, float b)
+{  // v_add_f32 with the output clamp (the scalar column of the C == 3 form)
+    float r;
+    asm("v_add_f32 %0, %1, %2 clamp" : "=v"(r) : "v"(a), "v"(b));
+    return r;
+}
 // fma(a, b, c) as a plain v_fma_f32 (same reason: two scalar FMAs on the halves of a pair would
 // otherwise become a packed FMA after a pair assembly)
 __device__ __forceinline__ float fma_scalar(float a, float b, float c)
@@ -176,8 +203,10 @@ __device__ __forceinline__ float fma_scalar(float a, float b, float c)
 
 template <int C, int T, int SRC, bool OUT16, bool FAST>
 struct JLag {
-    static_assert(C % 2 == 0, "column pairs: vector stores and the wrap logic assume even C");
-    static_assert(!FAST || C == 2 || C == 4, "the packed form works on column pairs");
+    static_assert(C % 2 == 0 || (C == 3 && FAST),
+                  "column pairs: vector stores and the wrap logic assume even C (C == 3: the "
+                  "packed form with per-column wraps and stores)");
+    static_assert(!FAST || C == 2 || C == 3 || C == 4, "the packed form works on column pairs");
     static constexpr int PF = PF_JLAG_PF, NB = PF_JLAG_PF + 1;
     // ring of R >= 2T+1 rows, R a multiple of 6: the loop body is unrolled over the R/6 groups
     // of 6 steps so every ring slot is a compile-time constant (LDS immediate offsets, no SALU)
@@ -185,7 +214,9 @@ struct JLag {
     // The L ring in registers -- every slot index is a compile-time constant of the unrolled
     // step -- so no LDS store / load latency sits on a step's dependency chain (passes deeper
     // than PF_JLREG_T keep it in LDS: VGPR budget).
-    static constexpr bool LREG = T <= PF_JLREG_T;
+    // (C == 3 keeps it in LDS: its register ring would not fit 256 VGPRs beside the level rings;
+    // 4 waves x 24 rows x 768 B = 72 KB per workgroup, two workgroups per CU)
+    static constexpr bool LREG = C != 3 && T <= PF_JLREG_T;
     Row<C> Lr[LREG ? R : 1];  // LREG: ring slot s = Lr[s]
     Row<C> H[T][3];   // H[t][r % 3] = level t row r
     Row<C> In[NB];    // input row r lands in In[r % NB] (issued at step r + 1 - PF)
@@ -207,6 +238,7 @@ struct JLag {
     const float *src, *prev, *emap, *lnorm;
     float* dst;
     uint16_t* out;
+    __amdgpu_buffer_rsrc_t orsrc;  // C == 3: the output plane (dst, or out with OUT16)
 
     // Row k of a plane: a wave-uniform row pointer (SGPR arithmetic) plus the lane offset, so
     // the loads use the global_load saddr form with no per-lane address math.
@@ -218,6 +250,8 @@ struct JLag {
         if constexpr (C == 2) {
             float2 q = *reinterpret_cast<const float2*>(rp + lo);
             r.v[0] = q.x; r.v[1] = q.y;
+        } else if constexpr (C == 3) {  // 12-B load (4-B aligned)
+            r.v = f3{rp[lo], rp[lo + 1], rp[lo + 2]};
         } else {
             float4 q = *reinterpret_cast<const float4*>(rp + lo);
             r.v[0] = q.x; r.v[1] = q.y; r.v[2] = q.z; r.v[3] = q.w;
@@ -229,6 +263,26 @@ struct JLag {
     {
         if constexpr (SRC == SRC_BUF) {
             return load_row(src, k);
+        } else if constexpr (C == 3) {
+            // a lane's three columns may straddle a row end (xs0 is any multiple of 3 shifted by
+            // the halo): each column wraps on its own, as JLag's pairs do below
+            Row<C> r;
+#pragma unroll
+            for (int j = 0; j < 3; j++) {
+                int xr = xs0 + j, Y = k;
+                if (xr < 0) { xr += w; Y -= 1; }
+                else if (xr >= w) { xr -= w; Y += 1; }
+                float v = 0.0f;
+                if (Y >= 0 && Y < P->h) {
+                    if constexpr (SRC == SRC_UPSAMPLE) {
+                        v = prev[(long long)(Y >> 1) * (w >> 1) + (xr >> 1)];
+                    } else if (Y >= P->h0 && Y <= P->h1) {  // level-0 seed (Depth.cpp:1442-1465)
+                        v = emap[P->erow[Y + 1] + P->ecol[xr + 1]];
+                    }
+                }
+                r.v[j] = v;
+            }
+            return r;
         } else {
             // Virtual column xs0 + j of row k is pixel (xr, Y) with |xs0 + j - xr| < w (the
             // halo is narrower than a row, jacobi_tcap), so the wrap is one compare, no division.
@@ -279,6 +333,7 @@ struct JLag {
             for (int j = 0; j < C; j++) r.v[j] = __builtin_isfinite(r.v[j]) ? r.v[j] : 0.0f;
         }
         if constexpr (C == 2) *reinterpret_cast<float2*>(p) = make_float2(r.v[0], r.v[1]);
+        else if constexpr (C == 3) { p[0] = r.v[0]; p[1] = r.v[1]; p[2] = r.v[2]; }
         else *reinterpret_cast<float4*>(p) = make_float4(r.v[0], r.v[1], r.v[2], r.v[3]);
     }
     // the L ring: row k of the group (slot GB + PH) enters; level t reads row k - 2t
@@ -307,6 +362,8 @@ struct JLag {
         if constexpr (C == 2) {
             float2 q = *reinterpret_cast<const float2*>(p);
             r.v[0] = q.x; r.v[1] = q.y;
+        } else if constexpr (C == 3) {
+            r.v = f3{p[0], p[1], p[2]};
         } else {
             float4 q = *reinterpret_cast<const float4*>(p);
             r.v[0] = q.x; r.v[1] = q.y; r.v[2] = q.z; r.v[3] = q.w;
@@ -460,6 +517,76 @@ struct JLag {
         }
     }
 
+    // FAST form, C == 3: columns 0, 1 are one packed pair (.xy), column 2 (.z) is scalar.  The
+    // cross-lane taps are the W of column 0 (lane - 1's column 2, folded into a v_add_f32_dpp)
+    // and the E of column 2 (lane + 1's column 0, a v_mov_b32_dpp); the rest is in-lane.  Per
+    // three pixels: 7 packed + 12 scalar + 2 DPP ops, the per-pixel issue cost of C == 2 at 1.5x
+    // the columns per strip (so the halo is a smaller share of a strip).
+    template <int PH, int T0, int T1, bool ROWS>
+    __device__ __forceinline__ void sweep_packed_group3(const Row<C>* Lv, Row<C>* nw, int k) const
+    {
+        constexpr int G = T1 - T0;
+        const f2 q = {-0.25f, -0.25f};
+        const f2 reg = {(float)1e-4, (float)1e-4};
+        const f2 reg_ = {1 - (float)1e-4, 1 - (float)1e-4};
+        f2 cur[G];
+        float cz[G];
+        // Lcur = (((W*q + N*q) + b) + S*q) + E*q, q = -1/4, as in sweep_general
+#pragma unroll
+        for (int g = 0; g < G; g++) {
+            const int t = T0 + 1 + g;
+            const f3 c = H[t - 1][slot(PH, 2 * t)].v, n = H[t - 1][slot(PH, 2 * t + 1)].v;
+            cur[g].x = dpp_from_left(c.z) + n.x;  // folds into v_add_f32_dpp
+            cur[g].y = add_scalar(c.x, n.y);
+            cz[g] = add_scalar(c.y, n.z);
+        }
+#pragma unroll
+        for (int g = 0; g < G; g++) {
+            const int t = T0 + 1 + g;
+            const f3 c = H[t - 1][slot(PH, 2 * t)].v;
+            cur[g] = __builtin_elementwise_fma(cur[g], q, c.xy);
+            cz[g] = fma_scalar(cz[g], vq, c.z);
+        }
+#pragma unroll
+        for (int g = 0; g < G; g++) {
+            const int t = T0 + 1 + g;
+            const f3 sv = H[t - 1][slot(PH, 2 * t - 1)].v;
+            cur[g] = __builtin_elementwise_fma(sv.xy, q, cur[g]);
+            cz[g] = fma_scalar(sv.z, vq, cz[g]);
+        }
+#pragma unroll
+        for (int g = 0; g < G; g++) {
+            const int t = T0 + 1 + g;
+            const f3 c = H[t - 1][slot(PH, 2 * t)].v;
+            cur[g].x = fma_scalar(c.y, vq, cur[g].x);
+            cur[g].y = fma_scalar(c.z, vq, cur[g].y);
+            cz[g] = __builtin_fmaf(dpp_from_right(c.x), vq, cz[g]);
+        }
+#pragma unroll
+        for (int g = 0; g < G; g++) {
+            const int t = T0 + 1 + g;
+            const f3 c = H[t - 1][slot(PH, 2 * t)].v;
+            f2 hh = f2{hcol[0], hcol[1]};
+            float hz = hcol[2];
+            if constexpr (ROWS) {
+                const int row = k - 2 * t;
+                const float hr = (row == h0 || row == h1) ? 0.0f : 1.0f;
+                hh = hh * hr;
+                hz = mul_scalar(hz, hr);
+            }
+            cur[g] = __builtin_elementwise_fma(Lv[g].v.xy - cur[g], hh, c.xy);
+            cz[g] = fma_scalar(sub_scalar(Lv[g].v.z, cz[g]), hz, c.z);
+        }
+#pragma unroll
+        for (int g = 0; g < G; g++) {
+            const int t = T0 + 1 + g;
+            const f3 c = H[t - 1][slot(PH, 2 * t)].v;
+            const f2 a = pk_add_clamp01(cur[g] * reg_, c.xy * reg);
+            const float z = add_clamp01(mul_scalar(cz[g], reg_.x), mul_scalar(c.z, reg.x));
+            nw[t - 1].v = f3{a.x, a.y, z};
+        }
+    }
+
     // FAST form (C == 2): the same update on the lane's column pair, stage-wise over groups of
     // PF_JPK_GROUP levels (bounds the live temporaries, i.e. the VGPR count).  The terms that
     // cross lanes are scalar ops: W + N of column 0 is one v_add_f32_dpp (the DPP move folded
@@ -545,6 +672,7 @@ struct JLag {
             Row<C> Lv[TB - TA];
             ring_get_range<GB, PH, TA + 1, TB>(Lv);
             if constexpr (C == 4) sweep_packed_group4<PH, TA, TB, ROWS>(Lv, nw, k);
+            else if constexpr (C == 3) sweep_packed_group3<PH, TA, TB, ROWS>(Lv, nw, k);
             else sweep_packed_group<PH, TA, TB, ROWS>(Lv, nw, k);
         }
     }
@@ -582,6 +710,26 @@ struct JLag {
             if (t >= LA && t <= NA) H[t][slot(PH, 2 * t)] = nw[t - 1];  // idle: keeps its rows
         if constexpr (NA < T) return;  // no stored row before every level runs (fill_from)
         const int j = k - 2 * T;  // final-level row finished this step
+        if constexpr (C == 3) {
+            // the strip edges cut lanes (the halo is not a multiple of 3): a store per column,
+            // each column inside [vlo, vhi) or dropped by the buffer's range check
+            if (j >= r0 && j < r1) {
+                const uint32_t rowb = (uint32_t)(j * w + colbase + lo);  // pixel index
+#pragma unroll
+                for (int p = 0; p < 3; p++) {
+                    const bool in = xs0 + p >= vlo && xs0 + p < vhi;
+                    if constexpr (OUT16) {
+                        const uint32_t qv = (uint32_t)(nw[T - 1].v[p] * 65535.0f);
+                        __builtin_amdgcn_raw_buffer_store_b16((uint16_t)qv, orsrc,
+                                                              in ? (int)(2 * (rowb + p)) : -16, 0, 0);
+                    } else {
+                        __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(nw[T - 1].v[p]), orsrc,
+                                                              in ? (int)(4 * (rowb + p)) : -16, 0, 0);
+                    }
+                }
+            }
+            return;
+        }
         // xs0, vlo, vhi and C are even, so a lane's columns are all inside [vlo, vhi) or all
         // outside: one vector store per lane.
         if (j >= r0 && j < r1 && xs0 >= vlo && xs0 < vhi) {
@@ -758,7 +906,9 @@ struct JLag {
 };
 
 template <int C, int T, int SRC, bool OUT16, bool FAST>
-__global__ void __launch_bounds__(256, FAST ? PF_JLAG_WAVES_FAST : PF_JLAG_WAVES) k_jlag(JacobiPass P)
+// C == 3: two waves per SIMD (its LDS ring allows two 4-wave workgroups per CU anyway)
+__global__ void __launch_bounds__(256, FAST ? (C == 3 ? 2 : PF_JLAG_WAVES_FAST) : PF_JLAG_WAVES)
+k_jlag(JacobiPass P)
 {
     using S_t = JLag<C, T, SRC, OUT16, FAST>;
     const int lane = threadIdx.x & 63;
@@ -796,7 +946,15 @@ __global__ void __launch_bounds__(256, FAST ? PF_JLAG_WAVES_FAST : PF_JLAG_WAVES
     // w-1 -- the seam quirk), whose H is 0; other halo cells get 0 too (never read).
 #pragma unroll
     for (int j = 0; j < C; j++) S.hcol[j] = 0.0f;
-    if constexpr (FAST) {
+    if constexpr (FAST && C == 3) {
+#pragma unroll
+        for (int j = 0; j < 3; j++)
+            if (S.xs0 + j >= 0 && S.xs0 + j < P.w) S.hcol[j] = P.hcol[S.xs0 + j];
+        // range-checked stores: offsets past the plane are dropped (a -16 offset wraps past it)
+        const uint32_t pbytes = (uint32_t)((long long)P.w * P.h * (OUT16 ? 2 : 4));
+        S.orsrc = __builtin_amdgcn_make_buffer_rsrc(OUT16 ? (void*)S.out : (void*)S.dst, 0,
+                                                    (int)pbytes, 0x00020000);
+    } else if constexpr (FAST) {
         // xs0 and w are multiples of C, so the lane's C columns are all inside or all outside
         if (S.xs0 >= 0 && S.xs0 < P.w)
 #pragma unroll
@@ -1309,6 +1467,12 @@ void PF_JCAT(jlag_launch_t, PF_JPART)(hipStream_t s, const JacobiPass& P, int C,
 #endif
         return;  // unreachable: the host checks jstream_supported_C first
     }
+#if PF_JACOBI_C3
+    if (C == 3) {  // packed form only (jstream_supported_C)
+        if (fast) launch_pass_ct<3, T, true>(s, P, batch);
+        return;
+    }
+#endif
     if (fast) launch_pass_ct<2, T, true>(s, P, batch);
     else launch_pass_ct<2, T, false>(s, P, batch);
 }
@@ -1325,6 +1489,9 @@ int PF_JCAT(jlag_waves_t, PF_JPART)(int C, bool fast)
 #endif
         return 4;
     }
+#if PF_JACOBI_C3
+    if (C == 3) return fast ? waves_per_cu_t<3, T, true>() : 4;
+#endif
     return fast ? waves_per_cu_t<2, T, true>() : waves_per_cu_t<2, T, false>();
 }
 #else  // PF_JPART == 0: dispatch, the pipelined engine, the border kernel
@@ -1346,16 +1513,17 @@ static int waves_per_cu_c(int C, int T, bool fast)
 // Resident waves per CU of the pass kernel at depth T (used to size the grid to whole rounds).
 int jstream_waves_per_cu(int C, int T, bool fast)
 {
-    static int cache[2][2][11] = {{{0}}};
+    static int cache[3][2][11] = {{{0}}};
     if (T < 1 || T > 10 || !jstream_supported_T(T)) return 4;
-    int& c = cache[C == 4 ? 1 : 0][fast ? 1 : 0][T];
-    if (!c) c = waves_per_cu_c(C == 4 ? 4 : 2, T, fast);
+    int& c = cache[C == 4 ? 1 : (C == 3 ? 2 : 0)][fast ? 1 : 0][T];
+    if (!c) c = waves_per_cu_c(C == 4 ? 4 : (C == 3 ? 3 : 2), T, fast);
     return c;
 }
 
 bool jstream_supported_C(int C, bool fast)
 {
     if (C == 2) return true;
+    if (C == 3) return fast && PF_JACOBI_C3 != 0;
     if (C != 4) return false;
     return fast ? PF_JACOBI_C4P != 0 : PF_JACOBI_C4 != 0;
 }
