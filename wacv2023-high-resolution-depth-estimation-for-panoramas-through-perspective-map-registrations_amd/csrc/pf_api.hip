@@ -1097,11 +1097,9 @@ static JresPlan jres_plan(pf_ctx* c, const LevelDims& L, int batch, bool fast)
     if (mode == 0 || !fast || batch < 1) return jp;
     const int rows = jres_region_rows(L.w);  // region rows of one workgroup
     if (rows <= 0 || L.iters < 1) return jp;
-    static int bpc_w[3] = {-1, -1, -1};  // resident blocks per CU at widths 256, 512, 1024
+    // resident blocks per CU at widths 256, 512, 1024, for the full and the half-height region
+    static int bpc_w[3][2] = {{-1, -1}, {-1, -1}, {-1, -1}};
     const int wi = L.w == 256 ? 0 : (L.w == 512 ? 1 : 2);
-    if (bpc_w[wi] < 0) bpc_w[wi] = jres_blocks_per_cu(L.w);
-    const int bpc = bpc_w[wi];
-    if (bpc < 1) return jp;
     const int band = L.h1 - L.h0 + 1;
     // cost in sweep units: the blocks run in ceil(blocks / resident) rounds of residency, each
     // sweep costs one unit (fixed region size), each K-sweep hand-off ~2.5 units (measured
@@ -1116,6 +1114,9 @@ static JresPlan jres_plan(pf_ctx* c, const LevelDims& L, int batch, bool fast)
     for (int hv = 0; hv < 2; hv++) {
         const int rows_h = hv ? jres_region_rows(L.w, true) : rows;
         if (rows_h <= 0) continue;
+        if (bpc_w[wi][hv] < 0) bpc_w[wi][hv] = jres_blocks_per_cu(L.w, hv == 1);
+        const int bpc = bpc_w[wi][hv];  // of the instantiation this choice launches
+        if (bpc < 1) continue;
         const double sweep = hv ? hcost : 1.0;
         for (int nb = 1; nb <= band && nb <= 64; nb++) {
             if (nb_force > 0 && nb != nb_force) continue;

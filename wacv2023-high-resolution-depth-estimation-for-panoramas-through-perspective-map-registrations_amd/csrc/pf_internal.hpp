@@ -238,7 +238,7 @@ int jres_region_rows(int w, bool half = false);  // 0: not supported
 int jres_threads();
 int jres_words_per_value();
 int jres_flags_per_block(int K);  // 2: the hand-off rows travel as {value, tag} granules
-int jres_blocks_per_cu(int w);
+int jres_blocks_per_cu(int w, bool half);
 void launch_jres(hipStream_t s, const JresArgs& A);
 
 // ------------------------------------------------------------------------------------------

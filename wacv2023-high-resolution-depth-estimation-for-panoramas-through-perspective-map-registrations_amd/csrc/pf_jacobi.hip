@@ -44,8 +44,9 @@
 #endif
 #ifndef PF_JACOBI_C3
 // packed form at 3 columns per lane (round 6; built, bit-exact, measured slower than C = 2 on
-// MI355X: DESIGN.md §3; the planner takes it only under PF_JC=3)
-#define PF_JACOBI_C3 1
+// MI355X: DESIGN.md §3; off in the default build, which it would double; a build with
+// -DPF_JACOBI_C3=1 takes it under PF_JC=3)
+#define PF_JACOBI_C3 0
 #endif
 #ifndef PF_JLAG_WAVES
 #define PF_JLAG_WAVES 1  // __launch_bounds__ min waves per SIMD of the lagged kernel

@@ -679,11 +679,18 @@ void launch_jres(hipStream_t s, const JresArgs& A)
 #endif
 }
 
-int jres_blocks_per_cu(int w)
+// resident blocks per CU of the instantiation that launches at this width (half: the half-height
+// 512-wide region, whose register and LDS use may differ from the full one's)
+int jres_blocks_per_cu(int w, bool half)
 {
     int nb = 0;
     const void* f = reinterpret_cast<const void*>(k_jres<8, kRS512, kJW, 0, false>);
     int threads = 64 * kJW;
+#if PF_JRES_HALF
+    if (w == 512 && half) f = reinterpret_cast<const void*>(k_jres<8, kRS512 / 2, kJW, 0, false>);
+#else
+    (void)half;
+#endif
     if (w == 256) f = reinterpret_cast<const void*>(k_jres<4, kRS256, kJW, 0, false>);
 #if PF_JRES_1024
     if (w == 1024) {
