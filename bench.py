@@ -51,6 +51,10 @@ def parse():
                     help="c5 rows mode: the coarsest levels replicated on every rank instead of "
                          "row-sharded (pf_dist.fuse_row_sharded rep_levels); -1 = auto "
                          "(pf_dist.auto_rep_levels)")
+    ap.add_argument("--c5-side", type=int, default=1,
+                    help="c5 rows mode: 1 = each rank's row-sharded levels' tile sums, their "
+                         "exchange and adds on a second stream beside the replicated levels' "
+                         "sweeps (HipRowShardBackend.enable_side); 0 = one stream")
     ap.add_argument("--mode", choices=("batch", "c5"), default="batch",
                     help="batch: configs C3/C4 (the headline metric); c5: one 8192x4096 "
                          "panorama, tiles sharded over the ranks")
@@ -228,6 +232,11 @@ def c5_measure(args, rank, world, local, dev, steps, warmup):
 
     logs = []
     be0 = pf_dist.HipRowShardBackend(fz, emap, tiles, coeffs, out_w, zr, out.view(-1))
+    fside = None
+    if args.c5_side:  # the row-sharded levels' tile sums beside the replicated levels' sweeps
+        fside = panofuse.Fuser(local, stream=torch.cuda.Stream(dev))
+        fside.set_tiles(lay)
+        be0.enable_side(fside)
     comm = pf_dist.TorchComm(dist, stage_host=args.backend == "gloo") if world > 1 else None
     # one choice for all ranks (rank 0's): the plans behind it depend on per-process state
     rep = args.c5_rep if args.c5_rep >= 0 else pf_dist.auto_rep_levels(be0, nlevels, world,
@@ -298,7 +307,7 @@ def c5_measure(args, rank, world, local, dev, steps, warmup):
     model8 = None
     if world == 1 and args.c5_shard == "rows":
         model8 = c5_rehearsal(fz, lay, gt, emap, resp_all, coeffs, tiles, out, out_w, zr,
-                              nlevels, dev, local)
+                              nlevels, dev, local, side=fside)
     nz = int((out != 0).sum().item())
     sent = logs[-1].sent if logs else None  # this rank's bytes of the last step, by kind
     if world > 1 and sent is not None:
@@ -322,13 +331,15 @@ XCHG_GBS = 50.0
 
 
 def c5_rehearsal(fz, lay, gt, emap, resp_all, coeffs, tiles, out, out_w, zr, nlevels, dev,
-                 local, world=8):
+                 local, world=8, side=None):
     import torch
 
     import panofuse
     import pf_dist
     import pf_layouts as PL
     be = pf_dist.HipRowShardBackend(fz, emap, tiles, coeffs, out_w, zr, out.view(-1))
+    if side is not None:
+        be.enable_side(side)
     dims = [be.dims(lv) for lv in range(nlevels)]
     ext = [[be.tile_rows(lv, *pf_dist.shard_range(lay.ntiles, r, world)) for r in range(world)]
            for lv in range(nlevels)]

@@ -208,7 +208,9 @@ int pf_fuse_band_pass(pf_ctx* ctx, const float* emap, int ew, int eh, int ec, co
  * pf_fuse_tile_rows: [*ymin, *ymax] = the rows where tiles [t0, t1) have non-zero partial sums at
  *   this level (*ymin > *ymax when none); host only, from the cached boxes.
  * pf_rows_add: dst[i] += src[i], i < n (a received partial-sum segment; exact where a pixel is
- *   covered by at most two tiles -- the rest is pf_fuse_multicover's). */
+ *   covered by at most two tiles -- the rest is pf_fuse_multicover's).
+ * pf_rows_add_batch: the same for `count` segments (dst[k], src[k], n[k]: host arrays of device
+ *   pointers and sizes) in one launch; the segments must not overlap. */
 int pf_fuse_partial_rows(pf_ctx* ctx, const float* tiles, const float* coeffs, int t0, int t1,
                          int out_w, int out_h, float zr0, float zr1, int level, int row0,
                          int row1, float* lsum, float* cnt);
@@ -220,6 +222,8 @@ int pf_fuse_normalize_rows(pf_ctx* ctx, const float* lsum, const float* cnt, int
 int pf_fuse_tile_rows(pf_ctx* ctx, int out_w, int out_h, float zr0, float zr1, int level, int t0,
                       int t1, int* ymin, int* ymax);
 int pf_rows_add(pf_ctx* ctx, float* dst, const float* src, long long n);
+int pf_rows_add_batch(pf_ctx* ctx, float* const* dst, const float* const* src,
+                      const long long* n, int count);
 
 /* ---- stage timing (hipEvents on the context stream; replaces the reference's timeGetTime
  * brackets around registration and fusion, Depth.cpp:792-808, 907-916) ----

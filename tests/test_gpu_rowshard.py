@@ -75,7 +75,7 @@ class ThreadComm:
         return RankComm()
 
 
-def _run(cfg, world, seed, flow="rows", rep=0):
+def _run(cfg, world, seed, flow="rows", rep=0, side=False):
     lay = PL.config_layout(cfg)
     out_w, ew = PL.CONFIGS["C5" if cfg == "C5" else "C2"]
     seeds = pf_synth.seeds_for(1, seed)
@@ -101,6 +101,10 @@ def _run(cfg, world, seed, flow="rows", rep=0):
             out = torch.zeros(out_w * (out_w // 2), dtype=torch.int16, device=DEV)
             if flow == "rows":
                 be = pf_dist.HipRowShardBackend(f, emap, tiles, coeffs[0], out_w, ZR, out)
+                if side:  # the row-sharded levels' tile sums on a second stream
+                    fs = panofuse.Fuser(0, stream=torch.cuda.Stream(DEV))
+                    fs.set_tiles(lay)
+                    be.enable_side(fs)
                 pf_dist.fuse_row_sharded(be, be.nlevels, lay.ntiles, r, world, comm.rank(r),
                                          rep_levels=rep)
             else:  # tiles only: rank 0 sweeps
@@ -142,6 +146,14 @@ def test_row_sharded_c5_eight_ranks_coarse_levels_replicated():
     all-gather of partial target rows) and the two finer levels row-sharded: rank 0's u16 ==
     the one-GPU fusion (8 threads on one GPU)."""
     _run("C5", 8, 20261015 + 14, rep=2)
+
+
+def test_row_sharded_c5_eight_ranks_side_stream():
+    """The same with each rank's row-sharded levels' tile sums, their exchange and adds on a
+    second stream beside the replicated levels' sweeps (HipRowShardBackend.enable_side, the
+    bench's C5 flow), and rank 0's own border rows standing in for the last rank's rows below
+    the band (pf_dist.border_local_from)."""
+    _run("C5", 8, 20261015 + 17, rep=2, side=True)
 
 
 def test_tile_sharded_c5_threads_equals_fuse():

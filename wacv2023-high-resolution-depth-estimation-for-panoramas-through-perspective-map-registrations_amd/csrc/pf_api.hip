@@ -2118,6 +2118,32 @@ int pf_rows_add(pf_ctx* c, float* dst, const float* src, long long n)
     return PF_OK;
 }
 
+int pf_rows_add_batch(pf_ctx* c, float* const* dst, const float* const* src, const long long* n,
+                      int count)
+{
+    int rc;
+    if ((rc = check_common(c, 1))) return rc;
+    if (count < 0 || (count > 0 && (!dst || !src || !n))) return fail(c, PF_EINVAL, "bad rows add batch");
+    for (int k0 = 0; k0 < count; k0 += kRowsAddBatch) {
+        RowsAddBatch B{};
+        int m = 0;
+        long long nmax = 0;
+        for (int k = k0; k < count && m < kRowsAddBatch; k++) {
+            if (n[k] < 0 || (n[k] > 0 && (!dst[k] || !src[k])))
+                return fail(c, PF_EINVAL, "bad rows add segment %d", k);
+            if (n[k] == 0) continue;
+            B.dst[m] = dst[k];
+            B.src[m] = src[k];
+            B.n[m] = n[k];
+            nmax = std::max(nmax, n[k]);
+            m++;
+        }
+        launch_rows_add_batch(c->stream, B, m, nmax);
+        HIPCHK(c, hipGetLastError());
+    }
+    return PF_OK;
+}
+
 int pf_fuse_seed(pf_ctx* c, const float* emap, int ew, int eh, int ec, const float* prev,
                  int out_w, int out_h, float zr0, float zr1, int level, float* buf)
 {

@@ -304,6 +304,14 @@ hipError_t launch_targets_partial(hipStream_t s, const TileGeom* geom, const Til
 void launch_coverage_rows(hipStream_t s, const TileBox* box, int ntiles, LevelDims L, float* cnt,
                           int r0, int r1);
 void launch_rows_add(hipStream_t s, float* dst, const float* src, long long n);
+// pf_rows_add_batch's kernel argument: up to kRowsAddBatch segments by value
+static constexpr int kRowsAddBatch = 32;
+struct RowsAddBatch {
+    float* dst[kRowsAddBatch];
+    const float* src[kRowsAddBatch];
+    long long n[kRowsAddBatch];
+};
+void launch_rows_add_batch(hipStream_t s, const RowsAddBatch& B, int count, long long nmax);
 void launch_normalize(hipStream_t s, const float* lsum, const float* cnt, LevelDims L,
                       float* lnorm, int r0 = -1, int r1 = -1);
 void launch_multicover(hipStream_t s, const TileGeom* geom, const int2* pairs, int npairs,

@@ -73,6 +73,12 @@ __device__ __forceinline__ float fma_scalar(float a, float b, float c)
 #ifndef PF_JRES_LDSFLAG
 #define PF_JRES_LDSFLAG 0  // barrier-free sweeps + per-row hand-off flags (measured: same time as barriers)
 #endif
+#ifndef PF_JRES_EARLY_EDGE
+// 1: a wave's new last row goes to LDS before its row 0 is computed (the store overlaps row 0's
+// arithmetic).  Round 6, three alternating serial rounds on one MI355X: 506-528 us against
+// 508-523 us per C3 launch: no change.  Off.
+#define PF_JRES_EARLY_EDGE 0
+#endif
 #ifndef PF_JRES_GRANULE
 #define PF_JRES_GRANULE 0  // hand-off by data-tagged granules (measured 2x slower: 32-KB edges)
 #endif
@@ -164,8 +170,12 @@ struct JRes {
             rows_mid<R + 1, HAS_EDGE>(n, dn, em);
         }
     }
+    // bot_out (JRES_EARLY_EDGE): the LDS slot of this wave's new last row, stored as soon as
+    // that row is done, so the store overlaps row 0's arithmetic instead of joining the stores
+    // every wave issues just before the sweep's barrier
     template <bool HAS_EDGE>
-    __device__ __forceinline__ void sweep(const f2* up_lds, const f2* dn_lds, uint32_t em)
+    __device__ __forceinline__ void sweep(const f2* up_lds, const f2* dn_lds, uint32_t em,
+                                          f2* bot_out = nullptr)
     {
         f2 up[NP], dn[NP], s1[NP], n[NP];
 #pragma unroll
@@ -176,6 +186,9 @@ struct JRes {
             n[k] = b[0][k];
         }
         if constexpr (RS > 1) rows_mid<1, HAS_EDGE>(n, dn, em);
+        if (RS > 1 && bot_out)
+#pragma unroll
+            for (int k = 0; k < NP; k++) bot_out[64 * k] = b[RS - 1][k];
         if (HAS_EDGE && (em & 1u)) row<0, true>(up, RS > 1 ? s1 : dn);
         else row<0, false>(up, RS > 1 ? s1 : dn);
     }
@@ -431,10 +444,23 @@ __global__ void __launch_bounds__(64 * NWV) k_jres(JresArgs A)
             const bool skip = (j > 0 && wv * RS + RS - 1 < qc0 - reach) ||
                               (j < A.nb - 1 && wv * RS >= qc1 + reach);
             if (!(A.dbg & 4) && !skip) {
-                if (em) S.template sweep<true>(up, dn, em);
-                else S.template sweep<false>(up, dn, em);
-            }
-            if (!(A.dbg & 8)) {
+#if PF_JRES_EARLY_EDGE
+                f2* bot = RS > 1 && !(A.dbg & 8) ? &lds_edge[cb ^ 1][1][wv][0][lane] : nullptr;
+#else
+                f2* bot = nullptr;
+#endif
+                if (em) S.template sweep<true>(up, dn, em, bot);
+                else S.template sweep<false>(up, dn, em, bot);
+                if (!(A.dbg & 8)) {
+                    if (bot) {  // the last row went out inside the sweep
+#pragma unroll
+                        for (int k = 0; k < NP; k++) lds_edge[cb ^ 1][0][wv][k][lane] = S.b[0][k];
+                    } else {
+                        put_edges(cb ^ 1);
+                    }
+                    __syncthreads();
+                }
+            } else if (!(A.dbg & 8)) {
                 put_edges(cb ^ 1);
                 __syncthreads();
             }

@@ -190,6 +190,26 @@ __global__ void __launch_bounds__(kBlock) k_rows_add(float* __restrict__ dst,
     }
 }
 
+// Several segments in one launch (pf_rows_add_batch): blockIdx.y = segment.
+__global__ void __launch_bounds__(kBlock) k_rows_add_batch(RowsAddBatch B)
+{
+    const int k = blockIdx.y;
+    float* __restrict__ dst = B.dst[k];
+    const float* __restrict__ src = B.src[k];
+    const long long n = B.n[k];
+    for (long long i = ((long long)blockIdx.x * kBlock + threadIdx.x) * 4; i < n;
+         i += (long long)gridDim.x * kBlock * 4) {
+        if (i + 3 < n && ((reinterpret_cast<uintptr_t>(dst + i) | reinterpret_cast<uintptr_t>(src + i)) & 15) == 0) {
+            float4 a = *reinterpret_cast<const float4*>(dst + i);
+            const float4 b = *reinterpret_cast<const float4*>(src + i);
+            a.x += b.x; a.y += b.y; a.z += b.z; a.w += b.w;
+            *reinterpret_cast<float4*>(dst + i) = a;
+        } else {
+            for (long long j = i; j < n && j < i + 4; j++) dst[j] += src[j];
+        }
+    }
+}
+
 // Parity probe: linear tile index of each tap of the first covering tile.
 __global__ void __launch_bounds__(kBlock) k_probe_taps(const TileGeom* __restrict__ geom,
                                                        const TileBox* __restrict__ box,
@@ -786,6 +806,14 @@ void launch_rows_add(hipStream_t s, float* dst, const float* src, long long n)
 {
     if (n <= 0) return;
     hipLaunchKernelGGL(k_rows_add, dim3(nblocks((n + 3) / 4)), dim3(kBlock), 0, s, dst, src, n);
+}
+
+void launch_rows_add_batch(hipStream_t s, const RowsAddBatch& B, int count, long long nmax)
+{
+    if (count <= 0 || nmax <= 0) return;
+    long long nb = (nmax + 4LL * kBlock - 1) / (4LL * kBlock);
+    if (nb > 1024) nb = 1024;
+    hipLaunchKernelGGL(k_rows_add_batch, dim3((unsigned)nb, (unsigned)count), dim3(kBlock), 0, s, B);
 }
 
 void launch_multicover(hipStream_t s, const TileGeom* geom, const int2* pairs, int npairs,

@@ -32,11 +32,12 @@ EXPORTS = [
     "pf_probe_warp_coords", "pf_probe_rgb_taps", "pf_debug_smooth_fault",
     "pf_fuse_partial_rows", "pf_fuse_coverage_rows", "pf_fuse_normalize_rows",
     "pf_fuse_tile_rows", "pf_rows_add", "pf_fuse_level", "pf_fuse_targets",
+    "pf_rows_add_batch",
 ]
 NEW_R4 = {"pf_debug_jres_fault", "pf_probe_warp_coords", "pf_probe_rgb_taps",
           "pf_debug_smooth_fault", "pf_fuse_partial_rows", "pf_fuse_coverage_rows",
           "pf_fuse_normalize_rows", "pf_fuse_tile_rows", "pf_rows_add", "pf_fuse_level",
-          "pf_fuse_targets"}
+          "pf_fuse_targets", "pf_rows_add_batch"}
 METRICS_ORDERS = {"tree": 0, "sequential": 1}  # PF_METRICS_*; "sequential" = the reference's
 SOLVERS = {"normal": 0, "lm": 1}  # PF_SOLVER_*; "lm" = the reference's Ceres LM (default)
 
@@ -118,6 +119,7 @@ def load():
                      ("pf_fuse_tile_rows", [vp, ip, ip, fp, fp, ip, ip, ip,
                                             C.POINTER(C.c_int), C.POINTER(C.c_int)]),
                      ("pf_rows_add", [vp, vp, vp, C.c_longlong]),
+                     ("pf_rows_add_batch", [vp, vp, vp, vp, ip]),
                      ("pf_fuse_level", [vp, vp, ip, ip, ip, vp, vp, vp, ip, ip, fp, fp, ip, vp,
                                         vp]),
                      ("pf_fuse_targets", [vp, vp, vp, ip, ip, fp, fp, ip, vp]),
@@ -355,6 +357,20 @@ class Fuser:
         """dst += src (same-size fp32 device tensors), on the context's stream."""
         assert dst.numel() == src.numel()
         self._check(self.L.pf_rows_add(self.h, _ptr(dst), _ptr(src), dst.numel()))
+
+    def rows_add_batch(self, pairs):
+        """dst += src for every (dst, src) pair of same-size fp32 device tensors, one launch
+        (pf_rows_add_batch); the destinations must not overlap."""
+        k = len(pairs)
+        if not k:
+            return
+        dst = (C.c_void_p * k)(*[_ptr(d).value for d, _ in pairs])
+        src = (C.c_void_p * k)(*[_ptr(s).value for _, s in pairs])
+        n = (C.c_longlong * k)()
+        for i, (d, s) in enumerate(pairs):
+            assert d.numel() == s.numel()
+            n[i] = d.numel()
+        self._check(self.L.pf_rows_add_batch(self.h, dst, src, n, k))
 
     def fuse_seed(self, emap, prev, out_w, zr, level, buf):
         ew, eh, ec = _emap_dims(emap) if emap is not None else (0, 0, 0)

@@ -242,6 +242,32 @@ def owned_rows(bounds, h, rank):
     return lo, hi
 
 
+def gather_rows(bounds, h, rank, local_from=None):
+    """Rows of the last level's u16 result rank `rank` sends to rank 0: its owned rows, except
+    that the last rank keeps the rows from `local_from` down, which rank 0's own border pass
+    computes exactly (border_local_from)."""
+    lo, hi = owned_rows(bounds, h, rank)
+    if local_from is not None and rank == len(bounds) - 2:
+        hi = max(bounds[-1], min(hi, local_from))
+    return lo, hi
+
+
+def border_local_from(dims, rep_levels):
+    """First row of the last level from which rank 0's border pass (k_border: the rows outside
+    [h0, h1], the previous level's nearest upsample) is exact by itself.  A level after a
+    replicated one: every row below the band (rank 0 holds the previous level whole).  After a
+    row-sharded level: border row y reads row y // 2 of the previous level, which rank 0 holds
+    exactly from that level's own first exact border row fb on, so fb' = max(h1 + 1, 2 fb).  The
+    last rank then sends only the rows above that (fuse_row_sharded's u16 gather)."""
+    fb = None
+    for lv, (w, h, h0, h1) in enumerate(dims):
+        if lv < rep_levels or lv == 0:
+            fb = None if lv < rep_levels else h1 + 1  # replicated (whole) / level 0 (zeros)
+            continue
+        fb = h1 + 1 if fb is None else max(h1 + 1, 2 * fb)
+    return fb
+
+
 def prev_rows_needed(bounds, h0, h1, K, hp, rank):
     """Rows of the previous level (hp rows) a rank's first pass and border read at this level: the
     2x upsample of its band + halo [b_r - K, b_r+1 + K) (a virtual column past a row end reaches
@@ -364,40 +390,72 @@ def fuse_row_sharded(backend, nlevels, ntiles, rank, world, comm=None, log=None,
     # its tiles only on the rows it needs (its band + halo) and the rows it sends.
     tgt = {}
 
-    def gather_targets(levels):
-        sends, recvs, bufs = [], [], []
+    # The targets of a group of levels in three phases: allocation (on the calling stream),
+    # the tile sums and multicover terms (kernels only), and the exchange + adds.  A backend with
+    # a side stream (HipRowShardBackend.side) runs the second phase of the row-sharded levels
+    # beside the replicated levels' sweeps and the third when those are queued; the targets
+    # depend on the tiles alone.
+    def targets_alloc(levels):
+        st = {"sends": [], "recvs": [], "bufs": [], "levels": list(levels)}
         for level in levels:
             rep, (plan, K, ext, bounds, need) = G[level]
             w = backend.dims(level)[0]
-            e0, e1 = need[rank]
             lsum = backend.plane(level)
             mlo, mhi = ext[rank][0], ext[rank][1] + 1
-            lo, hi = (min(e0, mlo), max(e1, mhi)) if mlo < mhi else (e0, e1)
-            backend.partial_rows(level, t0, t1, lo, hi, lsum, backend.plane(level))
             for d in range(world):
                 if d == rank:
                     continue
                 sp = _span(need[d], (mlo, mhi))
                 if sp:
-                    sends.append((d, lsum[sp[0] * w:sp[1] * w]))
+                    st["sends"].append((d, lsum[sp[0] * w:sp[1] * w]))
                 s_lo, s_hi = ext[d][0], ext[d][1] + 1
                 rp = _span(need[rank], (s_lo, s_hi)) if s_lo < s_hi else None
                 if rp:
                     buf = backend.scratch((rp[1] - rp[0]) * w)
-                    recvs.append((d, buf))
-                    bufs.append((level, rp, buf))
+                    st["recvs"].append((d, buf))
+                    st["bufs"].append((level, rp, buf))
+            tgt[level] = (lsum, None)
+        return st
+
+    def targets_compute(st):
+        for level in st["levels"]:
+            rep, (plan, K, ext, bounds, need) = G[level]
+            e0, e1 = need[rank]
+            lsum = tgt[level][0]
+            mlo, mhi = ext[rank][0], ext[rank][1] + 1
+            lo, hi = (min(e0, mlo), max(e1, mhi)) if mlo < mhi else (e0, e1)
+            backend.partial_rows(level, t0, t1, lo, hi, lsum, backend.plane(level))
             # every tile's coverage count (layout-only: counted once per backend and level)
             tgt[level] = (lsum, backend.coverage_plane(level))
+        st["mcl"] = [lv for lv in st["levels"] if backend.multicover_count(lv)]
+        st["parts"] = [backend.multicover(lv, t0, t1) for lv in st["mcl"]]
+
+    def targets_finish(st):
+        sends, recvs = st["sends"], st["recvs"]
         comm.exchange(sends, recvs)  # level-major on both sides: the pairs match in order
         if log:
             log.add("targets", sum(4 * t.numel() for _, t in sends))
-        for level, (a, b), buf in bufs:  # one addend per covering tile: exact up to 2 (3+: below)
+        # one addend per covering tile: exact up to 2 (3+: below).  The adds go in the order
+        # received (a pixel fed by two other ranks' tiles takes them in tile order); a batched
+        # launch holds only segments that do not overlap, so an overlapping one starts a new
+        # batch after the earlier adds.
+        batch, spans = [], []
+        for level, (a, b), buf in st["bufs"]:
             w = backend.dims(level)[0]
-            backend.rows_add(tgt[level][0][a * w:b * w], buf)
-        mcl = [lv for lv in levels if backend.multicover_count(lv)]
+            dst = tgt[level][0][a * w:b * w]
+            if not hasattr(backend, "rows_add_batch"):
+                backend.rows_add(dst, buf)
+                continue
+            if any(lv == level and a < b_ and a_ < b for lv, a_, b_ in spans):
+                backend.rows_add_batch(batch)
+                batch, spans = [], []
+            batch.append((dst, buf))
+            spans.append((level, a, b))
+        if batch:
+            backend.rows_add_batch(batch)
+        mcl, parts = st["mcl"], st["parts"]
         if mcl:  # exact sums where 3+ tiles meet, the group's terms in one all-reduce
             import torch
-            parts = [backend.multicover(lv, t0, t1) for lv in mcl]
             allc = torch.cat(parts) if len(parts) > 1 else parts[0]
             comm.all_reduce_sum(allc)
             if log:
@@ -407,14 +465,33 @@ def fuse_row_sharded(backend, nlevels, ntiles, rank, world, comm=None, log=None,
                 backend.multicover_patch(lv, allc[o:o + part.numel()], tgt[lv][0])
                 o += part.numel()
 
+    def gather_targets(levels):
+        st = targets_alloc(levels)
+        targets_compute(st)
+        targets_finish(st)
+
     nrep = sum(1 for r_, _ in G if r_)
     if nrep:
         gather_targets(range(nrep))
+    side = backend.side if getattr(backend, "has_side", False) else None
+    early = None
+    if side is not None and 0 < nrep < nlevels:
+        # the row-sharded levels' tile sums beside the replicated levels' sweeps
+        early = targets_alloc(range(nrep, nlevels))
+        with side():
+            targets_compute(early)
     for level in range(nlevels):
         last = level == nlevels - 1
         rep, (plan, K, ext, bounds, need) = G[level]
         if level == nrep:
-            gather_targets(range(nrep, nlevels))
+            if early is not None:
+                # the exchange and adds follow the side stream's tile sums only, not the sweeps
+                # queued on the calling stream since
+                with side(wait=False):
+                    targets_finish(early)
+                backend.join()
+            else:
+                gather_targets(range(nrep, nlevels))
         w, h, h0, h1 = backend.dims(level)
         r0, r1 = (h0, h1 + 1) if rep else (bounds[rank], bounds[rank + 1])
         e0, e1 = need[rank]
@@ -470,18 +547,20 @@ def fuse_row_sharded(backend, nlevels, ntiles, rank, world, comm=None, log=None,
             src, dst = dst, (b if dst is a else a)
         prev, pbounds = (None if last else src), bounds
     bounds = G[-1][1][3]
-    # the u16 result: every rank's owned rows to rank 0 (a replicated last level: all local)
+    # the u16 result: every rank's owned rows to rank 0 (a replicated last level: all local),
+    # except the rows below the band that rank 0's border pass computed (border_local_from)
     if pbounds is not None:
         import torch
         w, h = backend.dims(nlevels - 1)[:2]
+        loc = border_local_from([backend.dims(lv) for lv in range(nlevels)], nrep)
 
         def out8(a_, b_):  # as bytes: gloo has no 16-bit integers
             return backend.out[a_ * w:b_ * w].view(torch.uint8)
         if rank == 0:
-            recvs = [(s, out8(*owned_rows(bounds, h, s))) for s in range(1, world)]
+            recvs = [(s, out8(*gather_rows(bounds, h, s, loc))) for s in range(1, world)]
             comm.exchange([], recvs)
         else:
-            snd = out8(*owned_rows(bounds, h, rank))
+            snd = out8(*gather_rows(bounds, h, rank, loc))
             comm.exchange([(0, snd)], [])
             if log:
                 log.add("gather_u16", snd.numel())
@@ -540,8 +619,9 @@ def exchange_model(dims, plans, ext, world, multicover=None, rep_levels=0):
     if pb is None:  # a replicated last level: no gather
         return res
     w, h = dims[-1][:2]
+    loc = border_local_from(dims, rep_levels)
     for r in range(1, world):
-        lo, hi = owned_rows(pb, h, r)
+        lo, hi = gather_rows(pb, h, r, loc)
         add(r, "gather_u16", 2 * w * (hi - lo))
     return res
 
@@ -614,6 +694,42 @@ class HipRowShardBackend:
 
     def rows_add(self, dst, src):
         self.fz.rows_add(dst, src)
+
+    def rows_add_batch(self, pairs):
+        self.fz.rows_add_batch(pairs)
+
+    def enable_side(self, fuser):
+        """A second panofuse.Fuser of the same layout on its own stream: fuse_row_sharded runs the
+        row-sharded levels' tile sums on it beside the replicated levels' sweeps (side / join)."""
+        self.fz_side = fuser
+        self.has_side = True
+
+    def side(self, wait=True):
+        """Context: the backend's kernels go to the side Fuser's stream, which first waits for
+        everything queued so far on the calling stream (wait=False: only for its own earlier
+        work); torch's current stream is the side stream too (collectives, host copies).
+        Tensors the main stream uses later are allocated outside (targets_alloc)."""
+        import contextlib
+        import torch
+        be = self
+
+        @contextlib.contextmanager
+        def ctx():
+            s = be.fz_side.stream
+            if wait:
+                s.wait_stream(torch.cuda.current_stream(be.tiles.device))
+            fz, be.fz = be.fz, be.fz_side
+            try:
+                with torch.cuda.stream(s):
+                    yield
+            finally:
+                be.fz = fz
+        return ctx()
+
+    def join(self):
+        """The calling stream waits for the side stream's work."""
+        import torch
+        torch.cuda.current_stream(self.tiles.device).wait_stream(self.fz_side.stream)
 
     multicover_count = HipTileShardBackend.multicover_count
     multicover = HipTileShardBackend.multicover
