@@ -41,14 +41,17 @@ class ThreadComm:
         class RankComm:
             def all_reduce_sum(self, t):
                 outer.box[("ar", r)] = t
+                torch.cuda.current_stream().synchronize()
                 outer.bar.wait()
                 if r == 0:
                     acc = outer.box[("ar", 0)].clone()
                     for k in range(1, outer.world):
                         acc += outer.box[("ar", k)]
                     outer.box["ar"] = acc
+                torch.cuda.current_stream().synchronize()
                 outer.bar.wait()
                 t.copy_(outer.box["ar"])
+                torch.cuda.current_stream().synchronize()
                 outer.bar.wait()
 
             def reduce_sum(self, t, dst):
@@ -56,9 +59,11 @@ class ThreadComm:
 
             def exchange(self, sends, recvs):
                 # several messages per pair arrive in the order they were sent (as batched
-                # isend/irecv pairs match)
+                # isend/irecv pairs match); the clones are complete before another thread's
+                # stream reads them (a rank may exchange on its side stream)
                 for peer, t in sends:
                     outer.box.setdefault(("x", r, peer), []).append(t.clone())
+                torch.cuda.current_stream().synchronize()
                 outer.bar.wait()
                 for peer, t in recvs:
                     t.copy_(outer.box[("x", peer, r)].pop(0))
@@ -67,6 +72,7 @@ class ThreadComm:
             def broadcast(self, t, src):
                 if r == src:
                     outer.box["bc"] = t.clone()
+                torch.cuda.current_stream().synchronize()
                 outer.bar.wait()
                 if r != src:
                     t.copy_(outer.box["bc"])

@@ -13,6 +13,8 @@
 #   c5       the C5 line at world 1 (+ the 8-rank byte model)  -> bench_c5.log
 #   c4       bench.py --gpus 8 on the one GPU (gloo, --same-device): C4's 8-rank shape
 #   rgb      the RGB warp probe (tools/rgb_probe.py)   -> rgb.log
+#   warppipe k_warp_depth's vector-memory path counters (TA/TD busy and stalls, three --pmc
+#            passes over tools/warp_probe.py)          -> warppipe/summary.txt
 #   serials  the serial step per variant: $VARIANTS as for ab -> serial_NAME/levels.txt (one trace
 #            each, in $ROUNDS alternating rounds)
 #   ab       A/B of environment knobs: $VARIANTS = "NAME:ENV=VAL,ENV=VAL NAME2:" run in $ROUNDS
@@ -81,6 +83,18 @@ for s in $STEPS; do
     rgb)
       timeout -k 10 120 python3 tools/rgb_probe.py > $OUT/rgb.log 2>&1; rc=$?
       echo "rgb rc=$rc"; cat $OUT/rgb.log | tail -2; [ $rc -eq 0 ] || exit $rc ;;
+    warppipe)
+      rm -rf $OUT/warppipe; mkdir -p $OUT/warppipe; i=0
+      for set in "TA_TA_BUSY_sum TA_BUFFER_TOTAL_CYCLES_sum TD_TD_BUSY_sum TD_TC_STALL_sum GRBM_GUI_ACTIVE" \
+                 "TA_ADDR_STALLED_BY_TC_CYCLES_sum TA_DATA_STALLED_BY_TC_CYCLES_sum TD_TCP_STALL_CYCLES_sum TD_SPI_STALL_sum" \
+                 "TA_BUFFER_COALESCED_READ_CYCLES_sum TA_BUFFER_COALESCED_WRITE_CYCLES_sum"; do
+        i=$((i + 1))
+        timeout -k 5 -s KILL 120 rocprofv3 --pmc $set -d $OUT/warppipe/p$i -o run --output-format csv -- \
+          python3 tools/warp_probe.py > $OUT/warppipe/p$i.log 2>&1; rc=$?
+        [ $rc -eq 0 ] || { echo "warppipe pass $i rc=$rc"; tail -3 $OUT/warppipe/p$i.log; exit $rc; }
+      done
+      python3 tools/pmc_summary.py "$OUT/warppipe/p*/*counter_collection.csv" | grep -A10 "k_warp_depth" > $OUT/warppipe/summary.txt
+      cat $OUT/warppipe/summary.txt ;;
     ab)
       mkdir -p $OUT/ab
       for r in $(seq 1 ${ROUNDS:-2}); do
