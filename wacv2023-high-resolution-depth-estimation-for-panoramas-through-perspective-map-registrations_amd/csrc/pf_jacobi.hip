@@ -193,6 +193,23 @@ __device__ __forceinline__ float add_clamp01(float a, float b)
     asm("v_add_f32 %0, %1, %2 clamp" : "=v"(r) : "v"(a), "v"(b));
     return r;
 }
+#ifndef PF_JFMAC_DPP
+// 1: the E tap of a lane's last column is one v_fmac_f32_dpp (the neighbour lane's value read
+// through DPP inside the FMA) instead of a v_mov_b32_dpp + v_fmac_f32: hipcc's DPP combiner folds
+// a DPP move into a v_add_f32 but not into the tied-accumulator v_fmac_f32
+#define PF_JFMAC_DPP 1
+#endif
+// acc + x[lane + 1] * q (lane 63: + 0 * q, bound_ctrl), one rounding: fma(x[lane+1], q, acc)
+__device__ __forceinline__ float fmac_from_right(float acc, float x, float q)
+{
+#if PF_JFMAC_DPP
+    asm("v_fmac_f32_dpp %0, %1, %2 wave_shl:1 row_mask:0xf bank_mask:0xf bound_ctrl:0"
+        : "+v"(acc) : "v"(x), "v"(q));
+    return acc;
+#else
+    return __builtin_fmaf(dpp_from_right(x), q, acc);
+#endif
+}
 // fma(a, b, c) as a plain v_fma_f32 (same reason: two scalar FMAs on the halves of a pair would
 // otherwise become a packed FMA after a pair assembly)
 __device__ __forceinline__ float fma_scalar(float a, float b, float c)
@@ -561,7 +578,7 @@ struct JLag {
             const f3 c = H[t - 1][slot(PH, 2 * t)].v;
             cur[g].x = fma_scalar(c.y, vq, cur[g].x);
             cur[g].y = fma_scalar(c.z, vq, cur[g].y);
-            cz[g] = __builtin_fmaf(dpp_from_right(c.x), vq, cz[g]);
+            cz[g] = fmac_from_right(cz[g], c.x, vq);
         }
 #pragma unroll
         for (int g = 0; g < G; g++) {
@@ -626,7 +643,7 @@ struct JLag {
             const int t = T0 + 1 + g;
             const f2 c = H[t - 1][slot(PH, 2 * t)].v;
             cur[g].x = fma_scalar(c.y, vq, cur[g].x);
-            cur[g].y = __builtin_fmaf(dpp_from_right(c.x), vq, cur[g].y);
+            cur[g].y = fmac_from_right(cur[g].y, c.x, vq);
         }
 #pragma unroll
         for (int g = 0; g < G; g++) {
@@ -1114,7 +1131,7 @@ struct JPipe {
             const int t = T0 + 1 + g, l = t - TB;
             const f2 c = H[l][md(PH - 2 * t, 3)].v;
             cur[g].x = fma_scalar(c.y, vq, cur[g].x);
-            cur[g].y = __builtin_fmaf(dpp_from_right(c.x), vq, cur[g].y);
+            cur[g].y = fmac_from_right(cur[g].y, c.x, vq);
         }
 #pragma unroll
         for (int g = 0; g < NGR; g++) {
