@@ -51,6 +51,17 @@ __device__ __forceinline__ float dpp_rol(float v)
 {  // lane i <- lane (i+1) mod 64 (wave_rol:1)
     return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0x134, 0xF, 0xF, false));
 }
+// acc + x[(lane + 1) mod 64] * q in one v_fmac_f32_dpp (wave_rol:1), one rounding: the E tap of
+// a lane's last column (hipcc folds a DPP move into v_add_f32, not into the tied v_fmac_f32).
+// x is a select computed just before (the seam lane's operand), and the hazard recognizer does
+// not see into inline asm: the two wait states a DPP read of a fresh VGPR needs are the s_nop
+// (tools/dpp_hazards.py, tests/test_dpp_hazards.py)
+__device__ __forceinline__ float fmac_rol(float acc, float x, float q)
+{
+    asm("s_nop 1\n\tv_fmac_f32_dpp %0, %1, %2 wave_rol:1 row_mask:0xf bank_mask:0xf"
+        : "+v"(acc) : "v"(x), "v"(q));
+    return acc;
+}
 __device__ __forceinline__ f2 pk_add_clamp01(f2 a, f2 b)
 {
     f2 r;
@@ -122,7 +133,6 @@ struct JRes {
         // east tap of the lane's last column: the next lane's first column of this row; for
         // lane 63 (column w-1) lane 0's first column of the row below -- pixel (0, Y+1)
         const float xr = lane == 0 ? S[0].x : c[0].x;
-        const float e_last = dpp_rol(xr);
         f2 cur[NP];
 #pragma unroll
         for (int k = 0; k < NP; k++) {
@@ -138,8 +148,8 @@ struct JRes {
 #pragma unroll
         for (int k = 0; k < NP; k++) {
             cur[k].x = fma_scalar(c[k].y, vq, cur[k].x);
-            const float ey = k == NP - 1 ? e_last : c[k + 1].x;
-            cur[k].y = fma_scalar(ey, vq, cur[k].y);
+            if (k == NP - 1) cur[k].y = fmac_rol(cur[k].y, xr, vq);  // E from the next lane
+            else cur[k].y = fma_scalar(c[k + 1].x, vq, cur[k].y);
         }
 #pragma unroll
         for (int k = 0; k < NP; k++) {
