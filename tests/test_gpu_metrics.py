@@ -265,3 +265,32 @@ def test_sequential_redo_path_is_exact(fuser, merged, align_way, monkeypatch):
     for b in range(out.shape[0]):
         _check_exact(got[b], O.error_metrics(gt[b], res[b], ZR, align_way, True))
         _check_exact(got_e[b], O.error_metrics(gt[b], emap[b], ZR, align_way, True))
+
+
+@pytest.mark.parametrize("align_way", [0, 1, 2])
+def test_sequential_fused_terms_equal_planes(fuser, merged, align_way, monkeypatch):
+    """Round 6: where the geometry is the fast one (result of the gt's size, one channel), the
+    sequential chains form their terms from gt and the result as they stage each chunk
+    (InputSrc) instead of reading the four term planes k_seq_terms wrote.  Every field must equal
+    the planes path's (PF_METRICS_SEQ_PLANES=1), for the u16 result (ErrorData) and a float
+    result (ErrorEmap's fast form), and the u16 case stays exact against the oracle."""
+    emap, gt, out = merged
+    gv = (gt * np.float32(1.1) + np.float32(0.01)).astype(np.float32)
+    fuser.set_metrics_order("sequential")
+    try:
+        got = {}
+        for mode in ("fused", "planes"):
+            if mode == "planes":
+                monkeypatch.setenv("PF_METRICS_SEQ_PLANES", "1")
+            got[mode] = (fuser.error_metrics(_dev(gt), out, ZR, align_way, True),
+                         fuser.error_metrics(_dev(gt), _dev(gv), ZR, align_way, True))
+            monkeypatch.delenv("PF_METRICS_SEQ_PLANES", raising=False)
+    finally:
+        fuser.set_metrics_order("tree")
+    res = out.cpu().numpy().view(np.uint16)
+    for b in range(out.shape[0]):
+        for which in (0, 1):
+            f, p = got["fused"][which][b], got["planes"][which][b]
+            for k in f:
+                assert _same(f[k], p[k]), (which, k, f[k], p[k])
+        _check_exact(got["fused"][0][b], O.error_metrics(gt[b], res[b], ZR, align_way, True))

@@ -465,6 +465,27 @@ struct SeqTerms {  // four planes per panorama: component k of band pixel i = (y
     long long bandp;
 };
 
+// one pixel's four terms (the SeqTerms plane layout), v0 / v1 / ok from eval4
+template <bool LS>
+__device__ __forceinline__ float4 seq_px(float v0, float v1, bool ok, int align_way, const Align& A)
+{
+    float4 o = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+    if (LS) {
+        if (ok) o = make_float4(v1 * v1, v1, v0 * v1, v0);
+    } else if (ok) {
+        if (align_way == 1)
+            v1 *= A.shift;
+        else if (align_way == 2)
+            v1 = v1 * A.s + A.o;
+        const float d = v0 - v1;
+        o.x = d;
+        o.y = fabsf(d);
+        o.z = fabsf(d) / v0;
+        if ((double)v0 > 1e-4 && (double)v1 > 1e-4) o.w = log10f(v0) - log10f(v1);
+    }
+    return o;
+}
+
 template <bool LS>
 __global__ __launch_bounds__(MB) void k_seq_terms(MArgs a, int align_way, const Align* al,
                                                   SeqTerms T, long long band)
@@ -479,22 +500,7 @@ __global__ __launch_bounds__(MB) void k_seq_terms(MArgs a, int align_way, const 
       float* pl = T.t + (long long)b * 4 * T.bandp;
       for (int k = 0; k < 4 && x0 + k < a.w; ++k) {
         const long long i = (long long)(y - a.h0) * a.w + x0 + k;
-        const float v0 = V0[k];
-        float v1 = V1[k];
-        float4 o = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
-        if (LS) {
-            if (ok[k]) o = make_float4(v1 * v1, v1, v0 * v1, v0);
-        } else if (ok[k]) {
-            if (align_way == 1)
-                v1 *= A.shift;
-            else if (align_way == 2)
-                v1 = v1 * A.s + A.o;
-            const float d = v0 - v1;
-            o.x = d;
-            o.y = fabsf(d);
-            o.z = fabsf(d) / v0;
-            if ((double)v0 > 1e-4 && (double)v1 > 1e-4) o.w = log10f(v0) - log10f(v1);
-        }
+        const float4 o = seq_px<LS>(V0[k], V1[k], ok[k], align_way, A);
         pl[i] = o.x;
         pl[T.bandp + i] = o.y;
         pl[2 * T.bandp + i] = o.z;
@@ -547,34 +553,126 @@ __device__ __forceinline__ float sq_step(float acc, float v)
 // value) with no LDS writes on the chain's path.  Matching group ends make the chunk's result
 // the reference's by induction, whatever the steps inside did.  force (tests): one group per
 // chunk counts as a mismatch, so the exact redo path runs.
-template <int NPL, bool SQ>
-__device__ __forceinline__ float seq_chain(const float* __restrict__ pl, long long band,
-                                           long long bandp, const int (&pid)[NPL], float* lds,
-                                           uint32_t* cnt, int force = 0)
+constexpr int SNM = SCH / 256;  // 4-pixel groups per lane per chunk
+
+// Where a chain's chunks come from.  PlaneSrc: the term planes k_seq_terms wrote (any geometry).
+// InputSrc (round 6, MArgs::fast geometry): the terms computed from the inputs in the staging
+// step -- the chunk's gt / result loads are issued a chunk ahead (load) and the terms formed as
+// the chunk is staged to LDS (put) -- so no term planes are written or re-read (3.8 GB -> the
+// inputs' 6-8 B per pixel at C3).  Both stage band pixel c * SCH + u * 256 + lane * 4 + k of
+// plane pid[p] at L[p * SPS + u * 256 + lane * 4 + k], zeros past the band.
+template <int NPL>
+struct PlaneSrc {
+    static constexpr int NBUF = NPL;  // planes per LDS buffer (the wave's own)
+    const float* pl;
+    long long bandp;
+    float4 R[NPL][SNM];
+    __device__ __forceinline__ int boff(int p, const int (&)[NPL]) const { return p; }
+    __device__ __forceinline__ void sync() const { wave_sync(); }
+    __device__ __forceinline__ void load(long long c, const int (&pid)[NPL], int lane)
+    {
+#pragma unroll
+        for (int p = 0; p < NPL; ++p)
+#pragma unroll
+            for (int u = 0; u < SNM; ++u) {
+                const long long off = c * SCH + u * 256 + lane * 4;  // < bandp => off + 3 < bandp
+                R[p][u] = off < bandp ? *reinterpret_cast<const float4*>(pl + pid[p] * bandp + off)
+                                      : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+            }
+    }
+    __device__ __forceinline__ void put(float* L, const int (&pid)[NPL], int lane) const
+    {
+#pragma unroll
+        for (int p = 0; p < NPL; ++p)
+#pragma unroll
+            for (int u = 0; u < SNM; ++u)
+                *reinterpret_cast<float4*>(L + p * SPS + u * 256 + lane * 4) = R[p][u];
+    }
+};
+
+// SharedSrc: the block's producer waves (seq_produce) stage all four term planes of each chunk
+// in a shared double buffer; the chain waves read their planes from it and sync with the block
+template <int NPL>
+struct SharedSrc {
+    static constexpr int NBUF = 4;
+    __device__ __forceinline__ void load(long long, const int (&)[NPL], int) {}
+    __device__ __forceinline__ void put(float*, const int (&)[NPL], int) const {}
+    __device__ __forceinline__ int boff(int p, const int (&pid)[NPL]) const { return pid[p]; }
+    __device__ __forceinline__ void sync() const { __syncthreads(); }
+};
+
+// Producer wave pw of NP: the terms of chunk c (band pixels c * SCH ..), computed from gt and the
+// result (MArgs::fast: 16-B gt rows, w % 4 == 0, so a lane's 4 pixels share a row), all four
+// planes at L[k * SPS + u * 256 + lane * 4 + j]; zeros past the band.  Same per-pixel
+// arithmetic as k_seq_terms (eval4's fast form + seq_px), so the terms are bit-identical.
+template <bool LS>
+__device__ __forceinline__ void seq_produce(const MArgs& m, int b, int align_way, const Align& A,
+                                            long long band, long long c, float* L, int pw, int np,
+                                            int lane)
+{
+    for (int u = pw; u < SNM; u += np) {
+        const long long i0 = c * SCH + u * 256 + lane * 4;
+        float4 o[4];
+        if (i0 < band) {
+            const int r = (int)(i0 / m.w);
+            const long long px = (long long)(m.h0 + r) * m.w + (i0 - (long long)r * m.w);
+            const float4 g = *reinterpret_cast<const float4*>(m.gt + (long long)b * m.gstride + px);
+            const float G[4] = {g.x, g.y, g.z, g.w};
+            float V[4];
+            if (m.gv16) {
+                const uint2 q = *reinterpret_cast<const uint2*>(m.gv16 + (long long)b * m.vstride + px);
+                V[0] = u16_unit(q.x & 0xFFFFu), V[1] = u16_unit(q.x >> 16);
+                V[2] = u16_unit(q.y & 0xFFFFu), V[3] = u16_unit(q.y >> 16);
+            } else {
+                const float4 f = *reinterpret_cast<const float4*>(m.gv + (long long)b * m.vstride + px);
+                V[0] = f.x, V[1] = f.y, V[2] = f.z, V[3] = f.w;
+            }
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                float v0 = G[j], v1 = V[j];
+                const bool ok = finish_px(m, false, v0, v1);
+                o[j] = seq_px<LS>(v0, v1, ok, align_way, A);
+            }
+        } else {
+#pragma unroll
+            for (int j = 0; j < 4; ++j) o[j] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+        }
+        float* q = L + u * 256 + lane * 4;
+        *reinterpret_cast<float4*>(q) = make_float4(o[0].x, o[1].x, o[2].x, o[3].x);
+        *reinterpret_cast<float4*>(q + SPS) = make_float4(o[0].y, o[1].y, o[2].y, o[3].y);
+        *reinterpret_cast<float4*>(q + 2 * SPS) = make_float4(o[0].z, o[1].z, o[2].z, o[3].z);
+        *reinterpret_cast<float4*>(q + 3 * SPS) = make_float4(o[0].w, o[1].w, o[2].w, o[3].w);
+    }
+}
+
+// the producer waves' side of seq_chain's loop: one barrier before the first chunk and one per
+// chunk, as the chain waves (SharedSrc::sync)
+template <bool LS>
+__device__ __forceinline__ void seq_producers(const MArgs& m, int b, int align_way, const Align& A,
+                                              long long band, float* lds, int pw, int np, int lane)
+{
+    const long long nch = (band + SCH - 1) / SCH;
+    if (nch == 0) return;
+    seq_produce<LS>(m, b, align_way, A, band, 0, lds, pw, np, lane);
+    __syncthreads();
+    for (long long c = 0; c < nch; ++c) {
+        if (c + 1 < nch)
+            seq_produce<LS>(m, b, align_way, A, band, c + 1, lds + ((c + 1) & 1) * (4 * SPS), pw,
+                            np, lane);
+        __syncthreads();
+    }
+}
+
+template <int NPL, bool SQ, class Src>
+__device__ __forceinline__ float seq_chain(Src& src, long long band, const int (&pid)[NPL],
+                                           float* lds, uint32_t* cnt, int force = 0)
 {
     static_assert(!SQ || NPL == 1, "one squared chain per wave");
     constexpr int GRP = PF_SEQ_GRP, GQ = GRP / 4;  // pixels, float4 reads per group
     static_assert(SCH % GRP == 0 && SCH / GRP <= 64, "at most one group per lane");
     const int lane = threadIdx.x & 63;
-    constexpr int NM = SCH / 256;  // float4 loads per lane per plane and chunk
-    float4 R[NPL][NM];
-    auto load = [&](long long c) {
-#pragma unroll
-        for (int p = 0; p < NPL; ++p)
-#pragma unroll
-            for (int u = 0; u < NM; ++u) {
-                const long long off = c * SCH + u * 256 + lane * 4;  // < bandp => off + 3 < bandp
-                R[p][u] = off < bandp ? *reinterpret_cast<const float4*>(pl + pid[p] * bandp + off)
-                                      : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
-            }
-    };
-    auto put = [&](float* L) {
-#pragma unroll
-        for (int p = 0; p < NPL; ++p)
-#pragma unroll
-            for (int u = 0; u < NM; ++u)
-                *reinterpret_cast<float4*>(L + p * SPS + u * 256 + lane * 4) = R[p][u];
-    };
+    auto load = [&](long long c) { src.load(c, pid, lane); };
+    auto put = [&](float* L) { src.put(L, pid, lane); };
     const int my = lane < NPL ? lane : 0;
     float acc = 0.0f;
     uint32_t pos = 0;
@@ -585,11 +683,11 @@ __device__ __forceinline__ float seq_chain(const float* __restrict__ pl, long lo
     }
     load(0);
     put(lds);
-    wave_sync();
+    src.sync();
     for (long long c = 0; c < nch; ++c) {
         if (c + 1 < nch) load(c + 1);
-        const float* L = lds + (c & 1) * (NPL * SPS);
-        const float* Lm = L + my * SPS;
+        const float* L = lds + (c & 1) * (Src::NBUF * SPS);
+        const float* Lm = L + src.boff(my, pid) * SPS;
         const int n = (int)(band - c * SCH < SCH ? band - c * SCH : SCH);
         if (SQ && n < SCH) {  // the band's last, partial chunk: the reference's steps directly
             for (int j = 0; j < n; ++j) acc = sq_step(acc, Lm[j]);
@@ -659,11 +757,11 @@ __device__ __forceinline__ float seq_chain(const float* __restrict__ pl, long lo
             }
         }
         if (cnt) {
-            const float* Lc = L + (NPL - 1) * SPS;
+            const float* Lc = L + src.boff(NPL - 1, pid) * SPS;
             for (int i = lane; i < n; i += 64) pos += Lc[i] > 0.0f ? 1u : 0u;
         }
-        if (c + 1 < nch) put(lds + ((c + 1) & 1) * (NPL * SPS));
-        wave_sync();
+        if (c + 1 < nch) put(lds + ((c + 1) & 1) * (Src::NBUF * SPS));
+        src.sync();
     }
     if (cnt) {
         for (int o = 32; o > 0; o >>= 1) pos += __shfl_xor(pos, o);
@@ -675,14 +773,33 @@ __device__ __forceinline__ float seq_chain(const float* __restrict__ pl, long lo
 // Depth.cpp:2119-2134 in the reference's float order, one wave per panorama: lanes 0..3 add
 // a00 (v1*v1), a01 (v1), b0 (v0*v1), b1 (v0); a11 counts the compared pixels in a float, which
 // is the count itself up to 2^24 and stays at 2^24 after (2^24 + 1 rounds to even).
-__global__ __launch_bounds__(64) void k_ls_seq(SeqTerms T, long long band, Align* al)
+// FUSED (round 6, MArgs::fast geometry): the block's SEQ_NP producer waves form the terms from
+// gt and the result chunk by chunk into a shared LDS double buffer (seq_producers) while the
+// chain waves add the previous chunk -- no term planes in HBM (k_seq_terms wrote 2.25 GB of them
+// per C3 batch and the chains re-read 1.53 GB).  Else the chains read k_seq_terms' planes.
+constexpr int SEQ_NP = 4;
+
+template <bool FUSED>
+__global__ __launch_bounds__(64 * (1 + SEQ_NP)) void k_ls_seq(MArgs a, SeqTerms T, long long band,
+                                                               Align* al)
 {
     __shared__ float lds[2 * 4 * SPS];
-    const int b = blockIdx.x, lane = threadIdx.x;
+    const int b = blockIdx.x, lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     const int pid[4] = {0, 1, 2, 3};
     uint32_t n = 0;
-    const float r = seq_chain<4, false>(T.t + (long long)b * 4 * T.bandp, band, T.bandp, pid, lds,
-                                        &n);
+    float r;
+    if constexpr (FUSED) {
+        if (wv > 0) {
+            seq_producers<true>(a, b, 0, Align{1.0f, 0.0f, 0.0f, 0.0f, 0.0f}, band, lds, wv - 1,
+                                SEQ_NP, lane);
+            return;
+        }
+        SharedSrc<4> src;
+        r = seq_chain<4, false>(src, band, pid, lds, &n);
+    } else {
+        PlaneSrc<4> src{T.t + (long long)b * 4 * T.bandp, T.bandp};
+        r = seq_chain<4, false>(src, band, pid, lds, &n);
+    }
     const float a00 = __shfl(r, 0), a01 = __shfl(r, 1), b0 = __shfl(r, 2), b1 = __shfl(r, 3);
     const float a11 = (float)(n < (1u << 24) ? n : (1u << 24));
     if (lane != 0) return;
@@ -693,27 +810,52 @@ __global__ __launch_bounds__(64) void k_ls_seq(SeqTerms T, long long band, Align
     al[b] = A;
 }
 
-// Depth.cpp:2178-2186, 2207-2210 in the reference's order, three waves per panorama: mse (plane
-// 0) and mselog (plane 3) through the double square, one wave each; mae (plane 1) and mre (plane
-// 2) in float, lanes 0 and 1 of the third; the integer counts come from the parallel pass's
-// part[] (exact in any order).
-__global__ __launch_bounds__(192) void k_err_seq(SeqTerms T, long long band, const double* part,
-                                                 int nblk, const Align* al, pf_metrics* out,
-                                                 int force)
+// one chain wave of k_err_seq over the planes PIDS
+template <bool FUSED, bool SQ, int... PIDS>
+__device__ __forceinline__ float err_chain(const SeqTerms& T, long long band, int b, float* lds,
+                                           int force)
 {
-    __shared__ float lds_sq[2][2 * SPS];
-    __shared__ float lds_pl[2 * 2 * SPS];
+    constexpr int NPL = sizeof...(PIDS);
+    const int pid[NPL] = {PIDS...};
+    if constexpr (FUSED) {
+        SharedSrc<NPL> src;
+        return seq_chain<NPL, SQ>(src, band, pid, lds, nullptr, force);
+    } else {
+        PlaneSrc<NPL> src{T.t + (long long)b * 4 * T.bandp, T.bandp};
+        return seq_chain<NPL, SQ>(src, band, pid, lds, nullptr, force);
+    }
+}
+
+// Depth.cpp:2178-2186, 2207-2210 in the reference's order, three chain waves per panorama: mse
+// (plane 0) and mselog (plane 3) through the double square, one wave each; mae (plane 1) and mre
+// (plane 2) in float, lanes 0 and 1 of the third; the integer counts come from the parallel
+// pass's part[] (exact in any order).  FUSED: waves 3.. produce the terms (one shared buffer for
+// the three chains), else each chain wave stages its planes from k_seq_terms' output.
+template <bool FUSED>
+__global__ __launch_bounds__(64 * (3 + SEQ_NP)) void k_err_seq(MArgs a, int align_way, SeqTerms T,
+                                                                long long band, const double* part,
+                                                                int nblk, const Align* al,
+                                                                pf_metrics* out, int force)
+{
+    constexpr int BUF = FUSED ? 2 * 4 * SPS : 2 * SPS;
+    __shared__ float lds_sq[FUSED ? 1 : 2][BUF];
+    __shared__ float lds_pl[FUSED ? 1 : 2 * 2 * SPS];
     __shared__ float res[4];
     const int b = blockIdx.x, lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-    const float* pl = T.t + (long long)b * 4 * T.bandp;
-    if (wv < 2) {
-        const int pid[1] = {wv == 0 ? 0 : 3};
-        const float r = seq_chain<1, true>(pl, band, T.bandp, pid, lds_sq[wv], nullptr, force);
-        if (lane == 0) res[wv == 0 ? 0 : 3] = r;
-    } else {
-        const int pid[2] = {1, 2};
-        const float r = seq_chain<2, false>(pl, band, T.bandp, pid, lds_pl, nullptr);
+    float* l0 = lds_sq[0];
+    float* l1 = FUSED ? lds_sq[0] : lds_sq[FUSED ? 0 : 1];
+    float* l2 = FUSED ? lds_sq[0] : lds_pl;
+    if (wv == 0) {
+        const float r = err_chain<FUSED, true, 0>(T, band, b, l0, force);
+        if (lane == 0) res[0] = r;
+    } else if (wv == 1) {
+        const float r = err_chain<FUSED, true, 3>(T, band, b, l1, force);
+        if (lane == 0) res[3] = r;
+    } else if (wv == 2) {
+        const float r = err_chain<FUSED, false, 1, 2>(T, band, b, l2, 0);
         if (lane < 2) res[lane + 1] = r;
+    } else if constexpr (FUSED) {
+        seq_producers<false>(a, b, align_way, al[b], band, lds_sq[0], wv - 3, SEQ_NP, lane);
     }
     __syncthreads();
     if (threadIdx.x != 0) return;
@@ -801,8 +943,12 @@ void launch_metrics(hipStream_t s, const MetricsJob& j, void* ws, pf_metrics* ou
     // tests only: PF_METRICS_SEQ_FORCE_FIX=1 sends one step per chunk down the exact redo path
     const char* ff = getenv("PF_METRICS_SEQ_FORCE_FIX");
     const int seq_force = ff && ff[0] == '1' ? 1 : 0;
+    // the sequential sums form their terms from the inputs where the geometry is the fast one
+    // (PF_METRICS_SEQ_PLANES=1: the term planes of k_seq_terms, tests / A/B)
+    const char* sp = getenv("PF_METRICS_SEQ_PLANES");
+    const bool fused = a.fast && !(sp && sp[0] == '1');
     SeqTerms T{};
-    if (j.sequential) {
+    if (j.sequential && !fused) {
         T.bandp = (band + 3) & ~3LL;
         T.t = (float*)carve(sizeof(float) * 4 * T.bandp * j.batch);
     }
@@ -834,18 +980,26 @@ void launch_metrics(hipStream_t s, const MetricsJob& j, void* ws, pf_metrics* ou
             hipLaunchKernelGGL(k_ls_sums, grid, dim3(MB), 0, s, c, pc);
         }
         if (j.align_way == 2 && j.sequential) {  // least squares in the reference's float order
-            hipLaunchKernelGGL(k_seq_terms<true>, grid, dim3(MB), 0, s, c, 0, (const Align*)nullptr,
-                               Tc, band);
-            hipLaunchKernelGGL(k_ls_seq, dim3(nb), dim3(64), 0, s, Tc, band, ac);
+            if (fused) {
+                hipLaunchKernelGGL(k_ls_seq<true>, dim3(nb), dim3(64 * (1 + SEQ_NP)), 0, s, c, Tc,
+                                   band, ac);
+            } else {
+                hipLaunchKernelGGL(k_seq_terms<true>, grid, dim3(MB), 0, s, c, 0,
+                                   (const Align*)nullptr, Tc, band);
+                hipLaunchKernelGGL(k_ls_seq<false>, dim3(nb), dim3(64), 0, s, c, Tc, band, ac);
+            }
         } else {
             hipLaunchKernelGGL(k_align, dim3(nb), dim3(64), 0, s, j.align_way, sc, pc, MNBLK, ac);
         }
         hipLaunchKernelGGL(k_err_sums, grid, dim3(MB), 0, s, c, j.align_way, ac, pc);
-        if (j.sequential) {
+        if (j.sequential && fused) {
+            hipLaunchKernelGGL(k_err_seq<true>, dim3(nb), dim3(64 * (3 + SEQ_NP)), 0, s, c,
+                               j.align_way, Tc, band, pc, MNBLK, ac, out + b0, seq_force);
+        } else if (j.sequential) {
             hipLaunchKernelGGL(k_seq_terms<false>, grid, dim3(MB), 0, s, c, j.align_way, ac, Tc,
                                band);
-            hipLaunchKernelGGL(k_err_seq, dim3(nb), dim3(192), 0, s, Tc, band, pc, MNBLK, ac,
-                               out + b0, seq_force);
+            hipLaunchKernelGGL(k_err_seq<false>, dim3(nb), dim3(192), 0, s, c, j.align_way, Tc,
+                               band, pc, MNBLK, ac, out + b0, seq_force);
         } else {
             hipLaunchKernelGGL(k_err_final, dim3(nb), dim3(MB), 0, s, pc, MNBLK, ac, out + b0);
         }
