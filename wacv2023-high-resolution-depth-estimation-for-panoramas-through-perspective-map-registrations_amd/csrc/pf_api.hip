@@ -2498,9 +2498,7 @@ int pf_error_metrics(pf_ctx* c, const float* gt, int gw, int gh, int gc, const f
     j.cap_depth = cap_depth ? 1 : 0;
     j.sequential = c->metrics_order == PF_METRICS_SEQUENTIAL ? 1 : 0;
     int rc;
-    if ((rc = ensure(c, c->metrics_ws,
-                     metrics_workspace_bytes(batch, (long long)(j.h1 - j.h0 + 1) * w,
-                                             j.sequential != 0))))
+    if ((rc = ensure(c, c->metrics_ws, metrics_workspace_bytes(j))))
         return rc;
     // algorithmic bytes: one read of the compared band of gt (4 B, channel 0) and of the
     // result (2 B u16 / 4 B f32); the kernels make 4 passes (3 radix digits + the sums) for

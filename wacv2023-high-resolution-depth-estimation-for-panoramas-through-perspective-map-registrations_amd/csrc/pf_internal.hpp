@@ -430,7 +430,7 @@ struct MetricsJob {
     int align_way, cap_depth;
     int sequential;  // the reference's summation order (PF_METRICS_SEQUENTIAL)
 };
-size_t metrics_workspace_bytes(int batch, long long band, bool sequential);
+size_t metrics_workspace_bytes(const MetricsJob& j);
 void launch_d2d_map(hipStream_t s, float* data, long long npx, int c, const float* abcd);
 void launch_metrics(hipStream_t s, const MetricsJob& j, void* ws, pf_metrics* out);
 

@@ -892,8 +892,28 @@ static size_t seq_bytes(long long band, int batch)
     return (size_t)((band + 3) & ~3LL) * 4 * batch * sizeof(float) + 256;
 }
 
-size_t metrics_workspace_bytes(int batch, long long band, bool sequential)
+// MArgs::fast: gt and the result share the geometry, one channel, 16-B aligned 4-pixel groups
+static bool metrics_fast(const MetricsJob& j)
 {
+    const int gvc = j.given16 ? 1 : j.gc_given;
+    return j.gw == j.w && j.gh == j.h && j.gc == 1 && gvc == 1 && j.w % 4 == 0 &&
+           ((uintptr_t)j.gt & 15) == 0 &&
+           (j.given16 ? ((uintptr_t)j.given16 & 7) == 0 : ((uintptr_t)j.given & 15) == 0);
+}
+
+// the sequential order's terms: formed in the chain kernels (fast geometry), else term planes
+// in the workspace (k_seq_terms; PF_METRICS_SEQ_PLANES=1 forces them: tests / A/B)
+static bool metrics_seq_planes(const MetricsJob& j)
+{
+    const char* sp = getenv("PF_METRICS_SEQ_PLANES");
+    return j.sequential && (!metrics_fast(j) || (sp && sp[0] == '1'));
+}
+
+size_t metrics_workspace_bytes(const MetricsJob& j)
+{
+    const int batch = j.batch;
+    const long long band = (long long)(j.h1 - j.h0 + 1) * j.w;
+    const bool sequential = metrics_seq_planes(j);
     const size_t hist = sizeof(uint32_t) * 2 * HBINS * batch;
     const size_t st = sizeof(SelState) * 2 * batch;
     const size_t part = sizeof(double) * (NSUM + 1) * MNBLK * batch;
@@ -925,9 +945,7 @@ void launch_metrics(hipStream_t s, const MetricsJob& j, void* ws, pf_metrics* ou
     const float to_matterport = 65535.0f / 4000.0f;  // Depth.cpp:1999-2000
     a.depth_max = 10.0f / to_matterport;
     a.abs_median = j.given16 ? 0 : 1;
-    a.fast = j.gw == j.w && j.gh == j.h && j.gc == 1 && a.gvc == 1 && j.w % 4 == 0 &&
-             ((uintptr_t)j.gt & 15) == 0 &&
-             (j.given16 ? ((uintptr_t)j.given16 & 7) == 0 : ((uintptr_t)j.given & 15) == 0);
+    a.fast = metrics_fast(j) ? 1 : 0;
 
     char* p = (char*)ws;
     auto carve = [&](size_t bytes) {
@@ -943,10 +961,7 @@ void launch_metrics(hipStream_t s, const MetricsJob& j, void* ws, pf_metrics* ou
     // tests only: PF_METRICS_SEQ_FORCE_FIX=1 sends one step per chunk down the exact redo path
     const char* ff = getenv("PF_METRICS_SEQ_FORCE_FIX");
     const int seq_force = ff && ff[0] == '1' ? 1 : 0;
-    // the sequential sums form their terms from the inputs where the geometry is the fast one
-    // (PF_METRICS_SEQ_PLANES=1: the term planes of k_seq_terms, tests / A/B)
-    const char* sp = getenv("PF_METRICS_SEQ_PLANES");
-    const bool fused = a.fast && !(sp && sp[0] == '1');
+    const bool fused = !metrics_seq_planes(j);  // (sequential order only)
     SeqTerms T{};
     if (j.sequential && !fused) {
         T.bandp = (band + 3) & ~3LL;
