@@ -316,8 +316,8 @@ int pf_error_metrics(pf_ctx* ctx, const float* gt, int gw, int gh, int gc, const
  *     1e-2 of the reference's drifting float sums).
  *   PF_METRICS_SEQUENTIAL -- "bit-exact means": the reference's order, row-major float
  *     accumulators (mse and mselog through a double add, Depth.cpp:2119-2123, 2178-2186);
- *     bit-exact to it (mselog within 1e-5: device log10f).  The per-pixel terms are computed in
- *     parallel and summed as verified fp32 chains: ~7.8 ms per 64-panorama call at C3.
+ *     bit-exact to it (mselog within 1e-5: device log10f).  The per-pixel terms are formed by
+ *     producer waves beside verified fp32 chains: ~7.4 ms per 64-panorama call at C3.
  * The facade (include/pf_depth.h) and panofuse_main default to PF_METRICS_SEQUENTIAL, the order
  * the reference prints; PF_METRICS_ORDER=tree / --metrics-order tree select the tree. */
 #define PF_METRICS_TREE 0

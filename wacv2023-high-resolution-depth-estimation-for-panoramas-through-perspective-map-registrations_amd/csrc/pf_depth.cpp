@@ -47,7 +47,7 @@ pf_ctx* facade_ctx()
     }
     // ErrorData / ErrorEmap summation order: the facade mirrors Depth.cpp, so by default it sums
     // in the reference's row-major float order (the means the reference prints, bit for bit;
-    // ~7.8 ms per 64-panorama call, well under a millisecond more at the facade's batch 1).
+    // ~7.4 ms per 64-panorama call, well under a millisecond more at the facade's batch 1).
     // PF_METRICS_ORDER=tree (panofuse_main --metrics-order tree) opts into the fp64 tree.
     const char* mo = std::getenv("PF_METRICS_ORDER");
     pf_set_metrics_order(c, mo && std::strcmp(mo, "tree") == 0 ? PF_METRICS_TREE

@@ -250,7 +250,7 @@ class Fuser:
 
     def set_metrics_order(self, order):
         """"tree" (the context's default): fp64 partial sums (fast, means within 1e-5 of exact
-        sums); "sequential": the reference's float summation order, bit-exact means (~7.8 ms per
+        sums); "sequential": the reference's float summation order, bit-exact means (~7.4 ms per
         64-panorama call at C3; the facade and panofuse_main default to it)."""
         self._check(self.L.pf_set_metrics_order(self.h, METRICS_ORDERS[order]))
 
