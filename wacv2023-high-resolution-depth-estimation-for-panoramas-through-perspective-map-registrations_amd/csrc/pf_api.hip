@@ -2124,13 +2124,16 @@ int pf_rows_add_batch(pf_ctx* c, float* const* dst, const float* const* src, con
     int rc;
     if ((rc = check_common(c, 1))) return rc;
     if (count < 0 || (count > 0 && (!dst || !src || !n))) return fail(c, PF_EINVAL, "bad rows add batch");
-    for (int k0 = 0; k0 < count; k0 += kRowsAddBatch) {
+    for (int k = 0; k < count; k++)  // every segment checked before any is added
+        if (n[k] < 0 || (n[k] > 0 && (!dst[k] || !src[k])))
+            return fail(c, PF_EINVAL, "bad rows add segment %d", k);
+    // launches of up to kRowsAddBatch non-empty segments; k walks the list once (empty segments
+    // are skipped, so a launch may span more than kRowsAddBatch entries)
+    for (int k = 0; k < count;) {
         RowsAddBatch B{};
         int m = 0;
         long long nmax = 0;
-        for (int k = k0; k < count && m < kRowsAddBatch; k++) {
-            if (n[k] < 0 || (n[k] > 0 && (!dst[k] || !src[k])))
-                return fail(c, PF_EINVAL, "bad rows add segment %d", k);
+        for (; k < count && m < kRowsAddBatch; k++) {
             if (n[k] == 0) continue;
             B.dst[m] = dst[k];
             B.src[m] = src[k];
