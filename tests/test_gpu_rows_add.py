@@ -12,6 +12,7 @@ torch = pytest.importorskip("torch")
 pytestmark = pytest.mark.gpu
 
 import panofuse  # noqa: E402
+import pf_layouts as PL  # noqa: E402
 
 DEV = "cuda:0"
 
@@ -20,7 +21,9 @@ DEV = "cuda:0"
 def fuser():
     if not torch.cuda.is_available():
         pytest.fail("GPU test collected on a host without a GPU")
-    return panofuse.Fuser(0)
+    f = panofuse.Fuser(0)
+    f.set_tiles(PL.config_layout("C1"))  # the row entry points check for a layout, as in the flow
+    return f
 
 
 def test_rows_add_batch_equals_single_adds(fuser):
