@@ -326,6 +326,7 @@ def c5_measure(args, rank, world, local, dev, steps, warmup):
 # third).  Each rank's compute is measured: the sharded flow of rank r of 8 run alone on this GPU
 # with a communicator that moves nothing (pf_dist.NullComm), its own tiles warped and registered
 # first (hipEvents).  Predicted = max over ranks (compute) + rounds x latency + max bytes / rate.
+LANE_SHARE = 1.0  # the chip share the fusion lanes plan for (set by lane_steps)
 XCHG_LAT_US = 20.0
 XCHG_GBS = 50.0
 
@@ -587,6 +588,15 @@ def lane_steps(fz, lay, local, dev, gt, emap, resp, tiles, out, coeffs, zr, nlan
         f = panofuse.Fuser(local, stream=torch.cuda.Stream(dev))
         f.set_tiles(lay)
         lanes.append((f, torch.empty_like(tiles), torch.empty_like(out), torch.empty_like(coeffs)))
+    # Jacobi pass plans for concurrent fusions: two lanes offset by about half a step overlap
+    # their Jacobi stages about half the time, so a lane's expected share of the chip is ~3/4 and
+    # its levels take fewer, longer row chunks (less total work; round 6 A/B, DESIGN.md section 5:
+    # levels 1 / 2 in 2 / 3 chunks instead of 3 / 4, +1.5 %).  PF_LANE_SHARE overrides (A/B runs).
+    global LANE_SHARE
+    share = float(os.environ.get("PF_LANE_SHARE", 1.0 - (nlanes - 1) / (2.0 * nlanes)))
+    LANE_SHARE = share
+    for f, *_ in lanes:
+        f.set_jacobi_share(share)
     st = {"k": 0}
     # every lane is itself pipelined (bench.pipelined_step: its warps on a stream of their own,
     # its fusions on the lane's stream); PF_LANE_WARP=0 (A/B runs): warp and fusion in line
@@ -838,6 +848,18 @@ def main():
     prof = {k: (nps * sorted(p[k][0] for p in per_step)[nps // 2],  # median ms x steps
                 sum(p[k][1] for p in per_step), sum(p[k][2] for p in per_step))
             for k in per_step[0]}
+    # The lanes plan their passes for a share of the chip (lane_steps); the profiled steps above
+    # run those plans, as the timed steps do.  For the record, the Jacobi stage with the
+    # whole-chip plan (the serial step's; fewer rows per chunk, more waves) on the same batch.
+    jserial = None
+    if args.pipeline >= 2:
+        fz.set_jacobi_share(1.0)
+        js = []
+        for _ in range(max(1, args.prof_steps)):
+            step()
+            js.append(fz.profile_read()["jacobi"][0])
+        jserial = sorted(js)[len(js) // 2]
+        fz.set_jacobi_share(LANE_SHARE)
     # Accuracy metrics (ErrorData of each result against its ground truth, median alignment,
     # Depth.cpp:1980-2213): not part of the step (the reference computes them only when a
     # ground-truth file is given), timed the same way on the same batch.
@@ -983,7 +1005,14 @@ def main():
                          "flop_per_step": jbytes / 12.0 * 14.0 / nprof if nprof else None,
                          "updates_per_step": jbytes / 12.0 / nprof,
                          "traffic_source": "profiles/pmc_traffic.json (FETCH_SIZE + WRITE_SIZE "
-                                           "per launch of k_jlag and k_jres, scaled to one step)"},
+                                           "per launch of k_jlag and k_jres, scaled to one step)",
+                         "plan": (f"lane plan (pf_set_jacobi_share {LANE_SHARE:.2f}: the levels' "
+                                  "row chunks re-cut for concurrent lanes), as in the timed steps")
+                         if args.pipeline >= 2 else "whole-chip plan",
+                         "whole_chip_plan": ({"ms_per_step": jserial,
+                                              "frac": jbytes / nprof / 12.0 * 14.0
+                                              / (jserial * 1e-3) / 1e12 / VALU_PEAK_TF}
+                                             if jserial else None)},
             # the same stage on the HBM roof with its MEASURED traffic (temporal blocking moves
             # T sweeps per pass through HBM once; the resident kernel reads the level once), and
             # the 12 B/update algorithmic rate of SURVEY.md 8d as an "effective" bandwidth (>

@@ -255,6 +255,15 @@ int pf_stream_wait_level(pf_ctx* ctx, int level, void* hip_stream);
  * streaming temporally blocked passes everywhere. */
 int pf_set_jacobi_engine(pf_ctx* ctx, int mode, int row_blocks);
 
+/* ---- Jacobi pass planning for concurrent fusions (no reference counterpart) ----
+ * The streaming passes cut each level's band into row chunks by a cost model of the chip's wave
+ * slots (more chunks: more waves, but every chunk re-runs a T-row fill).  Contexts whose fusions
+ * run concurrently on one GPU (several fusion lanes) each see only part
+ * of the chip: `share` (0 < share <= 1, default 1) is the fraction this context's plans count
+ * on, so they take fewer, longer chunks -- less total work.  Results are bit-identical for any
+ * share (the chunking never changes a value).  PF_EINVAL for a share outside (0, 1]. */
+int pf_set_jacobi_share(pf_ctx* ctx, double share);
+
 /* ---- resident level kernel health (no reference counterpart) ----
  * The coarse fusion level runs all its sweeps in one launch whose row blocks trade halo rows
  * through device memory (pf_jres.hip).  Its waits are bounded: a wait that times out is counted

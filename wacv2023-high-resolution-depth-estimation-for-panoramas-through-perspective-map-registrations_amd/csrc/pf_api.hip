@@ -108,6 +108,7 @@ struct pf_ctx {
     DevBuf jres_x, jres_sync;
     uint32_t jres_tk = 0, jres_fb = 1;
     int jres_mode = -1, jres_nb = 0;  // pf_set_jacobi_engine (-1: not set, PF_JRES decides)
+    double jacobi_share = 1.0;  // pf_set_jacobi_share: the chip share the pass plans assume
     // timeout reporting: a resident launch whose wait times out also raises this flag in
     // coherent pinned host memory (a system-scope store from the kernel, no extra stream work);
     // jres_check reports a raised flag once as PF_ETIMEOUT and lowers it
@@ -395,6 +396,20 @@ int pf_stream_wait_level(pf_ctx* c, int level, void* hip_stream)
     if (!c || level < 0 || level >= c->nlev_recorded || !c->ev_level[level]) return PF_EINVAL;
     HIPCHK(c, hipStreamWaitEvent((hipStream_t)hip_stream, c->ev_level[level], 0));
     return PF_OK;
+}
+
+int pf_set_jacobi_share(pf_ctx* c, double share)
+{
+    if (!c || !(share > 0.0 && share <= 1.0)) return PF_EINVAL;
+    c->jacobi_share = share;
+    return PF_OK;
+}
+
+// SIMDs the pass plans of this context count on: the chip times the context's share
+static int plan_simds(const pf_ctx* c)
+{
+    const int n = (int)(4.0 * c->num_cu * c->jacobi_share + 0.5);
+    return n < 4 ? 4 : n;
 }
 
 int pf_set_jacobi_engine(pf_ctx* c, int mode, int row_blocks)
@@ -1025,6 +1040,15 @@ static std::vector<PassPlan> plan_level(pf_ctx* c, const LevelDims& L, int C, in
         }
     std::vector<PassPlan> plan;
     for (int r = L.iters; r > 0; r -= choice[r]) plan.push_back(opt[choice[r]]);
+    // a context that shares the chip with concurrent fusions (pf_set_jacobi_share) keeps the
+    // depths and engines chosen for the whole chip and re-chunks its streaming passes for its
+    // share: fewer, longer row chunks
+    if (c->jacobi_share < 1.0)
+        for (PassPlan& pp : plan)
+            if (pp.stages == 1)
+                pp.nchunks = best_chunks(pp.T, C, band_rows, L.w, batch,
+                                         jstream_waves_per_cu(C, pp.T, fast) / 4, plan_simds(c),
+                                         tune.step_overhead, tune.lone_cycles, tune.c4_eff).nchunks;
     // tuning runs: PF_JN<w> forces the row chunking of the level of width w
     char key[32];
     snprintf(key, sizeof(key), "PF_JN%d", L.w);
@@ -2410,7 +2434,7 @@ int pf_fuse_band_pass(pf_ctx* c, const float* emap, int ew, int eh, int ec, cons
     static const JacobiTuning tune = jacobi_tuning();
     const int band = row1 - row0;
     PassPlan pp = best_chunks(T, 2, band, L.w, 1, jstream_waves_per_cu(2, T, fast) / 4,
-                              4 * c->num_cu, tune.step_overhead, tune.lone_cycles, tune.c4_eff);
+                              plan_simds(c), tune.step_overhead, tune.lone_cycles, tune.c4_eff);
     const long long st = (long long)L.w * L.h;
     JacobiPass P{};
     if (src_mode == 2) {

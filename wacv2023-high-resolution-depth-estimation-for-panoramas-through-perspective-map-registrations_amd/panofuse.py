@@ -32,12 +32,12 @@ EXPORTS = [
     "pf_probe_warp_coords", "pf_probe_rgb_taps", "pf_debug_smooth_fault",
     "pf_fuse_partial_rows", "pf_fuse_coverage_rows", "pf_fuse_normalize_rows",
     "pf_fuse_tile_rows", "pf_rows_add", "pf_fuse_level", "pf_fuse_targets",
-    "pf_rows_add_batch",
+    "pf_rows_add_batch", "pf_set_jacobi_share",
 ]
 NEW_R4 = {"pf_debug_jres_fault", "pf_probe_warp_coords", "pf_probe_rgb_taps",
           "pf_debug_smooth_fault", "pf_fuse_partial_rows", "pf_fuse_coverage_rows",
           "pf_fuse_normalize_rows", "pf_fuse_tile_rows", "pf_rows_add", "pf_fuse_level",
-          "pf_fuse_targets", "pf_rows_add_batch"}
+          "pf_fuse_targets", "pf_rows_add_batch", "pf_set_jacobi_share"}
 METRICS_ORDERS = {"tree": 0, "sequential": 1}  # PF_METRICS_*; "sequential" = the reference's
 SOLVERS = {"normal": 0, "lm": 1}  # PF_SOLVER_*; "lm" = the reference's Ceres LM (default)
 
@@ -128,6 +128,7 @@ def load():
         if hasattr(L, name):
             getattr(L, name).argtypes = at
     L.pf_set_jacobi_engine.argtypes = [vp, ip, ip]
+    L.pf_set_jacobi_share.argtypes = [vp, C.c_double]
     L.pf_stream_wait_level.argtypes = [vp, ip, vp]
     L.pf_profile_read.argtypes = [vp, C.POINTER(C.c_double), C.POINTER(C.c_double),
                                   C.POINTER(C.c_longlong)]
@@ -463,6 +464,11 @@ class Fuser:
         """Jacobi engine of the fusion levels: the resident one-launch kernel where it applies
         (default) or the streaming passes; row_blocks forces its blocks per panorama."""
         self._check(self.L.pf_set_jacobi_engine(self.h, 1 if resident else 0, int(row_blocks)))
+
+    def set_jacobi_share(self, share):
+        """Fraction of the GPU this context's Jacobi pass plans count on (0 < share <= 1): for
+        fusions that run concurrently with others on the same device (pf_set_jacobi_share)."""
+        self._check(self.L.pf_set_jacobi_share(self.h, float(share)))
 
     def jres_errors(self):
         """Timed-out hand-off waits of the resident level kernel so far (0 = every resident
