@@ -67,3 +67,25 @@ def test_forced_chunks_bit_exact(inputs, env):
     bad = int((out != ref).sum())
     assert bad == 0, f"{env}: {bad} pixels differ from the default plan's fusion"
     assert np.count_nonzero(out.cpu().numpy()) > 0
+
+
+@pytest.mark.parametrize("share", [0.75, 0.3, 0.01])
+def test_jacobi_share_bit_exact(inputs, share):
+    """pf_set_jacobi_share (round 6): a context planning for part of the chip re-cuts its passes
+    into fewer, longer row chunks; the output stays the whole-chip plan's bit for bit."""
+    f, emap, tiles, coeffs, ref = inputs
+    f.set_jacobi_share(share)
+    try:
+        out = torch.zeros_like(ref)
+        f.fuse(emap, tiles, out, PL.ZENITH_RANGE, coeffs=coeffs)
+        torch.cuda.synchronize()
+    finally:
+        f.set_jacobi_share(1.0)
+    assert torch.equal(out, ref)
+
+
+def test_jacobi_share_rejects_out_of_range(inputs):
+    f = inputs[0]
+    for bad in (0.0, -0.5, 1.5, float("nan")):
+        with pytest.raises(panofuse.PanofuseError):
+            f.set_jacobi_share(bad)
