@@ -317,9 +317,36 @@ def test_row_sharded_fusion_gloo(world, rep):
     assert [(r, ok) for r, ok, _, _ in res] == [(r, True) for r in range(world)], res
     # world 2 deals the C1 layout band by band (tiles 0-2 = the upper zenith band), so only
     # halo-sized rows travel: per rank the target rows it sends are at most its neighbour's halo
-    # plus the shared boundary row (K + 1 <= 12 rows of <= 512 floats, 3 levels), far below a
-    # full plane.  (World 3 deals 2 tiles per rank across the bands: the bands fall back to an
-    # even split and more rows travel -- still exactly the model's bytes.)
+    # plus the shared boundary row (K + 1 rows of <= 512 floats, 3 levels; K = halo_rows(plan):
+    # 11 for passes of 10 with one exchange each, more with grouped passes), far below a plane.
+    # (World 3 deals 2 tiles per rank across the bands: the bands fall back to an even split and
+    # more rows travel -- still exactly the model's bytes.)
     if world == 2 and rep == 0:
+        K = pf_dist.halo_rows([10] * 5, max(pf_dist.PASS_GROUP, 2))
         for _, _, sent, _ in res:
-            assert 0 < sent.get("targets", 0) <= 3 * 12 * 512 * 4, sent
+            assert 0 < sent.get("targets", 0) <= 3 * (K + 1) * 512 * 4, sent
+
+
+def test_pass_groups_pair_the_exchanges():
+    """Grouped passes (round 6): one exchange per run of G passes after the first, sum(T + 1)
+    rows, each pass of a run computing the rows past the band the rest of its run reads; G = 1:
+    T + 1 before every pass but the first."""
+    plan = [10, 10, 10, 8, 8, 5]
+    assert pf_dist.pass_groups(plan, 1) == [(0, 0), (11, 0), (11, 0), (9, 0), (9, 0), (6, 0)]
+    assert pf_dist.pass_groups(plan, 2) == [(0, 0), (22, 11), (0, 0), (18, 9), (0, 0), (6, 0)]
+    assert pf_dist.pass_groups(plan, 3) == [(0, 0), (31, 20), (0, 9), (0, 0), (15, 6), (0, 0)]
+    assert pf_dist.halo_rows(plan, 2) == 22 and pf_dist.halo_rows(plan, 1) == 11
+    assert pf_dist.pass_groups([10], 4) == [(0, 0)]
+    # the group a level gets: the largest whose halo every band supplies
+    g, K, b = pf_dist.level_geometry(0, 99, 4, None, [10] * 9, gmax=4)
+    assert (g, K) == (2, 22) and min(b[r + 1] - b[r] for r in range(4)) >= K
+    g, K, _ = pf_dist.level_geometry(0, 999, 4, None, [10] * 9, gmax=4)
+    assert (g, K) == (4, 44)
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_row_sharded_fusion_gloo_one_exchange_per_pass(world, monkeypatch):
+    """The one-exchange-per-pass flow (PF_C5_GROUP=1, pf_dist.PASS_GROUP) stays bit-exact with its
+    own byte model."""
+    monkeypatch.setenv("PF_C5_GROUP", "1")  # the spawned workers import pf_dist afresh
+    test_row_sharded_fusion_gloo(world, 0)

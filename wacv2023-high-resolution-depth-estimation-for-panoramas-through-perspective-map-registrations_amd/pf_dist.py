@@ -18,6 +18,7 @@
 The reference has no distributed code; this replaces its single-process OpenMP tile loop
 (Depth.cpp:1492-1624).
 """
+import os
 
 
 def shard_range(n, rank, world):
@@ -307,6 +308,50 @@ class NullComm:
         return list(values)
 
 
+# Communication-avoiding pass halos (round 6): the passes after a level's first go in groups of up
+# to PASS_GROUP with one halo exchange per group (PF_C5_GROUP=1: one exchange per pass, the
+# round-5 flow).  A level takes the largest group size whose halo its thinnest band can supply.
+PASS_GROUP = max(1, int(os.environ.get("PF_C5_GROUP", "4")))
+
+
+def pass_groups(plan, group=2):
+    """Per pass i of a row-sharded level: (k, ext).  k > 0: the halo rows exchanged with each
+    neighbour before the pass (0: none); ext: the rows the pass computes past each side of the
+    band.  A pass of depth T on rows [r0, r1) reads rows [r0 - T - 1, r1 + T + 1) (T sweeps, plus
+    the row a virtual column wraps into).  group 1: every pass but the first exchanges T + 1 rows.
+    group G: the passes after the first in runs of G share one exchange of sum(T + 1) rows, and
+    each computes the rows past the band that the rest of its run reads (sum of their T + 1):
+    1/G of the exchange rounds for the same bytes, some rows computed twice -- by the rank and by
+    its neighbour, bit-identically."""
+    out = [(0, 0)] if plan else []
+    for s0 in range(1, len(plan), max(1, group)):
+        run = plan[s0:s0 + max(1, group)]
+        need = [T + 1 for T in run]
+        for j in range(len(run)):
+            out.append((sum(need) if j == 0 else 0, sum(need[j + 1:])))
+    return out
+
+
+def halo_rows(plan, group=2):
+    """The rows past its band a rank's passes read or compute on (targets, previous-level rows):
+    the largest exchange of pass_groups, and the first pass's T + 1."""
+    return max([plan[0] + 1] + [k for k, _ in pass_groups(plan, group)])
+
+
+def level_geometry(h0, h1, world, ext, plan, gmax=None):
+    """(group, K, bounds) of a row-sharded level: the largest pass group <= gmax whose halo K
+    every band can supply (band_bounds' layout-dealt bands if thick enough, else the even split),
+    falling back to group 1.  A function of the layout and the plan: identical on every rank and
+    in exchange_model."""
+    gmax = PASS_GROUP if gmax is None else gmax
+    for g in range(max(1, gmax), 0, -1):
+        K = halo_rows(plan, g)
+        bnd = band_bounds(h0, h1, world, ext, K)
+        if g == 1 or min(bnd[r + 1] - bnd[r] for r in range(world)) >= K:
+            return g, K, bnd
+    raise AssertionError("unreachable")
+
+
 def fuse_row_sharded(backend, nlevels, ntiles, rank, world, comm=None, log=None, rep_levels=0):
     """One panorama's fusion with tiles AND rows sharded over `world` ranks.
 
@@ -364,19 +409,20 @@ def fuse_row_sharded(backend, nlevels, ntiles, rank, world, comm=None, log=None,
                 # count, occupancy, PF_J* overrides -- and mismatched passes would hang the
                 # exchanges)
                 plan = comm.agree(plan, 0, getattr(backend, "device", None))
-            K = max(plan) + 1
             ext = [backend.tile_rows(level, *shard_range(ntiles, r, world)) for r in range(world)]
+            group = 1
             if rep:
+                K = max(plan) + 1
                 bnd = [h0] + [h1 + 1] * world  # rank 0's band is the level; all sweep it
                 need = [(h0, h1 + 1)] * world
             else:
-                bnd = band_bounds(h0, h1, world, ext, K)
+                group, K, bnd = level_geometry(h0, h1, world, ext, plan)
                 if world > 1 and min(bnd[r + 1] - bnd[r] for r in range(world)) < K:
                     raise ValueError(f"level {level}: {h1 - h0 + 1} band rows over {world} ranks "
                                      f"leave bands thinner than the {K}-row halo")
                 need = [(max(h0, bnd[d] - K), min(h1 + 1, bnd[d + 1] + K))
                         for d in range(world)]
-            geo[key] = (plan, K, ext, bnd, need)
+            geo[key] = (plan, K, ext, bnd, need, group)
         G.append((rep, geo[key]))
     if world == 1:  # nothing travels: each level's normalised targets from every tile
         for level in range(nlevels):
@@ -398,7 +444,7 @@ def fuse_row_sharded(backend, nlevels, ntiles, rank, world, comm=None, log=None,
     def targets_alloc(levels):
         st = {"sends": [], "recvs": [], "bufs": [], "levels": list(levels)}
         for level in levels:
-            rep, (plan, K, ext, bounds, need) = G[level]
+            rep, (plan, K, ext, bounds, need, group) = G[level]
             w = backend.dims(level)[0]
             lsum = backend.plane(level)
             mlo, mhi = ext[rank][0], ext[rank][1] + 1
@@ -419,7 +465,7 @@ def fuse_row_sharded(backend, nlevels, ntiles, rank, world, comm=None, log=None,
 
     def targets_compute(st):
         for level in st["levels"]:
-            rep, (plan, K, ext, bounds, need) = G[level]
+            rep, (plan, K, ext, bounds, need, group) = G[level]
             e0, e1 = need[rank]
             lsum = tgt[level][0]
             mlo, mhi = ext[rank][0], ext[rank][1] + 1
@@ -482,7 +528,7 @@ def fuse_row_sharded(backend, nlevels, ntiles, rank, world, comm=None, log=None,
             targets_compute(early)
     for level in range(nlevels):
         last = level == nlevels - 1
-        rep, (plan, K, ext, bounds, need) = G[level]
+        rep, (plan, K, ext, bounds, need, group) = G[level]
         if level == nrep:
             if early is not None:
                 # the exchange and adds follow the side stream's tile sums only, not the sweeps
@@ -526,9 +572,10 @@ def fuse_row_sharded(backend, nlevels, ntiles, rank, world, comm=None, log=None,
         if rank == 0 or rank == world - 1:  # the rows above / below the band
             backend.border(level, prev, a, b)
         src, dst = None, a
+        groups = pass_groups(plan, group)
         for i, T in enumerate(plan):
-            if i > 0:
-                k = T + 1
+            k, xt = groups[i]
+            if k:
                 hsends, hrecvs = [], []
                 if rank > 0:
                     lo_ = max(r0 - k, h0)
@@ -543,7 +590,8 @@ def fuse_row_sharded(backend, nlevels, ntiles, rank, world, comm=None, log=None,
                     log.add("pass_halo", sum(4 * t.numel() for _, t in hsends))
             mode = (2 if level == 0 else 1) if i == 0 else 0
             fin = last and i == len(plan) - 1
-            backend.band_pass(level, lnorm, mode, src, dst, T, r0, r1, fin, prev)
+            backend.band_pass(level, lnorm, mode, src, dst, T, max(r0 - xt, h0),
+                              min(r1 + xt, h1 + 1), fin, prev)
             src, dst = dst, (b if dst is a else a)
         prev, pbounds = (None if last else src), bounds
     bounds = G[-1][1][3]
@@ -582,7 +630,6 @@ def exchange_model(dims, plans, ext, world, multicover=None, rep_levels=0):
         return res
     pb = None
     for lv, (w, h, h0, h1) in enumerate(dims):
-        K = max(plans[lv]) + 1
         if lv < rep_levels:  # replicated: every rank's tile rows to every other rank
             for r in range(world):
                 lo, hi = ext[lv][r][0], ext[lv][r][1] + 1
@@ -592,7 +639,7 @@ def exchange_model(dims, plans, ext, world, multicover=None, rep_levels=0):
                     add(r, "multicover", 4 * multicover[lv])
             pb = None
             continue
-        b = band_bounds(h0, h1, world, ext[lv], K)
+        group, K, b = level_geometry(h0, h1, world, ext[lv], plans[lv])
         need = [(max(h0, b[d] - K), min(h1 + 1, b[d + 1] + K)) for d in range(world)]
         for r in range(world):
             if lv > 0 and pb is not None:
@@ -609,8 +656,9 @@ def exchange_model(dims, plans, ext, world, multicover=None, rep_levels=0):
             if multicover and multicover[lv]:
                 add(r, "multicover", 4 * multicover[lv])
             r0, r1 = b[r], b[r + 1]
-            for T in plans[lv][1:]:
-                k = T + 1
+            for k, _ in pass_groups(plans[lv], group):
+                if not k:
+                    continue
                 if r > 0:
                     add(r, "pass_halo", 4 * w * (min(r0 + k, r1) - r0))
                 if r < world - 1:
