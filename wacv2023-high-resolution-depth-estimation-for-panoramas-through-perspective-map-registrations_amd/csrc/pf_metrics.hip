@@ -843,8 +843,10 @@ __global__ __launch_bounds__(64 * (3 + SEQ_NP)) void k_err_seq(MArgs a, int alig
     __shared__ float res[4];
     const int b = blockIdx.x, lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     float* l0 = lds_sq[0];
-    float* l1 = FUSED ? lds_sq[0] : lds_sq[FUSED ? 0 : 1];
+    float* l1 = FUSED ? lds_sq[0] : lds_sq[FUSED ? 0 : 1];  // (the index is valid in both forms)
     float* l2 = FUSED ? lds_sq[0] : lds_pl;
+    // the branches are wave-uniform, and in the FUSED form every wave -- chain or producer --
+    // passes the same 1 + nch workgroup barriers (seq_chain's SharedSrc::sync, seq_producers)
     if (wv == 0) {
         const float r = err_chain<FUSED, true, 0>(T, band, b, l0, force);
         if (lane == 0) res[0] = r;
