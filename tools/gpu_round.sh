@@ -15,6 +15,8 @@
 #   rgb      the RGB warp probe (tools/rgb_probe.py)   -> rgb.log
 #   warppipe k_warp_depth's vector-memory path counters (TA/TD busy and stalls, three --pmc
 #            passes over tools/warp_probe.py)          -> warppipe/summary.txt
+#   jsq      SQ counters of the Jacobi kernels over serial steps (two --pmc passes; occupancy,
+#            VALU issue, waits)                          -> jsq/summary.txt
 #   serials  the serial step per variant: $VARIANTS as for ab -> serial_NAME/levels.txt (one trace
 #            each, in $ROUNDS alternating rounds)
 #   ab       A/B of environment knobs: $VARIANTS = "NAME:ENV=VAL,ENV=VAL NAME2:" run in $ROUNDS
@@ -95,6 +97,17 @@ for s in $STEPS; do
       done
       python3 tools/pmc_summary.py "$OUT/warppipe/p*/*counter_collection.csv" | grep -A10 "k_warp_depth" > $OUT/warppipe/summary.txt
       cat $OUT/warppipe/summary.txt ;;
+    jsq)
+      rm -rf $OUT/jsq; mkdir -p $OUT/jsq; i=0
+      for set in "SQ_WAVES SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_ANY SQ_INSTS_SALU SQ_INSTS_VMEM_RD" \
+                 "GRBM_GUI_ACTIVE SQ_WAIT_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_LDS SQ_ACTIVE_INST_LDS"; do
+        i=$((i + 1))
+        timeout -k 5 -s KILL 120 rocprofv3 --pmc $set -d $OUT/jsq/p$i -o run --output-format csv -- \
+          python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-extra-configs --pipeline 0 > $OUT/jsq/p$i.log 2>&1; rc=$?
+        [ $rc -eq 0 ] || { echo "jsq pass $i rc=$rc"; tail -3 $OUT/jsq/p$i.log; exit $rc; }
+      done
+      python3 tools/pmc_summary.py "$OUT/jsq/p*/*counter_collection.csv" | grep -A14 -E "k_jlag|k_jres" > $OUT/jsq/summary.txt
+      cat $OUT/jsq/summary.txt | head -60 ;;
     ab)
       mkdir -p $OUT/ab
       for r in $(seq 1 ${ROUNDS:-2}); do
