@@ -314,7 +314,7 @@ class NullComm:
 PASS_GROUP = max(1, int(os.environ.get("PF_C5_GROUP", "4")))
 
 
-def pass_groups(plan, group=2):
+def pass_groups(plan, group=None):
     """Per pass i of a row-sharded level: (k, ext).  k > 0: the halo rows exchanged with each
     neighbour before the pass (0: none); ext: the rows the pass computes past each side of the
     band.  A pass of depth T on rows [r0, r1) reads rows [r0 - T - 1, r1 + T + 1) (T sweeps, plus
@@ -323,16 +323,17 @@ def pass_groups(plan, group=2):
     each computes the rows past the band that the rest of its run reads (sum of their T + 1):
     1/G of the exchange rounds for the same bytes, some rows computed twice -- by the rank and by
     its neighbour, bit-identically."""
+    group = max(1, PASS_GROUP if group is None else group)
     out = [(0, 0)] if plan else []
-    for s0 in range(1, len(plan), max(1, group)):
-        run = plan[s0:s0 + max(1, group)]
+    for s0 in range(1, len(plan), group):
+        run = plan[s0:s0 + group]
         need = [T + 1 for T in run]
         for j in range(len(run)):
             out.append((sum(need) if j == 0 else 0, sum(need[j + 1:])))
     return out
 
 
-def halo_rows(plan, group=2):
+def halo_rows(plan, group=None):
     """The rows past its band a rank's passes read or compute on (targets, previous-level rows):
     the largest exchange of pass_groups, and the first pass's T + 1."""
     return max([plan[0] + 1] + [k for k, _ in pass_groups(plan, group)])
