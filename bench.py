@@ -977,7 +977,8 @@ def main():
                        "pipeline": (f"{args.pipeline} fusion lanes: batch k warped, registered "
                                     f"and fused on lane k % {args.pipeline} (own contexts, streams "
                                     f"and buffers; each lane warps its next batch on a second "
-                                    f"stream)" if args.pipeline >= 2 else
+                                    f"stream; Jacobi passes planned for {LANE_SHARE:.2f} of the "
+                                    f"chip)" if args.pipeline >= 2 else
                                     "warp of batch k+1 on a second stream beside the fusion "
                                     "of batch k, from the end of its level-0 sweeps"
                                     if args.pipeline else "off"),
