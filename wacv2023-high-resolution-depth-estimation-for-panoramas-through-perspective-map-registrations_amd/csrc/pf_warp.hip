@@ -1143,7 +1143,11 @@ void launch_warp_depth(hipStream_t s, const TileGeom* geom, int ntiles, const Wa
 // one 12-B store, so a wave writes four 192-B runs of tile rows.  Patches whose box exceeds
 // the LDS slot (near the poles) blend from direct byte gathers of the taps.
 // =============================================================================================
-static constexpr int kNBR = 16;  // panoramas per block
+#ifndef PF_RGB_NB
+// round 6 A/B (profiles/r06/ab/rgb_panoramas_per_block.txt): 8 slower, 32 the same
+#define PF_RGB_NB 16
+#endif
+static constexpr int kNBR = PF_RGB_NB;  // panoramas per block
 
 static inline int wrap_signed(int d, int n)
 {
