@@ -777,7 +777,12 @@ __device__ __forceinline__ float seq_chain(Src& src, long long band, const int (
 // gt and the result chunk by chunk into a shared LDS double buffer (seq_producers) while the
 // chain waves add the previous chunk -- no term planes in HBM (k_seq_terms wrote 2.25 GB of them
 // per C3 batch and the chains re-read 1.53 GB).  Else the chains read k_seq_terms' planes.
-constexpr int SEQ_NP = 4;
+#ifndef PF_SEQ_NP
+// producer waves per block; round 6 A/B on the C3 batch (whole sequential call): 1 -> 8.06,
+// 2 -> 7.32-7.38, 4 -> 7.34-7.40 ms
+#define PF_SEQ_NP 4
+#endif
+constexpr int SEQ_NP = PF_SEQ_NP;
 
 template <bool FUSED>
 __global__ __launch_bounds__(64 * (1 + SEQ_NP)) void k_ls_seq(MArgs a, SeqTerms T, long long band,
